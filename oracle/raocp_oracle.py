@@ -1,0 +1,558 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY.
+
+CPU restatement (vectorised NumPy, fp64) of raocp's Chambolle-Pock inner loop,
+the checker the HIP path is compared against. Only `tests/`,
+`__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg may import this
+module; the product (`raocp-toolbox_amd/raocp`) never does, and it never falls
+back to it.
+
+Parity of this oracle is PINNED against the reference itself: the fixtures in
+`tests/golden/*.npz` were produced by running /root/reference in this container
+(`tests/golden/gen_golden.py`), and `tests/test_oracle_golden.py` checks every
+function below against them (L / L^T, prox_f and its sub-steps, prox_g* and its
+sub-steps, offline P/K/Abar, full CP traces including main.py's 937-iteration
+trace, which also matches the published 4-3-residuals.tex).
+
+All vectors are FLAT in the reference's block order (np.vstack of the block
+lists, cache.py:126-170), placeholders included:
+  primal  = [x_0..x_{n-1} | u_0..u_{m-1} | y_0..y_{m-1} | tau_0..tau_{n-1} | s_0..s_{n-1}]
+  dual    = [eta1 | eta2 | eta3 | eta4 | eta5 | eta6 | eta7 | eta11 | eta12 | eta13 | eta14],
+            n blocks per segment, (1,1) zero placeholders where a block is unused.
+"""
+import numpy as np
+import scipy.linalg
+from scipy.sparse.linalg import LinearOperator, eigs
+
+__all__ = ["OracleProblem"]
+
+
+def _grouped_matvec(mats, gidx, V):
+    """out[r] = mats[gidx[r]] @ V[r] for row-stacked vectors V."""
+    if V.shape[0] == 0:
+        rows = mats[0].shape[0] if len(mats) else 0
+        return np.zeros((0, rows))
+    rows = mats[gidx[0]].shape[0]
+    out = np.empty((V.shape[0], rows))
+    for g in np.unique(gidx):
+        sel = np.flatnonzero(gidx == g)
+        out[sel] = V[sel] @ mats[g].T
+    return out
+
+
+class _Dedup:
+    """Matrix table keyed by object identity (the builder shares objects between nodes)."""
+
+    def __init__(self):
+        self.mats, self._key = [], {}
+
+    def add(self, M):
+        k = id(M)
+        if k not in self._key:
+            self._key[k] = len(self.mats)
+            self.mats.append(np.asarray(M, dtype=float))
+        return self._key[k]
+
+
+def _offsets(sizes):
+    off = np.zeros(len(sizes) + 1, dtype=np.int64)
+    np.cumsum(sizes, out=off[1:])
+    return off
+
+
+def _ranges(starts, lengths):
+    """Concatenation of [s, s+l) for each (s, l)."""
+    lengths = np.asarray(lengths, dtype=np.int64)
+    tot = int(lengths.sum())
+    if tot == 0:
+        return np.zeros(0, dtype=np.int64)
+    rep = np.repeat(np.asarray(starts, dtype=np.int64) - (np.cumsum(lengths) - lengths), lengths)
+    return rep + np.arange(tot, dtype=np.int64)
+
+
+class OracleProblem:
+    """Flat-layout CPU restatement built from a RAOCP spec (duck-typed: only the
+    reference's public accessors are used: raocp_spec.py:54-95, scenario_tree.py:71-154)."""
+
+    def __init__(self, spec):
+        tree = spec.tree
+        self.n = n = int(tree.num_nodes)
+        self.m = m = int(tree.num_nonleaf_nodes)
+        self.nx = nx = spec.state_dynamics_at_node(1).shape[1]
+        self.nu = nu = spec.control_dynamics_at_node(1).shape[1]
+        anc = np.array([tree.ancestor_of(i) for i in range(n)], dtype=np.int64)
+        self.anc = anc
+        self.stage = np.array([tree.stage_of(i) for i in range(n)], dtype=np.int64)
+        nch = np.zeros(m, dtype=np.int64)
+        chs = np.zeros(m, dtype=np.int64)
+        for i in range(m):
+            ch = np.asarray(tree.children_of(i))
+            nch[i] = len(ch)
+            chs[i] = ch[0]
+            assert np.array_equal(ch, np.arange(ch[0], ch[0] + len(ch))), "children must be contiguous"
+        self.nch, self.chs = nch, chs
+        self.rank = np.zeros(n, dtype=np.int64)  # position of j among its siblings
+        for i in range(m):
+            self.rank[chs[i]:chs[i] + nch[i]] = np.arange(nch[i])
+        self.N = int(self.stage.max())
+
+        # ---- per-node matrices (tables + indices)
+        A, B, SQ, SR, SP, GX, GU, GL = (_Dedup() for _ in range(8))
+        self.iA = np.full(n, -1); self.iB = np.full(n, -1)
+        self.iSQ = np.full(n, -1); self.iSR = np.full(n, -1); self.iSP = np.full(n, -1)
+        self.dyn_key = [None] * n
+        for j in range(1, n):
+            self.iA[j] = A.add(spec.state_dynamics_at_node(j))
+            self.iB[j] = B.add(spec.control_dynamics_at_node(j))
+            self.dyn_key[j] = (self.iA[j], self.iB[j])
+            c = spec.nonleaf_cost_at_node(j)
+            self.iSQ[j] = SQ.add(c.sqrt_state_weights)
+            self.iSR[j] = SR.add(c.sqrt_control_weights)
+        for l in range(m, n):
+            self.iSP[l] = SP.add(spec.leaf_cost_at_node(l).sqrt_state_weights)
+        self.A, self.B, self.SQ, self.SR, self.SP = A.mats, B.mats, SQ.mats, SR.mats, SP.mats
+        # risks: b = [p; 0; 1] (risks.py:28-35); alpha for the kernel projection
+        self.cond = np.zeros(n)
+        self.alpha_r = np.zeros(m)
+        self.b_list = []
+        for i in range(m):
+            r = spec.risk_at_node(i)
+            b = np.asarray(r.vector_b, dtype=float).reshape(-1)
+            self.b_list.append(b)
+            self.cond[chs[i]:chs[i] + nch[i]] = b[:nch[i]]
+            self.alpha_r[i] = r.alpha
+        # constraints
+        self.nl_active = np.array([spec.nonleaf_constraint_at_node(i).is_active for i in range(m)], dtype=bool)
+        self.l_active = np.array([spec.leaf_constraint_at_node(l).is_active for l in range(m, n)], dtype=bool)
+        self.nl_cons = [spec.nonleaf_constraint_at_node(i) for i in range(m)]
+        self.l_cons = [spec.leaf_constraint_at_node(l) for l in range(m, n)]
+        self.iGX = np.full(m, -1); self.iGU = np.full(m, -1); self.iGL = np.full(n - m, -1)
+        self.nl_lo = np.zeros((m, nx + nu)); self.nl_hi = np.zeros((m, nx + nu))
+        self.l_lo = np.zeros((n - m, nx)); self.l_hi = np.zeros((n - m, nx))
+        nl_rows = np.ones(m, dtype=np.int64)
+        l_rows = np.ones(n - m, dtype=np.int64)
+        for i in range(m):
+            if self.nl_active[i]:
+                cns = self.nl_cons[i]
+                self.iGX[i] = GX.add(cns.state_matrix)
+                self.iGU[i] = GU.add(cns.control_matrix)
+                nl_rows[i] = cns.state_matrix.shape[0]
+                self.nl_lo[i] = np.asarray(cns.lower, dtype=float).reshape(-1)
+                self.nl_hi[i] = np.asarray(cns.upper, dtype=float).reshape(-1)
+        for k in range(n - m):
+            if self.l_active[k]:
+                cns = self.l_cons[k]
+                self.iGL[k] = GL.add(cns.state_matrix)
+                l_rows[k] = cns.state_matrix.shape[0]
+                self.l_lo[k] = np.asarray(cns.lower, dtype=float).reshape(-1)
+                self.l_hi[k] = np.asarray(cns.upper, dtype=float).reshape(-1)
+        self.GX, self.GU, self.GL = GX.mats, GU.mats, GL.mats
+
+        # ---- flat layout (cache.py:126-170)
+        ysz = 2 * nch + 1
+        self.p_sizes = [np.full(n, nx), np.full(m, nu), ysz, np.ones(n, np.int64), np.ones(n, np.int64)]
+        seg_p = _offsets([int(s.sum()) for s in self.p_sizes])
+        self.X0, self.U0, self.Y0, self.T0, self.S0, self.P = [int(v) for v in seg_p]
+        self.y_off = self.Y0 + _offsets(ysz)[:-1]
+        one = np.ones(n, np.int64)
+        s1 = np.ones(n, np.int64); s1[:m] = ysz
+        s3 = np.full(n, nx); s3[0] = 1
+        s4 = np.full(n, nu); s4[0] = 1
+        s7 = np.ones(n, np.int64); s7[:m] = np.where(self.nl_active, nl_rows, 1)
+        s11 = np.ones(n, np.int64); s11[m:] = nx
+        s14 = np.ones(n, np.int64); s14[m:] = np.where(self.l_active, l_rows, 1)
+        self.d_sizes = [s1, one, s3, s4, one, one, s7, s11, one, one, s14]
+        seg_d = _offsets([int(s.sum()) for s in self.d_sizes])
+        self.D = int(seg_d[-1])
+        self.d_off = [int(seg_d[k]) + _offsets(self.d_sizes[k])[:-1] for k in range(11)]
+        (self.E1, self.E2, self.E3, self.E4, self.E5, self.E6, self.E7,
+         self.E11, self.E12, self.E13, self.E14) = self.d_off
+
+        # index helpers
+        self.kids = np.arange(1, n)                    # nodes carrying eta3..eta6
+        self.leaves = np.arange(m, n)
+        self.x_idx = self.X0 + np.arange(n * nx).reshape(n, nx)
+        self.u_idx = self.U0 + np.arange(m * nu).reshape(m, nu)
+        self.y_all = _ranges(self.y_off, ysz)
+        self.e1_all = _ranges(self.E1[:m], ysz)
+        self.seg_of_y = np.repeat(np.arange(m), ysz)
+        self.ya_idx = np.zeros(n, np.int64); self.yb_idx = np.zeros(n, np.int64)
+        j = self.kids
+        par = anc[j]
+        self.ya_idx[j] = self.y_off[par] + self.rank[j]
+        self.yb_idx[j] = self.y_off[par] + nch[par] + self.rank[j]
+        self.yc_idx = self.y_off + 2 * nch
+        self._offline_done = False
+
+    # ------------------------------------------------------------------------------------------
+    # L and L^T  (operators.py:19-94)
+    # ------------------------------------------------------------------------------------------
+    def _X(self, z):
+        return z[self.X0:self.U0].reshape(self.n, self.nx)
+
+    def _U(self, z):
+        return z[self.U0:self.Y0].reshape(self.m, self.nu)
+
+    def ell(self, z, template=None):
+        """operators.py:19-53. Output slots L does not write keep `template` (zeros by default)."""
+        n, m, nx, nu = self.n, self.m, self.nx, self.nu
+        out = np.zeros(self.D) if template is None else np.array(template, dtype=float, copy=True)
+        X, U = self._X(z), self._U(z)
+        # eta1 = y ; eta2 = s - b'y
+        out[self.e1_all] = z[self.y_all]
+        b_all = np.concatenate(self.b_list) if m else np.zeros(0)
+        by = np.add.reduceat(b_all * z[self.y_all], _offsets(2 * self.nch + 1)[:-1]) if m else np.zeros(0)
+        out[self.E2[:m]] = z[self.S0 + np.arange(m)] - by
+        # eta3..eta6 at child j
+        j = self.kids
+        par = self.anc[j]
+        e3 = _grouped_matvec(self.SQ, self.iSQ[j], X[par])
+        e4 = _grouped_matvec(self.SR, self.iSR[j], U[par])
+        out[(self.E3[j][:, None] + np.arange(nx)).reshape(-1)] = e3.reshape(-1)
+        out[(self.E4[j][:, None] + np.arange(nu)).reshape(-1)] = e4.reshape(-1)
+        half_tau = 0.5 * z[self.T0 + j]
+        out[self.E5[j]] = half_tau
+        out[self.E6[j]] = half_tau
+        # eta7 = Gx x + Gu u (active nonleaf)
+        act = np.flatnonzero(self.nl_active)
+        if act.size:
+            e7 = _grouped_matvec(self.GX, self.iGX[act], X[act]) + _grouped_matvec(self.GU, self.iGU[act], U[act])
+            rows = e7.shape[1]
+            out[(self.E7[act][:, None] + np.arange(rows)).reshape(-1)] = e7.reshape(-1)
+        # leaves
+        lf = self.leaves
+        e11 = _grouped_matvec(self.SP, self.iSP[lf], X[lf])
+        out[(self.E11[lf][:, None] + np.arange(nx)).reshape(-1)] = e11.reshape(-1)
+        half_s = 0.5 * z[self.S0 + lf]
+        out[self.E12[lf]] = half_s
+        out[self.E13[lf]] = half_s
+        lact = np.flatnonzero(self.l_active)
+        if lact.size:
+            e14 = _grouped_matvec(self.GL, self.iGL[lact], X[lf[lact]])
+            rows = e14.shape[1]
+            out[(self.E14[lf[lact]][:, None] + np.arange(rows)).reshape(-1)] = e14.reshape(-1)
+        return out
+
+    def ell_t(self, eta, template=None):
+        """operators.py:55-94. tau_0 is never written (keeps `template`, zero by default)."""
+        n, m, nx, nu = self.n, self.m, self.nx, self.nu
+        out = np.zeros(self.P) if template is None else np.array(template, dtype=float, copy=True)
+        # y = eta1 - b eta2 ; s = eta2 (nonleaf)
+        e2 = eta[self.E2[:m]]
+        b_all = np.concatenate(self.b_list) if m else np.zeros(0)
+        out[self.y_all] = eta[self.e1_all] - b_all * e2[self.seg_of_y]
+        out[self.S0 + np.arange(m)] = e2
+        # x_i, u_i of nonleaf: Gx' eta7 + sum_children sqrtQ_j eta3_j
+        xs = np.zeros((m, nx))
+        us = np.zeros((m, nu))
+        act = np.flatnonzero(self.nl_active)
+        if act.size:
+            rows = len(self.GX[0]) if self.GX else 0
+            e7 = eta[(self.E7[act][:, None] + np.arange(rows)).reshape(-1)].reshape(act.size, rows)
+            xs[act] = _grouped_matvec([g.T for g in self.GX], self.iGX[act], e7)
+            us[act] = _grouped_matvec([g.T for g in self.GU], self.iGU[act], e7)
+        j = self.kids
+        par = self.anc[j]
+        e3 = eta[(self.E3[j][:, None] + np.arange(nx)).reshape(-1)].reshape(-1, nx)
+        e4 = eta[(self.E4[j][:, None] + np.arange(nu)).reshape(-1)].reshape(-1, nu)
+        cx = _grouped_matvec(self.SQ, self.iSQ[j], e3)
+        cu = _grouped_matvec(self.SR, self.iSR[j], e4)
+        for r in range(int(self.nch.max()) if m else 0):  # children in order (sequential sums)
+            sel = np.flatnonzero(self.rank[j] == r)
+            xs[par[sel]] += cx[sel]
+            us[par[sel]] += cu[sel]
+        out[self.x_idx[:m].reshape(-1)] = xs.reshape(-1)
+        out[self.u_idx.reshape(-1)] = us.reshape(-1)
+        out[self.T0 + j] = 0.5 * (eta[self.E5[j]] + eta[self.E6[j]])
+        # leaves: x = sqrtPf eta11 + Gx' eta14 ; s = (eta12 + eta13) / 2
+        lf = self.leaves
+        e11 = eta[(self.E11[lf][:, None] + np.arange(nx)).reshape(-1)].reshape(-1, nx)
+        xl = _grouped_matvec(self.SP, self.iSP[lf], e11)
+        lact = np.flatnonzero(self.l_active)
+        if lact.size:
+            rows = self.GL[0].shape[0]
+            e14 = eta[(self.E14[lf[lact]][:, None] + np.arange(rows)).reshape(-1)].reshape(-1, rows)
+            xl[lact] = xl[lact] + _grouped_matvec([g.T for g in self.GL], self.iGL[lact], e14)
+        out[self.x_idx[m:].reshape(-1)] = xl.reshape(-1)
+        out[self.S0 + lf] = 0.5 * (eta[self.E12[lf]] + eta[self.E13[lf]])
+        return out
+
+    # ------------------------------------------------------------------------------------------
+    # prox of f (cache.py:207-317)
+    # ------------------------------------------------------------------------------------------
+    def offline(self):
+        """cache.py:207-233, with nodes of identical subtree signature sharing one result."""
+        if self._offline_done:
+            return
+        n, m, nx, nu = self.n, self.m, self.nx, self.nu
+        I_x, I_u = np.eye(nx), np.eye(nu)
+        cls = np.zeros(n, dtype=np.int64)      # class 0 = leaf, P = I
+        self.Pc = [I_x]
+        self.Kc, self.choc, self.Rinvc = [None], [None], [None]
+        memo = {}
+        abar_memo = {}
+        self.Abar = []
+        self.iAbar = np.full(n, -1)
+        for i in reversed(range(m)):
+            ch = range(self.chs[i], self.chs[i] + self.nch[i])
+            key = tuple((self.dyn_key[j], int(cls[j])) for j in ch)
+            if key not in memo:
+                sum_r, sum_k = 0, 0
+                for j in ch:
+                    Bj, Aj, Pj = self.B[self.iB[j]], self.A[self.iA[j]], self.Pc[cls[j]]
+                    sum_r = sum_r + Bj.T @ Pj @ Bj
+                    sum_k = sum_k + Bj.T @ Pj @ Aj
+                cho = scipy.linalg.cho_factor(I_u + sum_r)
+                K = scipy.linalg.cho_solve(cho, -sum_k)
+                sum_p = 0
+                for j in ch:
+                    Bj, Aj, Pj = self.B[self.iB[j]], self.A[self.iA[j]], self.Pc[cls[j]]
+                    Ab = Aj + Bj @ K
+                    sum_p = sum_p + Ab.T @ Pj @ Ab
+                memo[key] = len(self.Pc)
+                self.Pc.append(I_x + K.T @ K + sum_p)
+                self.Kc.append(K)
+                self.choc.append(cho)
+                self.Rinvc.append(scipy.linalg.cho_solve(cho, I_u))
+            cls[i] = memo[key]
+            for j in ch:
+                akey = (self.dyn_key[j], int(cls[i]))
+                if akey not in abar_memo:
+                    abar_memo[akey] = len(self.Abar)
+                    self.Abar.append(self.A[self.iA[j]] + self.B[self.iB[j]] @ self.Kc[cls[i]])
+                self.iAbar[j] = abar_memo[akey]
+        self.cls = cls
+        self.KcT = [None] + [K.T for K in self.Kc[1:]]
+        # P_j B_j per (class of j, B of j)
+        pb_memo = {}
+        self.PB = []
+        self.iPB = np.full(n, -1)
+        for j in range(1, n):
+            key = (int(cls[j]), int(self.iB[j]))
+            if key not in pb_memo:
+                pb_memo[key] = len(self.PB)
+                self.PB.append(self.Pc[cls[j]] @ self.B[self.iB[j]])
+            self.iPB[j] = pb_memo[key]
+        self._offline_done = True
+
+    def offline_per_node(self):
+        """(P, K, Abar) expanded per node, in the reference's shapes (cache.py:37-42)."""
+        self.offline()
+        P = np.array([self.Pc[c] for c in self.cls])
+        K = np.array([self.Kc[self.cls[i]] for i in range(self.m)])
+        Ab = np.array([self.Abar[self.iAbar[j]] if j > 0 else np.zeros((self.nx, self.nx)) for j in range(self.n)])
+        return P, K, Ab
+
+    def project_on_dynamics(self, z, x0):
+        """cache.py:259-288: backward sweep over stages N-1..0, forward sweep 0..N-1."""
+        self.offline()
+        n, m, nx, nu = self.n, self.m, self.nx, self.nu
+        out = np.array(z, dtype=float, copy=True)
+        X = out[self.X0:self.U0].reshape(n, nx)
+        U = out[self.U0:self.Y0].reshape(m, nu)
+        q = np.zeros((n, nx))
+        d = np.zeros((m, nu))
+        q[m:] = -X[m:]
+        for t in range(self.N - 1, -1, -1):
+            nodes = np.flatnonzero((self.stage == t) & (np.arange(n) < m))
+            if nodes.size == 0:
+                continue
+            kids = _ranges(self.chs[nodes], self.nch[nodes])
+            par = self.anc[kids]
+            btq = _grouped_matvec([b.T for b in self.B], self.iB[kids], q[kids])
+            sum_d = np.zeros((n, nu))
+            np.add.at(sum_d, par, btq)
+            rhs = U[nodes] - sum_d[nodes]
+            ci = self.cls[nodes]
+            d[nodes] = self._cho_batch(ci, rhs)
+            tj = _grouped_matvec(self.PB, self.iPB[kids], d[par]) + q[kids]
+            at = _grouped_matvec([a.T for a in self.Abar], self.iAbar[kids], tj)
+            sum_q = np.zeros((n, nx))
+            np.add.at(sum_q, par, at)
+            kt = _grouped_matvec(self.KcT, ci, d[nodes] - U[nodes])
+            q[nodes] = -X[nodes] + kt + sum_q[nodes]
+        X[0] = np.asarray(x0, dtype=float).reshape(-1)
+        for t in range(0, self.N):
+            nodes = np.flatnonzero((self.stage == t) & (np.arange(n) < m))
+            if nodes.size == 0:
+                continue
+            ci = self.cls[nodes]
+            U[nodes] = _grouped_matvec(self.Kc, ci, X[nodes]) + d[nodes]
+            kids = _ranges(self.chs[nodes], self.nch[nodes])
+            par = self.anc[kids]
+            X[kids] = _grouped_matvec(self.Abar, self.iAbar[kids], X[par]) + \
+                _grouped_matvec(self.B, self.iB[kids], d[par])
+        return out
+
+    def _cho_batch(self, ci, rhs):
+        out = np.empty_like(rhs)
+        for c in np.unique(ci):
+            sel = np.flatnonzero(ci == c)
+            out[sel] = scipy.linalg.cho_solve(self.choc[c], rhs[sel].T).T
+        return out
+
+    def project_on_kernel(self, z):
+        """cache.py:290-317 in closed form: projection onto ker[E', -I, -I] with
+        E' = [alpha I | -I | 1]; K K' = (alpha^2 + 3) I + 1 1' (Sherman-Morrison)."""
+        out = np.array(z, dtype=float, copy=True)
+        m = self.m
+        if m == 0:
+            return out
+        j = self.kids
+        par = self.anc[j]
+        al = self.alpha_r[par]
+        c = self.nch[par]
+        r = al * z[self.ya_idx[j]] - z[self.yb_idx[j]] + z[self.yc_idx[par]] - z[self.T0 + j] - z[self.S0 + j]
+        sum_r = np.zeros(self.n)
+        np.add.at(sum_r, par, r)
+        a = al * al + 3.0
+        w = (r - sum_r[par] / (a + c)) / a
+        sum_w = np.zeros(self.n)
+        np.add.at(sum_w, par, w)
+        out[self.ya_idx[j]] -= al * w
+        out[self.yb_idx[j]] += w
+        out[self.T0 + j] += w
+        out[self.S0 + j] += w
+        out[self.yc_idx] -= sum_w[:m]
+        return out
+
+    def prox_f(self, z, alpha, x0):
+        """cache.py:248-257."""
+        out = np.array(z, dtype=float, copy=True)
+        out[self.S0] -= alpha
+        out = self.project_on_dynamics(out, x0)
+        return self.project_on_kernel(out)
+
+    # ------------------------------------------------------------------------------------------
+    # prox of g* (cache.py:321-393, cones.py, rectangle.py)
+    # ------------------------------------------------------------------------------------------
+    def modify_dual_add_halves(self, eta, alpha):
+        """cache.py:329-347: eta / alpha, then -1/2 on eta5, eta12 and +1/2 on eta6, eta13
+        (all n blocks of each segment, placeholders included)."""
+        v = np.asarray(eta, dtype=float) / alpha
+        v[self.E5] += -0.5
+        v[self.E6] += 0.5
+        v[self.E12] += -0.5
+        v[self.E13] += 0.5
+        return v
+
+    @staticmethod
+    def _soc(F, t):
+        """SecondOrderCone.project on rows [F | t] (cones.py:113-132)."""
+        nf = np.linalg.norm(F, axis=1)
+        outF = F.copy()
+        outt = t.copy()
+        zero = (nf > t) & (nf <= -t)
+        mid = (nf > t) & ~(nf <= -t)
+        outF[zero] = 0.0
+        outt[zero] = 0.0
+        s = (nf[mid] + t[mid]) / 2
+        outF[mid] = s[:, None] * (F[mid] / nf[mid][:, None])
+        outt[mid] = s
+        return outF, outt
+
+    def project_on_constraints_nonleaf(self, v):
+        """cache.py:349-371."""
+        n, m, nx, nu = self.n, self.m, self.nx, self.nu
+        out = np.array(v, dtype=float, copy=True)
+        # eta1: (R_+^{2c} x {0})^* = R_+^{2c} x R ; eta2: R_+
+        mask_last = np.zeros(self.y_all.size, dtype=bool)
+        mask_last[_offsets(2 * self.nch + 1)[1:] - 1] = True
+        e1 = out[self.e1_all]
+        out[self.e1_all] = np.where(mask_last, e1, np.maximum(e1, 0.0))
+        out[self.E2[:m]] = np.maximum(out[self.E2[:m]], 0.0)
+        j = self.kids
+        F = np.concatenate([out[(self.E3[j][:, None] + np.arange(nx))], out[(self.E4[j][:, None] + np.arange(nu))],
+                            out[self.E5[j]][:, None]], axis=1)
+        F2, t2 = self._soc(F, out[self.E6[j]])
+        out[(self.E3[j][:, None] + np.arange(nx))] = F2[:, :nx]
+        out[(self.E4[j][:, None] + np.arange(nu))] = F2[:, nx:nx + nu]
+        out[self.E5[j]] = F2[:, nx + nu]
+        out[self.E6[j]] = t2
+        act = np.flatnonzero(self.nl_active)
+        if act.size:
+            idx = self.E7[act][:, None] + np.arange(nx + nu)
+            out[idx] = self._clip(out[idx], self.nl_lo[act], self.nl_hi[act])
+        return out
+
+    def project_on_constraints_leaf(self, v):
+        """cache.py:373-390."""
+        m, nx = self.m, self.nx
+        out = np.array(v, dtype=float, copy=True)
+        lf = self.leaves
+        F = np.concatenate([out[self.E11[lf][:, None] + np.arange(nx)], out[self.E12[lf]][:, None]], axis=1)
+        F2, t2 = self._soc(F, out[self.E13[lf]])
+        out[self.E11[lf][:, None] + np.arange(nx)] = F2[:, :nx]
+        out[self.E12[lf]] = F2[:, nx]
+        out[self.E13[lf]] = t2
+        lact = np.flatnonzero(self.l_active)
+        if lact.size:
+            idx = self.E14[lf[lact]][:, None] + np.arange(nx)
+            out[idx] = self._clip(out[idx], self.l_lo[lact], self.l_hi[lact])
+        return out
+
+    @staticmethod
+    def _clip(v, lo, hi):
+        """Rectangle._constrain (rectangle.py:50-59): NaN raises."""
+        if np.isnan(v).any():
+            bad = v[np.isnan(v)][0]
+            raise ValueError(f"Rectangle constraint - '{bad}' value cannot be constrained")
+        return np.where(v <= lo, lo, np.where(v >= hi, hi, v))
+
+    def prox_gconj(self, eta, alpha):
+        """cache.py:321-327 and 392-393: Moreau, eta+ = alpha (v - Pi(v))."""
+        v = self.modify_dual_add_halves(eta, alpha)
+        proj = self.project_on_constraints_leaf(self.project_on_constraints_nonleaf(v))
+        return alpha * (v - proj)
+
+    # ------------------------------------------------------------------------------------------
+    # step size and the CP loop (solver.py:27-171)
+    # ------------------------------------------------------------------------------------------
+    def step_size(self, seed=0):
+        """solver.py:104-118: lambda = max Re eig(L'L) via ARPACK; alpha = 0.999 / lambda."""
+        Lop = LinearOperator(shape=(self.D, self.P), matvec=lambda v: self.ell(np.ravel(v)), dtype=float)
+        LTop = LinearOperator(shape=(self.P, self.D), matvec=lambda v: self.ell_t(np.ravel(v)), dtype=float)
+        v0 = np.random.default_rng(seed).standard_normal(self.P)
+        vals, _ = eigs(LTop * Lop, v0=v0)
+        lam = float(np.real(max(vals)))
+        return lam, 0.999 / lam
+
+    def initial_primal(self, x0):
+        z = np.zeros(self.P)
+        z[self.X0:self.X0 + self.nx] = np.asarray(x0, dtype=float).reshape(-1)
+        return z
+
+    def cp_iteration(self, p, d, alpha, x0):
+        """One pass of solver.py:124-143: returns (z+, eta+, error[3], delta_error[3])."""
+        zh = p - alpha * self.ell_t(d, template=p)
+        zp = self.prox_f(zh, alpha, x0)
+        eh = d + alpha * self.ell(2 * zp - p, template=d)
+        ep = self.prox_gconj(eh, alpha)
+        # solver.py:63-95
+        xi1 = (p - zp) / alpha - self.ell_t(d - ep, template=p)
+        xi2 = (d - ep) / alpha + self.ell(zp - p, template=d)
+        xi0 = xi1 + self.ell_t(xi2, template=p)
+        dl1 = zp - p
+        dl2 = ep - d
+        dl0 = dl1 - self.ell_t(dl2, template=p)
+        err = np.array([np.max(np.abs(v), initial=0.0) for v in (xi0, xi1, xi2)])
+        derr = np.array([np.max(np.abs(v), initial=0.0) for v in (dl0, dl1, dl2)])
+        return zp, ep, err, derr
+
+    def chock(self, x0, max_iters=10, tol=1e-5, alpha=None):
+        """solver.py:97-171. Returns (status, error_cache (k x 3), delta_error_cache, z, eta, alpha)."""
+        if alpha is None:
+            _, alpha = self.step_size()
+        p = self.initial_primal(x0)
+        d = np.zeros(self.D)
+        errs, derrs = [], []
+        k = 0
+        while True:
+            p, d, err, derr = self.cp_iteration(p, d, alpha, x0)
+            errs.append(err)
+            derrs.append(derr)
+            stop = k >= max_iters or max(err) <= tol
+            if stop:
+                break
+            k += 1
+        status = 0 if k < max_iters else 1
+        return status, np.array(errs), np.array(derrs), p, d, alpha
