@@ -1,0 +1,178 @@
+#!/usr/bin/env python3
+"""Benchmark: Chambolle–Pock iterations/s + L-sweep HBM GB/s (BASELINE.json `metric`).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2] [--no-cpu]
+
+One step = one CP iteration (solver.py:124-161: L^T half step, prox_f with the
+dynamics sweeps and AVaR kernel projection, L half step, prox_g*, residuals and
+the stopping test) on the BASELINE configs[1] tree (i.i.d. binary, N = 12:
+8,191 nodes, nx = 20, nu = 8), with the iterate already
+resident in HBM. The loop runs entirely on the device (graph-replayed, on-device
+stopping test); tol = 0 so exactly K iterations run.
+
+Multi-GPU (N > 1, one process per GPU launched by torch.distributed.run): every
+rank solves its own tree instance (an MPC-style batch of independent problems:
+same tree, its own x0), no collective on the data path; the value is the total
+CP iterations/s of the job (weak scaling). Subtree sharding of ONE tree across
+GPUs is SURVEY.md 8(e) and is tracked in DESIGN.md.
+
+The JSON line also carries
+  roofline: the L-sweep kernel (k_ell, operators.py:19-53) timed with HIP events
+            on its own stream, algorithmic bytes = 8 (|P| + |D|) per launch
+            (SURVEY.md 8(d)), against the 8 TB/s HBM3E peak;
+  cpu_baseline: the oracle (vectorised NumPy restatement, oracle/raocp_oracle.py)
+            timed on this host on a bounded sample of the same workload.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "raocp-toolbox_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def algorithmic_bytes(cache):
+    """w (|P| + |D|) over ACTIVE entries: placeholders excluded."""
+    pk = cache.packed
+    n, m, nx, nu = pk.n, pk.m, pk.nx, pk.nu
+    nl = n - m
+    P = n * nx + m * nu + (2 * (n - 1) + m) + (n - 1) + n
+    nl_box = int((pk.i_box_nl >= 0).sum())
+    l_box = int((pk.i_box_l[m:] >= 0).sum())
+    D = (2 * (n - 1) + m) + m + (n - 1) * (nx + nu + 2) + nl_box * (nx + nu) + nl * (nx + 2) + l_box * nx
+    return 8 * P, 8 * D
+
+
+def cpu_baseline(recipe, budget_s=12.0):
+    """Oracle CP iterations on the host (bounded sample of the same workload)."""
+    from oracle.raocp_oracle import OracleProblem
+    from raocp.problems import build_problem
+    try:
+        from threadpoolctl import threadpool_info
+        blas_threads = max([t.get("num_threads", 1) for t in threadpool_info()] or [1])
+    except Exception:
+        blas_threads = 1
+    tree, prob = build_problem(recipe)
+    orc = OracleProblem(prob)
+    orc.offline()
+    lam, alpha = orc.step_size()
+    p = orc.initial_primal(recipe["x0"])
+    d = np.zeros(orc.D)
+    orc.cp_iteration(p, d, alpha, recipe["x0"])  # warm-up
+    k = 0
+    t0 = time.perf_counter()
+    while True:
+        p, d, _, _ = orc.cp_iteration(p, d, alpha, recipe["x0"])
+        k += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": k / dt, "unit": "it/s", "cores": int(blas_threads), "kind": "port",
+            "sample": f"{k} CP iterations of the oracle (NumPy fp64) on the same {orc.n}-node tree in {dt:.1f} s; "
+                      f"elementwise work single-threaded, BLAS up to {blas_threads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--op-reps", type=int, default=2000)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    dist = None
+    import raocp.core as core
+    from raocp.core._native import load_library
+    load_library()  # bind /opt/rocm's HIP runtime before torch (gloo only, no torch.cuda) is imported
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    from raocp.problems import build_problem, recipe_config
+
+    recipe = recipe_config(args.config, seed=0)
+    if world > 1:  # each rank: its own instance (same tree/dynamics, own initial state)
+        recipe["x0"] = np.random.default_rng(1000 + rank).standard_normal(recipe["x0"].size)
+    tree, prob = build_problem(recipe)
+    cache = core.Cache(prob)
+    nat = cache.native
+    lam = nat.step_size()
+    alpha = 0.999 / lam
+
+    # warm-up (W untimed iterations; also captures the CP graph)
+    if args.warmup > 0:
+        nat.cp_bench(recipe["x0"], args.warmup, alpha)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    # The timed region is bracketed by barrier + device synchronize. The synchronize is
+    # hipDeviceSynchronize through libraocp_hip.so: torch's wheel bundles its own
+    # libamdhip64 (ROCm 7.0) with the same soname as /opt/rocm's (7.2) the library is
+    # built against, so torch.cuda must not be initialised in this process.
+    from raocp.core._native import device_synchronize
+    barrier()
+    device_synchronize(nat.device)
+    t0 = time.perf_counter()
+    dev_ms = nat.cp_bench(recipe["x0"], args.steps, alpha)
+    device_synchronize(nat.device)
+    barrier()
+    wall = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t[0])
+    its = world * args.steps / wall
+
+    # L-sweep roofline: k_ell timed with HIP events on the context's stream
+    bP, bD = algorithmic_bytes(cache)
+    ms_l = nat.op_bench(0, args.op_reps)
+    ms_lt = nat.op_bench(1, args.op_reps)
+    gbs_l = (bP + bD) / (ms_l * 1e-3) / 1e9
+    gbs_lt = (bP + bD) / (ms_lt * 1e-3) / 1e9
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+        return
+    out = {
+        "metric": "Chambolle–Pock iterations/sec + L-sweep HBM GB/s, 10k-node tree nₓ=20",
+        "value": its, "unit": "it/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * wall / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"BASELINE configs[1]: i.i.d. binary scenario tree, N=12, {cache.packed.n} nodes, "
+                               f"nx={cache.packed.nx}, nu={cache.packed.nu}, AVaR 0.9, boxes +-1 "
+                               f"(SURVEY.md 8(d) config {args.config})",
+                   "nodes": cache.packed.n, "nx": cache.packed.nx, "nu": cache.packed.nu,
+                   "alpha": alpha, "tol": 0.0,
+                   "parallelism": f"replicas{world}: one independent tree instance per GPU" if world > 1 else "1 GPU"},
+        "device_ms_per_step": dev_ms / args.steps,
+        "roofline": {"bound": "hbm", "kernel": "k_ell (L sweep)", "achieved": gbs_l, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": gbs_l / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": bP + bD, "us_per_launch": ms_l * 1e3,
+                     "note": "working set L2/MALL-resident at this size (SURVEY.md 8(d))"},
+        "l_transpose": {"kernel": "k_ell_t", "achieved": gbs_lt, "unit": "GB/s", "us_per_launch": ms_lt * 1e3},
+    }
+    if not args.no_cpu and world == 1:
+        out["cpu_baseline"] = cpu_baseline(recipe, args.cpu_seconds)
+    print(json.dumps(out))
+    if dist is not None:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

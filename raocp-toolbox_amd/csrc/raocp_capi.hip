@@ -1,0 +1,834 @@
+// raocp_capi.hip — host side of libraocp_hip.so: the C-ABI declared in
+// include/raocp_hip.h. Owns one HIP device context per raocp_ctx: uploads the
+// packed problem, keeps the CP iterate resident in HBM, launches the kernels of
+// raocp_kernels.hip and replays the CP iteration as a captured hipGraph.
+
+#include "raocp_kernels.hip"
+#include "../../include/raocp_hip.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+using raocp::Ctl;
+using raocp::Dev;
+using raocp::kBlock;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                             \
+    do {                                                                                         \
+        hipError_t _e = (expr);                                                                  \
+        if (_e != hipSuccess)                                                                    \
+            return fail(RAOCP_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));       \
+    } while (0)
+
+int cdiv(int a, int b) { return b <= 0 ? 0 : (a + b - 1) / b; }
+
+}  // namespace
+
+struct raocp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    Dev dev{};
+    int n = 0, m = 0, nx = 0, nu = 0, cmax = 0, N = 0;
+    std::vector<int> stage_ptr;  // start id of each stage, size N+2
+    int64_t P = 0, D = 0;
+    // iterate and work buffers
+    double* Z[3] = {nullptr, nullptr, nullptr};
+    double* E[2] = {nullptr, nullptr};
+    double* XI2 = nullptr;
+    double* q = nullptr;
+    double* d = nullptr;
+    double* x0 = nullptr;
+    double** zbuf = nullptr;     // device array {Z0, Z1, Z2}
+    double** ebuf = nullptr;     // device array {E0, E1}
+    double** solo = nullptr;     // device array {cur, cur, cur} for standalone calls
+    Ctl* ctl = nullptr;
+    Ctl* h_ctl = nullptr;        // pinned host mirror
+    double* hist = nullptr;
+    size_t hist_rows = 0;
+    double* cur_z = nullptr;     // the Cache's current primal / dual
+    double* cur_e = nullptr;
+    double* tmpP = nullptr;      // staging for host-pointer calls
+    double* tmpD = nullptr;
+    double* part = nullptr;      // dot-product partials
+    double* scal = nullptr;      // device scalars
+    const int* ph = nullptr;     // dual placeholder offsets
+    int n_ph = 0;
+    bool has_x0 = false;
+    std::vector<double> h_x0;
+    // captured CP iterations
+    hipGraphExec_t graph = nullptr;
+    int graph_iters = 0;
+    std::vector<void*> allocs;
+
+    template <class T>
+    int alloc(T** p, size_t count) {
+        void* v = nullptr;
+        if (count == 0) count = 1;
+        hipError_t e = hipMalloc(&v, count * sizeof(T));
+        if (e != hipSuccess) return fail(RAOCP_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+        allocs.push_back(v);
+        *p = (T*)v;
+        return RAOCP_OK;
+    }
+    template <class T>
+    int upload(const T** dst, const T* src, size_t count) {
+        T* p = nullptr;
+        int rc = alloc(&p, count);
+        if (rc) return rc;
+        if (count) HIPCHK(hipMemcpy(p, src, count * sizeof(T), hipMemcpyHostToDevice));
+        *dst = p;
+        return RAOCP_OK;
+    }
+    template <class T>
+    int upload_vec(const T** dst, const std::vector<T>& v) {
+        return upload(dst, v.data(), v.size());
+    }
+};
+
+namespace {
+
+// row-major table [cnt][rows][cols] -> column-major per matrix: out[k*rows + r] = M[r][k]
+std::vector<double> to_colmajor(const double* src, int cnt, int rows, int cols) {
+    std::vector<double> out((size_t)cnt * rows * cols);
+    for (int t = 0; t < cnt; ++t)
+        for (int r = 0; r < rows; ++r)
+            for (int k = 0; k < cols; ++k)
+                out[(size_t)t * rows * cols + (size_t)k * rows + r] = src[(size_t)t * rows * cols + (size_t)r * cols + k];
+    return out;
+}
+
+std::vector<double> copy_table(const double* src, size_t count) {
+    return std::vector<double>(src, src + count);
+}
+
+struct Launch {
+    int G, per, blocks;
+};
+
+Launch groups(int G, int count) {
+    Launch l;
+    l.G = G;
+    l.per = kBlock / G;
+    l.blocks = cdiv(count, l.per);
+    return l;
+}
+
+int check_group(int G, const char* what) {
+    if (G > kBlock)
+        return fail(RAOCP_ERR_ARG, std::string("group size of ") + what + " (" + std::to_string(G) +
+                                       ") exceeds the 256-lane workgroup; nx/nu/children too large for this build");
+    return RAOCP_OK;
+}
+
+int copy_in(raocp_ctx* c, double* dst, const double* src, size_t count, int flags) {
+    HIPCHK(hipMemcpyAsync(dst, src, count * sizeof(double),
+                          (flags & RAOCP_DEVICE_PTR) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
+    return RAOCP_OK;
+}
+
+int copy_out(raocp_ctx* c, double* dst, const double* src, size_t count, int flags) {
+    HIPCHK(hipMemcpyAsync(dst, src, count * sizeof(double),
+                          (flags & RAOCP_DEVICE_PTR) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
+    if (!(flags & RAOCP_DEVICE_PTR)) HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+// ---- launches (all on c->stream)
+void launch_ell(raocp_ctx* c, const double* z, double* eta) {
+    const Launch a = groups(c->nx + c->nu + 2, c->n - 1);
+    const Launch b = groups(2 * c->cmax + 2 + c->nx + c->nu, c->m);
+    const Launch l = groups(2 * c->nx + 2, c->n - c->m);
+    const int grid = a.blocks + b.blocks + l.blocks;
+    if (grid) raocp::k_ell<<<grid, kBlock, 0, c->stream>>>(c->dev, z, eta, a.blocks, b.blocks);
+}
+
+void launch_ell_t(raocp_ctx* c, const double* eta, double* z) {
+    const Launch a = groups(c->nx + c->nu + 2 * c->cmax + 2 + c->cmax, c->m);
+    const Launch l = groups(c->nx + 1, c->n - c->m);
+    const int grid = a.blocks + l.blocks;
+    if (grid) raocp::k_ell_t<<<grid, kBlock, 0, c->stream>>>(c->dev, eta, z, a.blocks);
+}
+
+// dynamics sweeps on z = zbuf[(k + zsel) % 3] (k from ctl when kptr != null)
+void launch_dynamics(raocp_ctx* c, double* const* zbuf, int zsel, const int* kptr, const Ctl* ctl) {
+    const int G = std::max(c->nx, c->nu);
+    for (int t = c->N - 1; t >= 0; --t) {
+        const int b = c->stage_ptr[t], e = c->stage_ptr[t + 1];
+        const Launch L = groups(G, e - b);
+        if (L.blocks)
+            raocp::k_dyn_back<<<L.blocks, kBlock, 0, c->stream>>>(c->dev, kptr, ctl, zbuf, zsel, c->q, c->d, b, e);
+    }
+    for (int t = 0; t < c->N; ++t) {
+        const int b = c->stage_ptr[t], e = c->stage_ptr[t + 1];
+        const int nkids = c->stage_ptr[t + 2] - c->stage_ptr[t + 1];
+        const Launch U = groups(c->nu, e - b);
+        const Launch X = groups(c->nx, nkids);
+        if (U.blocks + X.blocks)
+            raocp::k_dyn_fwd<<<U.blocks + X.blocks, kBlock, 0, c->stream>>>(c->dev, kptr, ctl, zbuf, zsel, c->d,
+                                                                             c->x0, b, e, U.blocks);
+    }
+}
+
+void launch_cp_primal(raocp_ctx* c, bool full) {
+    const Launch a = groups(c->nx + c->nu + c->cmax + 1, c->m);
+    const Launch l = groups(c->nx, c->n - c->m);
+    const int grid = a.blocks + l.blocks;
+    if (full)
+        raocp::k_cp_primal<true><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->zbuf, c->ebuf, c->XI2, a.blocks);
+    else
+        raocp::k_cp_primal<false><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->zbuf, c->ebuf, c->XI2, a.blocks);
+}
+
+void launch_cp_dual(raocp_ctx* c, bool with_l, double* dsolo, int mode = raocp::kDualAll) {
+    const Launch a = groups(c->nx + c->nu + 2, c->n - 1);
+    const Launch b = groups(2 * c->cmax + 2 + c->nx + c->nu, c->m);
+    const Launch l = groups(2 * c->nx + 2, c->n - c->m);
+    const int grid = a.blocks + b.blocks + l.blocks;
+    if (with_l)
+        raocp::k_cp_dual<true><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->zbuf, c->ebuf, c->XI2, nullptr,
+                                                                a.blocks, b.blocks, raocp::kDualAll);
+    else
+        raocp::k_cp_dual<false><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->zbuf, c->ebuf, c->XI2, dsolo,
+                                                                 a.blocks, b.blocks, mode);
+}
+
+void enqueue_cp_iteration(raocp_ctx* c) {
+    launch_dynamics(c, c->zbuf, 1, &c->ctl->k, c->ctl);
+    launch_cp_dual(c, true, nullptr);
+    launch_cp_primal(c, true);
+    raocp::k_cp_check<<<1, 1, 0, c->stream>>>(c->ctl, c->hist);
+}
+
+int set_solo(raocp_ctx* c, double* cur) {
+    double* h[3] = {cur, cur, cur};
+    HIPCHK(hipMemcpyAsync(c->solo, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
+    return RAOCP_OK;
+}
+
+int set_ctl_alpha(raocp_ctx* c, double alpha) {
+    HIPCHK(hipMemcpyAsync(&c->ctl->alpha, &alpha, sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+int ensure_hist(raocp_ctx* c, size_t rows) {
+    if (rows <= c->hist_rows) return RAOCP_OK;
+    if (c->hist) {
+        (void)hipFree(c->hist);
+        c->allocs.erase(std::remove(c->allocs.begin(), c->allocs.end(), (void*)c->hist), c->allocs.end());
+        c->hist = nullptr;
+    }
+    int rc = c->alloc(&c->hist, rows * 6);
+    if (rc) return rc;
+    c->hist_rows = rows;
+    // the graph references the history buffer
+    if (c->graph) {
+        (void)hipGraphExecDestroy(c->graph);
+        c->graph = nullptr;
+        c->graph_iters = 0;
+    }
+    return RAOCP_OK;
+}
+
+// Reset the iterate to (x0 at node 0, zeros) / 0 and prepare ctl for a CP run.
+int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double alpha) {
+    for (int b = 0; b < 3; ++b) HIPCHK(hipMemsetAsync(c->Z[b], 0, c->P * sizeof(double), c->stream));
+    for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(c->E[b], 0, c->D * sizeof(double), c->stream));
+    HIPCHK(hipMemsetAsync(c->XI2, 0, c->D * sizeof(double), c->stream));
+    HIPCHK(hipMemcpyAsync(c->Z[0] + c->dev.X0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(c->x0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    Ctl h{};
+    h.alpha = alpha;
+    h.k = 0;
+    h.done = 0;
+    h.final_k = -1;
+    h.flags = 0;
+    h.max_iters = max_iters;
+    h.tol = tol;
+    *c->h_ctl = h;
+    HIPCHK(hipMemcpyAsync(c->ctl, c->h_ctl, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
+    launch_cp_primal(c, false);
+    return RAOCP_OK;
+}
+
+int ensure_graph(raocp_ctx* c, int iters) {
+    if (c->graph && c->graph_iters == iters) return RAOCP_OK;
+    if (c->graph) {
+        (void)hipGraphExecDestroy(c->graph);
+        c->graph = nullptr;
+    }
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+    for (int it = 0; it < iters; ++it) enqueue_cp_iteration(c);
+    HIPCHK(hipStreamEndCapture(c->stream, &g));
+    hipError_t e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    if (e != hipSuccess) return fail(RAOCP_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+    c->graph_iters = iters;
+    return RAOCP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* raocp_last_error(void) { return g_err.c_str(); }
+
+int raocp_device_synchronize(int device) {
+    HIPCHK(hipSetDevice(device));
+    HIPCHK(hipDeviceSynchronize());
+    return RAOCP_OK;
+}
+
+int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int device, raocp_ctx** out) {
+    if (!t || !pr || !out) return fail(RAOCP_ERR_ARG, "null argument");
+    *out = nullptr;
+    const int n = t->n, m = t->m, nx = t->nx, nu = t->nu;
+    if (n < 2 || m < 1 || m >= n || nx < 1 || nu < 1) return fail(RAOCP_ERR_ARG, "bad tree sizes");
+    // ---- validate the layout invariants the kernels rely on
+    if (t->anc[0] != -1 || t->stage[0] != 0) return fail(RAOCP_ERR_TREE, "node 0 must be the root");
+    for (int i = 1; i < n; ++i) {
+        if (t->stage[i] < t->stage[i - 1]) return fail(RAOCP_ERR_TREE, "stage must be non-decreasing in node id");
+        if (t->anc[i] < 0 || t->anc[i] >= i) return fail(RAOCP_ERR_TREE, "ancestor must precede its child");
+    }
+    const int N = t->stage[n - 1];
+    int expect = 1, cmax = 0;
+    for (int i = 0; i < m; ++i) {
+        if (t->stage[i] >= N) return fail(RAOCP_ERR_TREE, "nonleaf nodes must be ids 0..m-1");
+        if (t->nch[i] < 1 || t->ch_start[i] != expect)
+            return fail(RAOCP_ERR_TREE, "children must be contiguous id ranges in parent order");
+        for (int k = 0; k < t->nch[i]; ++k)
+            if (t->anc[expect + k] != i || t->stage[expect + k] != t->stage[i] + 1)
+                return fail(RAOCP_ERR_TREE, "child range inconsistent with ancestors/stages");
+        expect += t->nch[i];
+        cmax = std::max(cmax, (int)t->nch[i]);
+    }
+    if (expect != n) return fail(RAOCP_ERR_TREE, "children ranges do not cover nodes 1..n-1");
+    for (int i = m; i < n; ++i)
+        if (t->stage[i] != N) return fail(RAOCP_ERR_TREE, "leaves must all be at the last stage");
+    // group sizes of every kernel must fit one workgroup
+    int rc;
+    if ((rc = check_group(nx + nu + 2, "child block")) || (rc = check_group(2 * cmax + 2 + nx + nu, "nonleaf block")) ||
+        (rc = check_group(2 * nx + 2, "leaf block")) || (rc = check_group(nx + nu + 2 * cmax + 2 + cmax, "L^T nonleaf")) ||
+        (rc = check_group(nx + nu + cmax + 1, "CP primal nonleaf")))
+        return rc;
+
+    HIPCHK(hipSetDevice(device));
+    raocp_ctx* c = new raocp_ctx();
+    c->device = device;
+    c->n = n; c->m = m; c->nx = nx; c->nu = nu; c->cmax = cmax; c->N = N;
+    auto bail = [&](int code) { raocp_ctx_destroy(c); return code; };
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(RAOCP_ERR_HIP, "hipStreamCreate failed"));
+
+    c->stage_ptr.assign(N + 2, n);
+    for (int i = n - 1; i >= 0; --i) c->stage_ptr[t->stage[i]] = i;
+    c->stage_ptr[N + 1] = n;
+
+    // ---- flat layout (cache.py:126-170)
+    Dev& D = c->dev;
+    D.n = n; D.m = m; D.nx = nx; D.nu = nu; D.cmax = cmax;
+    std::vector<int> yrel(m), e7off(m, -1), e14off(n - m, -1), rank(n, 0);
+    int ysum = 0;
+    for (int i = 0; i < m; ++i) {
+        yrel[i] = ysum;
+        ysum += 2 * t->nch[i] + 1;
+        for (int k = 0; k < t->nch[i]; ++k) rank[t->ch_start[i] + k] = k;
+    }
+    int64_t off = 0;
+    D.X0 = (int)off; off += (int64_t)n * nx;
+    D.U0 = (int)off; off += (int64_t)m * nu;
+    D.Y0 = (int)off; off += ysum;
+    D.T0 = (int)off; off += n;
+    D.S0 = (int)off; off += n;
+    c->P = off; D.P = (int)off;
+    off = 0;
+    D.E1 = (int)off; off += ysum + (n - m);
+    D.E2 = (int)off; off += n;
+    D.E3 = (int)off; off += 1 + (int64_t)(n - 1) * nx;
+    D.E4 = (int)off; off += 1 + (int64_t)(n - 1) * nu;
+    D.E5 = (int)off; off += n;
+    D.E6 = (int)off; off += n;
+    D.E7 = (int)off;
+    for (int i = 0; i < n; ++i) {
+        if (i < m && pr->i_box_nl[i] >= 0) { e7off[i] = (int)off; off += nx + nu; }
+        else off += 1;
+    }
+    D.E11 = (int)off; off += m + (int64_t)(n - m) * nx;
+    D.E12 = (int)off; off += n;
+    D.E13 = (int)off; off += n;
+    D.E14 = (int)off;
+    for (int i = 0; i < n; ++i) {
+        if (i >= m && pr->i_box_l[i] >= 0) { e14off[i - m] = (int)off; off += nx; }
+        else off += 1;
+    }
+    c->D = off; D.D = (int)off;
+    // dual placeholders: (1,1) blocks no projection touches; prox_g* maps them to exactly 0
+    std::vector<int> ph;
+    for (int l = m; l < n; ++l) ph.push_back(D.E1 + ysum + (l - m));
+    for (int l = m; l < n; ++l) ph.push_back(D.E2 + l);
+    ph.push_back(D.E3); ph.push_back(D.E4); ph.push_back(D.E5); ph.push_back(D.E6);
+    {
+        int o = D.E7;
+        for (int i = 0; i < n; ++i) {
+            if (i < m && e7off[i] >= 0) o += nx + nu;
+            else ph.push_back(o++);
+        }
+        o = D.E14;
+        for (int i = 0; i < n; ++i) {
+            if (i >= m && e14off[i - m] >= 0) o += nx;
+            else ph.push_back(o++);
+        }
+    }
+    for (int i = 0; i < m; ++i) { ph.push_back(D.E11 + i); ph.push_back(D.E12 + i); ph.push_back(D.E13 + i); }
+    if (c->P >= (int64_t)1 << 31 || c->D >= (int64_t)1 << 31)
+        return bail(fail(RAOCP_ERR_ARG, "flat vectors exceed 2^31 entries (int32 offsets)"));
+
+    // ---- tables
+    std::vector<int> ch_start(t->ch_start, t->ch_start + m), nch(t->nch, t->nch + m), anc(t->anc, t->anc + n);
+    c->n_ph = (int)ph.size();
+    if ((rc = c->upload_vec(&c->ph, ph))) return bail(rc);
+    if ((rc = c->upload_vec(&D.anc, anc)) || (rc = c->upload_vec(&D.ch_start, ch_start)) ||
+        (rc = c->upload_vec(&D.nch, nch)) || (rc = c->upload_vec(&D.rank, rank)) || (rc = c->upload_vec(&D.yrel, yrel)) ||
+        (rc = c->upload_vec(&D.e7off, e7off)) || (rc = c->upload_vec(&D.e14off, e14off)))
+        return bail(rc);
+    if ((rc = c->upload_vec(&D.SQ, to_colmajor(pr->sqrt_q, pr->n_sq, nx, nx))) ||
+        (rc = c->upload_vec(&D.SR, to_colmajor(pr->sqrt_r, pr->n_sr, nu, nu))) ||
+        (rc = c->upload_vec(&D.SP, to_colmajor(pr->sqrt_pf, pr->n_sp, nx, nx))) ||
+        (rc = c->upload(&D.iSQ, pr->i_sq, n)) || (rc = c->upload(&D.iSR, pr->i_sr, n)) ||
+        (rc = c->upload(&D.iSP, pr->i_sp, n)) || (rc = c->upload(&D.alpha_r, pr->alpha_r, m)) ||
+        (rc = c->upload(&D.cond, pr->cond, n)))
+        return bail(rc);
+    const int nbn = std::max(1, pr->n_box_nl), nbl = std::max(1, pr->n_box_l);
+    std::vector<double> lo_nl(nbn * (nx + nu), 0.0), hi_nl(nbn * (nx + nu), 0.0), lo_l(nbl * nx, 0.0), hi_l(nbl * nx, 0.0);
+    if (pr->n_box_nl) {
+        std::copy(pr->box_nl_lo, pr->box_nl_lo + lo_nl.size(), lo_nl.begin());
+        std::copy(pr->box_nl_hi, pr->box_nl_hi + hi_nl.size(), hi_nl.begin());
+    }
+    if (pr->n_box_l) {
+        std::copy(pr->box_l_lo, pr->box_l_lo + lo_l.size(), lo_l.begin());
+        std::copy(pr->box_l_hi, pr->box_l_hi + hi_l.size(), hi_l.begin());
+    }
+    if ((rc = c->upload_vec(&D.blo_nl, lo_nl)) || (rc = c->upload_vec(&D.bhi_nl, hi_nl)) ||
+        (rc = c->upload_vec(&D.blo_l, lo_l)) || (rc = c->upload_vec(&D.bhi_l, hi_l)) ||
+        (rc = c->upload(&D.iBnl, pr->i_box_nl, m)) || (rc = c->upload(&D.iBl, pr->i_box_l, n)))
+        return bail(rc);
+    // dynamics products
+    if ((rc = c->upload_vec(&D.Brm, copy_table(pr->B, (size_t)pr->n_b * nx * nu))) ||
+        (rc = c->upload_vec(&D.Bcm, to_colmajor(pr->B, pr->n_b, nx, nu))) ||
+        (rc = c->upload_vec(&D.Arm, copy_table(pr->Abar, (size_t)pr->n_abar * nx * nx))) ||
+        (rc = c->upload_vec(&D.Acm, to_colmajor(pr->Abar, pr->n_abar, nx, nx))) ||
+        (rc = c->upload_vec(&D.PBcm, to_colmajor(pr->PB, pr->n_pb, nx, nu))) ||
+        (rc = c->upload_vec(&D.Krm, copy_table(pr->K, (size_t)pr->n_k * nu * nx))) ||
+        (rc = c->upload_vec(&D.Kcm, to_colmajor(pr->K, pr->n_k, nu, nx))) ||
+        (rc = c->upload_vec(&D.Rcm, to_colmajor(pr->Rinv, pr->n_k, nu, nu))) ||
+        (rc = c->upload(&D.iB, pr->i_b, n)) || (rc = c->upload(&D.iAbar, pr->i_abar, n)) ||
+        (rc = c->upload(&D.iPB, pr->i_pb, n)) || (rc = c->upload(&D.iK, pr->i_k, m)))
+        return bail(rc);
+
+    // ---- iterate and work buffers
+    for (int b = 0; b < 3; ++b)
+        if ((rc = c->alloc(&c->Z[b], c->P))) return bail(rc);
+    for (int b = 0; b < 2; ++b)
+        if ((rc = c->alloc(&c->E[b], c->D))) return bail(rc);
+    if ((rc = c->alloc(&c->XI2, c->D)) || (rc = c->alloc(&c->q, (size_t)n * nx)) || (rc = c->alloc(&c->d, (size_t)m * nu)) ||
+        (rc = c->alloc(&c->x0, nx)) || (rc = c->alloc(&c->zbuf, 3)) || (rc = c->alloc(&c->ebuf, 2)) ||
+        (rc = c->alloc(&c->solo, 3)) || (rc = c->alloc(&c->ctl, 1)) || (rc = c->alloc(&c->tmpP, c->P)) ||
+        (rc = c->alloc(&c->tmpD, c->D)) || (rc = c->alloc(&c->part, 1024)) || (rc = c->alloc(&c->scal, 8)))
+        return bail(rc);
+    if (hipHostMalloc((void**)&c->h_ctl, sizeof(Ctl), 0) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "hipHostMalloc"));
+    for (int b = 0; b < 3; ++b)
+        if (hipMemset(c->Z[b], 0, c->P * sizeof(double)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
+    for (int b = 0; b < 2; ++b)
+        if (hipMemset(c->E[b], 0, c->D * sizeof(double)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
+    if (hipMemset(c->XI2, 0, c->D * sizeof(double)) != hipSuccess || hipMemset(c->ctl, 0, sizeof(Ctl)) != hipSuccess ||
+        hipMemset(c->q, 0, (size_t)n * nx * sizeof(double)) != hipSuccess ||
+        hipMemset(c->d, 0, (size_t)m * nu * sizeof(double)) != hipSuccess)
+        return bail(fail(RAOCP_ERR_HIP, "memset"));
+    HIPCHK(hipMemcpy(c->zbuf, c->Z, sizeof(c->Z), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->ebuf, c->E, sizeof(c->E), hipMemcpyHostToDevice));
+    c->cur_z = c->Z[0];
+    c->cur_e = c->E[0];
+    if ((rc = ensure_hist(c, 1024))) return bail(rc);
+    *out = c;
+    return RAOCP_OK;
+}
+
+void raocp_ctx_destroy(raocp_ctx* c) {
+    if (!c) return;
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->graph) (void)hipGraphExecDestroy(c->graph);
+    for (void* p : c->allocs) (void)hipFree(p);
+    if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+int raocp_sizes(raocp_ctx* c, int64_t* P, int64_t* D) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    if (P) *P = c->P;
+    if (D) *D = c->D;
+    return RAOCP_OK;
+}
+
+int raocp_ell(raocp_ctx* c, const double* z, double* eta, int flags) {
+    if (!c || !z || !eta) return fail(RAOCP_ERR_ARG, "null argument");
+    int rc;
+    if (flags & RAOCP_DEVICE_PTR) {
+        launch_ell(c, z, eta);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return RAOCP_OK;
+    }
+    if ((rc = copy_in(c, c->tmpP, z, c->P, 0)) || (rc = copy_in(c, c->tmpD, eta, c->D, 0))) return rc;
+    launch_ell(c, c->tmpP, c->tmpD);
+    HIPCHK(hipGetLastError());
+    return copy_out(c, eta, c->tmpD, c->D, 0);
+}
+
+int raocp_ell_t(raocp_ctx* c, const double* eta, double* z, int flags) {
+    if (!c || !z || !eta) return fail(RAOCP_ERR_ARG, "null argument");
+    int rc;
+    if (flags & RAOCP_DEVICE_PTR) {
+        launch_ell_t(c, eta, z);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return RAOCP_OK;
+    }
+    if ((rc = copy_in(c, c->tmpD, eta, c->D, 0)) || (rc = copy_in(c, c->tmpP, z, c->P, 0))) return rc;
+    launch_ell_t(c, c->tmpD, c->tmpP);
+    HIPCHK(hipGetLastError());
+    return copy_out(c, z, c->tmpP, c->P, 0);
+}
+
+int raocp_set_primal(raocp_ctx* c, const double* z, int flags) {
+    if (!c || !z) return fail(RAOCP_ERR_ARG, "null argument");
+    int rc = copy_in(c, c->cur_z, z, c->P, flags);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+int raocp_get_primal(raocp_ctx* c, double* z, int flags) {
+    if (!c || !z) return fail(RAOCP_ERR_ARG, "null argument");
+    return copy_out(c, z, c->cur_z, c->P, flags);
+}
+int raocp_set_dual(raocp_ctx* c, const double* e, int flags) {
+    if (!c || !e) return fail(RAOCP_ERR_ARG, "null argument");
+    int rc = copy_in(c, c->cur_e, e, c->D, flags);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+int raocp_get_dual(raocp_ctx* c, double* e, int flags) {
+    if (!c || !e) return fail(RAOCP_ERR_ARG, "null argument");
+    return copy_out(c, e, c->cur_e, c->D, flags);
+}
+
+int raocp_set_initial_state(raocp_ctx* c, const double* x0) {
+    if (!c || !x0) return fail(RAOCP_ERR_ARG, "null argument");
+    c->h_x0.assign(x0, x0 + c->nx);
+    HIPCHK(hipMemcpy(c->x0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice));
+    c->has_x0 = true;
+    return RAOCP_OK;
+}
+
+int raocp_relax_s0(raocp_ctx* c, double alpha) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    raocp::k_relax_s0<<<1, 1, 0, c->stream>>>(c->dev, c->cur_z, alpha);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+int raocp_project_on_dynamics(raocp_ctx* c) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    if (!c->has_x0) return fail(RAOCP_ERR_STATE, "initial state not cached (call cache_initial_state first)");
+    int rc = set_solo(c, c->cur_z);
+    if (rc) return rc;
+    launch_dynamics(c, c->solo, 0, nullptr, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+int raocp_project_on_kernel(raocp_ctx* c) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    const Launch L = groups(c->cmax + 1, c->m);
+    raocp::k_kernel_proj<<<L.blocks, kBlock, 0, c->stream>>>(c->dev, c->cur_z);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+int raocp_prox_f(raocp_ctx* c, double alpha) {
+    int rc;
+    if ((rc = raocp_relax_s0(c, alpha)) || (rc = raocp_project_on_dynamics(c)) || (rc = raocp_project_on_kernel(c)))
+        return rc;
+    return RAOCP_OK;
+}
+
+int raocp_prox_gconj(raocp_ctx* c, double alpha) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    int rc = set_ctl_alpha(c, alpha);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(&c->ctl->flags, 0, sizeof(int), c->stream));
+    launch_cp_dual(c, false, c->cur_e);
+    if (c->n_ph) raocp::k_zero_idx<<<cdiv(c->n_ph, kBlock), kBlock, 0, c->stream>>>(c->cur_e, c->ph, c->n_ph);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->h_ctl->flags & 1) return fail(RAOCP_ERR_NAN_IN_BOX, "Rectangle constraint - 'nan' value cannot be constrained");
+    return RAOCP_OK;
+}
+
+int raocp_dual_scale(raocp_ctx* c, double alpha) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    raocp::k_div<<<std::min(2048, cdiv((int)c->D, kBlock)), kBlock, 0, c->stream>>>(c->cur_e, alpha, (int)c->D);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+int raocp_dual_add_halves(raocp_ctx* c) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    const Dev& D = c->dev;
+    const int nb = cdiv(c->n, kBlock);
+    raocp::k_add_const<<<nb, kBlock, 0, c->stream>>>(c->cur_e, -0.5, D.E5, D.E6);
+    raocp::k_add_const<<<nb, kBlock, 0, c->stream>>>(c->cur_e, 0.5, D.E6, D.E7);
+    raocp::k_add_const<<<nb, kBlock, 0, c->stream>>>(c->cur_e, -0.5, D.E12, D.E13);
+    raocp::k_add_const<<<nb, kBlock, 0, c->stream>>>(c->cur_e, 0.5, D.E13, D.E14);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+int raocp_dual_project(raocp_ctx* c, int which) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    HIPCHK(hipMemsetAsync(&c->ctl->flags, 0, sizeof(int), c->stream));
+    const int mode = (which & 1 ? raocp::kDualNonleaf : 0) | (which & 2 ? raocp::kDualLeaf : 0);
+    launch_cp_dual(c, false, c->cur_e, mode);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (c->h_ctl->flags & 1) return fail(RAOCP_ERR_NAN_IN_BOX, "Rectangle constraint - 'nan' value cannot be constrained");
+    return RAOCP_OK;
+}
+
+int raocp_dual_moreau(raocp_ctx* c, double alpha, const double* modified) {
+    if (!c || !modified) return fail(RAOCP_ERR_ARG, "null argument");
+    int rc = copy_in(c, c->tmpD, modified, c->D, 0);
+    if (rc) return rc;
+    raocp::k_moreau<<<std::min(2048, cdiv((int)c->D, kBlock)), kBlock, 0, c->stream>>>(c->cur_e, c->tmpD, alpha,
+                                                                                        (int)c->D);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+// ---- step size: Lanczos on L'L with device mat-vecs (replaces ARPACK, solver.py:109-118)
+static double tridiag_max_eig(const std::vector<double>& a, const std::vector<double>& b) {
+    // largest eigenvalue of the symmetric tridiagonal (a diag, b off-diag) by Sturm bisection
+    const int k = (int)a.size();
+    double lo = a[0], hi = a[0];
+    for (int i = 0; i < k; ++i) {
+        const double r = (i > 0 ? std::fabs(b[i - 1]) : 0.0) + (i + 1 < k ? std::fabs(b[i]) : 0.0);
+        lo = std::min(lo, a[i] - r);
+        hi = std::max(hi, a[i] + r);
+    }
+    auto count_greater = [&](double x) {
+        int cnt = 0;
+        double dd = 1.0;
+        for (int i = 0; i < k; ++i) {
+            const double bb = i > 0 ? b[i - 1] * b[i - 1] : 0.0;
+            dd = (a[i] - x) - (i > 0 ? bb / dd : 0.0);
+            if (dd == 0.0) dd = -1e-300;
+            if (dd > 0) ++cnt;
+        }
+        return cnt;  // number of eigenvalues > x
+    };
+    for (int it = 0; it < 200 && hi - lo > 1e-16 * std::max(1.0, std::fabs(hi)); ++it) {
+        const double mid = 0.5 * (lo + hi);
+        if (count_greater(mid) >= 1) lo = mid;
+        else hi = mid;
+    }
+    return 0.5 * (lo + hi);
+}
+
+static int dev_dot(raocp_ctx* c, const double* a, const double* b, int n, double* out) {
+    const int nb = std::min(1024, cdiv(n, kBlock));
+    raocp::k_dot_partial<<<nb, kBlock, 0, c->stream>>>(a, b, n, c->part);
+    raocp::k_dot_final<<<1, kBlock, 0, c->stream>>>(c->part, nb, c->scal);
+    HIPCHK(hipMemcpyAsync(out, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
+    if (!c || !lambda_max) return fail(RAOCP_ERR_ARG, "null argument");
+    if (max_it <= 0) max_it = 300;
+    if (rtol <= 0) rtol = 1e-14;
+    const int P = (int)c->P;
+    max_it = std::min<int64_t>(max_it, c->P);
+    double *v = nullptr, *vprev = nullptr, *w = nullptr, *eta = nullptr;
+    int rc;
+    if ((rc = c->alloc(&v, P)) || (rc = c->alloc(&vprev, P)) || (rc = c->alloc(&w, P)) || (rc = c->alloc(&eta, c->D)))
+        return rc;
+    std::vector<double> h(P);
+    std::mt19937_64 gen(12345);
+    std::normal_distribution<double> nd(0.0, 1.0);
+    for (int i = 0; i < P; ++i) h[i] = nd(gen);
+    h[c->dev.T0] = 0.0;  // tau_0 is outside the range of L'L (the reference's template keeps it 0)
+    HIPCHK(hipMemcpy(v, h.data(), P * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemsetAsync(vprev, 0, P * sizeof(double), c->stream));
+    HIPCHK(hipMemsetAsync(w, 0, P * sizeof(double), c->stream));
+    HIPCHK(hipMemsetAsync(eta, 0, c->D * sizeof(double), c->stream));
+    const int nbv = std::min(2048, cdiv(P, kBlock));
+    double nrm2;
+    if ((rc = dev_dot(c, v, v, P, &nrm2))) return rc;
+    raocp::k_scale_copy<<<nbv, kBlock, 0, c->stream>>>(1.0 / std::sqrt(nrm2), v, v, P);
+    std::vector<double> al, be;
+    double beta = 0.0, lam = 0.0, lam_prev = -1.0;
+    int stable = 0;
+    for (int j = 0; j < max_it; ++j) {
+        launch_ell(c, v, eta);
+        HIPCHK(hipMemsetAsync(w, 0, P * sizeof(double), c->stream));
+        launch_ell_t(c, eta, w);          // w = L'L v (tau_0 = 0)
+        raocp::k_axpby<<<nbv, kBlock, 0, c->stream>>>(-beta, vprev, 1.0, w, P);
+        double a;
+        if ((rc = dev_dot(c, w, v, P, &a))) return rc;
+        raocp::k_axpby<<<nbv, kBlock, 0, c->stream>>>(-a, v, 1.0, w, P);
+        double bb;
+        if ((rc = dev_dot(c, w, w, P, &bb))) return rc;
+        al.push_back(a);
+        lam = tridiag_max_eig(al, be);
+        beta = std::sqrt(bb);
+        if (std::fabs(lam - lam_prev) <= rtol * std::fabs(lam)) {
+            if (++stable >= 3) break;
+        } else {
+            stable = 0;
+        }
+        lam_prev = lam;
+        if (beta <= 1e-300) break;
+        be.push_back(beta);
+        // vprev <- v ; v <- w / beta
+        HIPCHK(hipMemcpyAsync(vprev, v, P * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        raocp::k_scale_copy<<<nbv, kBlock, 0, c->stream>>>(1.0 / beta, w, v, P);
+    }
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    for (double* p : {v, vprev, w, eta}) {
+        (void)hipFree(p);
+        c->allocs.erase(std::remove(c->allocs.begin(), c->allocs.end(), (void*)p), c->allocs.end());
+    }
+    *lambda_max = lam;
+    return RAOCP_OK;
+}
+
+int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, double alpha, int* status, int* iters,
+                 double* err_hist, double* delta_hist) {
+    if (!c || !x0) return fail(RAOCP_ERR_ARG, "null argument");
+    if (max_iters < 0) return fail(RAOCP_ERR_ARG, "max_iters must be >= 0");
+    int rc;
+    if ((rc = ensure_hist(c, (size_t)max_iters + 1))) return rc;
+    if ((rc = raocp_set_initial_state(c, x0))) return rc;
+    if ((rc = cp_init(c, x0, max_iters, tol, alpha))) return rc;
+    const int batch = 16;
+    if ((rc = ensure_graph(c, batch))) return rc;
+    for (;;) {
+        HIPCHK(hipGraphLaunch(c->graph, c->stream));
+        HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (c->h_ctl->done) break;
+    }
+    const int fk = c->h_ctl->final_k;
+    std::vector<double> h((size_t)(fk + 1) * 6);
+    HIPCHK(hipMemcpy(h.data(), c->hist, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int k = 0; k <= fk; ++k)
+        for (int q = 0; q < 3; ++q) {
+            if (err_hist) err_hist[k * 3 + q] = h[(size_t)k * 6 + q];
+            if (delta_hist) delta_hist[k * 3 + q] = h[(size_t)k * 6 + 3 + q];
+        }
+    c->cur_z = c->Z[(fk + 1) % 3];
+    c->cur_e = c->E[(fk + 1) % 2];
+    if (iters) *iters = fk + 1;
+    if (status) *status = fk < max_iters ? 0 : 1;
+    if (c->h_ctl->flags & 1) return fail(RAOCP_ERR_NAN_IN_BOX, "Rectangle constraint - 'nan' value cannot be constrained");
+    return RAOCP_OK;
+}
+
+int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, float* ms) {
+    if (!c || !x0 || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
+    int rc;
+    if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
+    const int batch = 16;
+    if ((rc = ensure_graph(c, batch))) return rc;
+    if ((rc = cp_init(c, x0, iters - 1, 0.0, alpha))) return rc;
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipEventRecord(e0, c->stream));
+    for (int done = 0; done < iters; done += batch) HIPCHK(hipGraphLaunch(c->graph, c->stream));
+    HIPCHK(hipEventRecord(e1, c->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    HIPCHK(hipEventElapsedTime(ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIPCHK(hipMemcpy(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
+    if (c->h_ctl->final_k != iters - 1) return fail(RAOCP_ERR_STATE, "bench did not run the requested iterations");
+    c->cur_z = c->Z[iters % 3];
+    c->cur_e = c->E[iters % 2];
+    return RAOCP_OK;
+}
+
+int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
+    if (!c || reps < 1 || !ms_per_launch) return fail(RAOCP_ERR_ARG, "bad argument");
+    // random inputs (seed 1), resident in HBM
+    std::vector<double> hz(c->P), he(c->D);
+    std::mt19937_64 gen(1);
+    std::normal_distribution<double> nd(0.0, 1.0);
+    for (auto& v : hz) v = nd(gen);
+    for (auto& v : he) v = nd(gen);
+    HIPCHK(hipMemcpy(c->tmpP, hz.data(), c->P * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(c->tmpD, he.data(), c->D * sizeof(double), hipMemcpyHostToDevice));
+    double* outP = c->Z[2];
+    double* outD = c->E[1];
+    // warm-up
+    for (int i = 0; i < 3; ++i) {
+        if (op == 0) launch_ell(c, c->tmpP, outD);
+        else launch_ell_t(c, c->tmpD, outP);
+    }
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipEventRecord(e0, c->stream));
+    for (int i = 0; i < reps; ++i) {
+        if (op == 0) launch_ell(c, c->tmpP, outD);
+        else launch_ell_t(c, c->tmpD, outP);
+    }
+    HIPCHK(hipEventRecord(e1, c->stream));
+    HIPCHK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    HIPCHK(hipGetLastError());
+    *ms_per_launch = ms / reps;
+    return RAOCP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,950 @@
+// raocp_kernels.hip — HIP kernels for gfx950 (MI355X) implementing raocp's
+// Chambolle–Pock inner loop on the reference's flat block layout.
+//
+// Mapping ("lanes over rows"): every kernel processes one kind of tree node
+// ("group type"); a node is handled by a GROUP of G consecutive lanes, lane r of
+// the group producing row r of that node's output blocks. A 256-thread workgroup
+// holds floor(256/G) groups. Rows of one node are contiguous in the flat layout,
+// so stores are coalesced; the node's inputs (parent state, child duals) are read
+// once per lane from L1/L2 as broadcasts, and matrix tables are stored so lane r
+// reads column-contiguous elements. Group reductions (SOC norms, AVaR kernel
+// sums) go through LDS with workgroup barriers.
+//
+// Reference formulas are cited as /root/reference file:line.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace raocp {
+
+typedef unsigned long long u64;
+
+constexpr int kBlock = 256;
+
+struct Ctl {
+    u64 red[6];          // |xi0| |xi1| |xi2| |delta0| |delta1| |delta2| maxima (bit patterns)
+    double alpha;        // CP step size (alpha_1 = alpha_2, solver.py:116-118)
+    int k;               // current CP iteration
+    int done;            // 1 once the stopping test fired
+    int final_k;
+    int flags;           // bit0: NaN reached a box projection
+    int max_iters;
+    int pad;
+    double tol;
+};
+
+// Device-side problem description (all pointers are HBM).
+struct Dev {
+    int n, m, nx, nu, cmax;
+    int X0, U0, Y0, T0, S0, P;
+    int E1, E2, E3, E4, E5, E6, E7, E11, E12, E13, E14, D;
+    const int* anc;
+    const int* ch_start;
+    const int* nch;
+    const int* rank;
+    const int* yrel;     // [m] offset of y_i (and eta1_i) inside its segment
+    const int* e7off;    // [m] absolute offset of eta7_i or -1
+    const int* e14off;   // [n-m] absolute offset of eta14_l or -1
+    // L / L^T weights, column-major: M[k*rows + r] = M_rk
+    const double* SQ; const double* SR; const double* SP;
+    const int* iSQ; const int* iSR; const int* iSP;
+    const double* alpha_r; const double* cond;
+    const double* blo_nl; const double* bhi_nl; const double* blo_l; const double* bhi_l;
+    const int* iBnl; const int* iBl;
+    // dynamics offline products
+    const double* Brm;   // row-major  B[k*nu + c]
+    const double* Bcm;   // col-major  B[c*nx + k]
+    const double* Arm;   // Abar row-major [k*nx + r] = Abar_kr
+    const double* Acm;   // Abar col-major [k*nx + r] = Abar_rk
+    const double* PBcm;  // PB col-major [c*nx + k] = PB_kc
+    const double* Krm;   // K row-major [c*nx + r] = K_cr
+    const double* Kcm;   // K col-major [k*nu + r] = K_rk
+    const double* Rcm;   // Rinv col-major [c*nu + r] = Rinv_rc
+    const int* iB; const int* iAbar; const int* iPB; const int* iK;
+};
+
+__device__ __forceinline__ int e3(const Dev& p, int j) { return p.E3 + 1 + (j - 1) * p.nx; }
+__device__ __forceinline__ int e4(const Dev& p, int j) { return p.E4 + 1 + (j - 1) * p.nu; }
+__device__ __forceinline__ int e11(const Dev& p, int l) { return p.E11 + p.m + (l - p.m) * p.nx; }
+
+__device__ __forceinline__ u64 dbits(double v) { return (u64)__double_as_longlong(v); }
+
+// block-wide max of non-negative doubles, one atomicMax per block
+__device__ void block_max_atomic(double v, u64* dst, double* s_red) {
+    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_red[w] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double b = s_red[0];
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) b = fmax(b, s_red[i]);
+        atomicMax(dst, dbits(b));
+    }
+}
+
+struct GroupIdx {
+    int gl, r, per, node;
+    bool live;
+};
+
+__device__ __forceinline__ GroupIdx group_index(int G, int begin, int end) {
+    GroupIdx g;
+    g.per = blockDim.x / G;
+    g.gl = threadIdx.x / G;
+    g.r = threadIdx.x - g.gl * G;
+    g.node = begin + blockIdx.x * g.per + g.gl;
+    g.live = g.gl < g.per && g.node < end;
+    return g;
+}
+
+// ==============================================================================
+// L (operators.py:19-53): eta <- L z on active slots only.
+// Three node types in one launch, block-uniform branch on blockIdx.x.
+// ==============================================================================
+__global__ void __launch_bounds__(kBlock) k_ell(Dev p, const double* __restrict__ z, double* __restrict__ eta,
+                                                 int nbA, int nbB) {
+    const int nx = p.nx, nu = p.nu;
+    if ((int)blockIdx.x < nbA) {
+        // child blocks j = 1..n-1: eta3 = sqrtQ_j x_anc, eta4 = sqrtR_j u_anc, eta5 = eta6 = tau_j/2
+        GroupIdx g = group_index(nx + nu + 2, 1, p.n);
+        if (!g.live) return;
+        const int j = g.node, a = p.anc[j], r = g.r;
+        if (r < nx) {
+            const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
+            const double* x = z + p.X0 + (size_t)a * nx;
+            double acc = 0.0;
+            for (int k = 0; k < nx; ++k) acc = fma(M[k * nx + r], x[k], acc);
+            eta[e3(p, j) + r] = acc;
+        } else if (r < nx + nu) {
+            const int rr = r - nx;
+            const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
+            const double* u = z + p.U0 + (size_t)a * nu;
+            double acc = 0.0;
+            for (int k = 0; k < nu; ++k) acc = fma(M[k * nu + rr], u[k], acc);
+            eta[e4(p, j) + rr] = acc;
+        } else {
+            const double ht = 0.5 * z[p.T0 + j];
+            eta[(r == nx + nu ? p.E5 : p.E6) + j] = ht;
+        }
+        return;
+    }
+    if ((int)blockIdx.x < nbA + nbB) {
+        // nonleaf i: eta1 = y, eta2 = s - b'y, eta7 = [x; u]
+        const int G = 2 * p.cmax + 2 + nx + nu;
+        const int bid = blockIdx.x - nbA;
+        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+        const int i = bid * per + gl;
+        if (gl >= per || i >= p.m) return;
+        const int c = p.nch[i], cs = p.ch_start[i];
+        const double* y = z + p.Y0 + p.yrel[i];
+        if (r < 2 * c + 1) {
+            eta[p.E1 + p.yrel[i] + r] = y[r];
+        } else if (r == 2 * p.cmax + 1) {
+            double by = 0.0;
+            for (int k = 0; k < c; ++k) by = fma(p.cond[cs + k], y[k], by);
+            for (int k = c; k < 2 * c; ++k) by += 0.0 * y[k];
+            by += y[2 * c];
+            eta[p.E2 + i] = z[p.S0 + i] - by;
+        } else if (r >= 2 * p.cmax + 2) {
+            const int rr = r - (2 * p.cmax + 2);
+            const int o7 = p.e7off[i];
+            if (o7 >= 0) eta[o7 + rr] = rr < nx ? z[p.X0 + (size_t)i * nx + rr] : z[p.U0 + (size_t)i * nu + rr - nx];
+        }
+        return;
+    }
+    {
+        // leaf l: eta11 = sqrtPf x, eta12 = eta13 = s/2, eta14 = x
+        const int G = 2 * nx + 2;
+        const int bid = blockIdx.x - nbA - nbB;
+        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+        const int l = p.m + bid * per + gl;
+        if (gl >= per || l >= p.n) return;
+        const double* x = z + p.X0 + (size_t)l * nx;
+        if (r < nx) {
+            const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
+            double acc = 0.0;
+            for (int k = 0; k < nx; ++k) acc = fma(M[k * nx + r], x[k], acc);
+            eta[e11(p, l) + r] = acc;
+        } else if (r < nx + 2) {
+            eta[(r == nx ? p.E12 : p.E13) + l] = 0.5 * z[p.S0 + l];
+        } else {
+            const int o14 = p.e14off[l - p.m];
+            if (o14 >= 0) eta[o14 + r - nx - 2] = x[r - nx - 2];
+        }
+    }
+}
+
+// ==============================================================================
+// L^T (operators.py:55-94): z <- L^T eta on every slot except tau_0.
+// ==============================================================================
+__global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restrict__ eta, double* __restrict__ z,
+                                                   int nbA) {
+    const int nx = p.nx, nu = p.nu;
+    if ((int)blockIdx.x < nbA) {
+        // nonleaf i: x, u (child sums), y = eta1 - b eta2, s = eta2, tau of the children
+        const int G = nx + nu + (2 * p.cmax + 1) + 1 + p.cmax;
+        GroupIdx g = group_index(G, 0, p.m);
+        if (!g.live) return;
+        const int i = g.node, r = g.r, c = p.nch[i], cs = p.ch_start[i];
+        const int o7 = p.e7off[i];
+        if (r < nx) {
+            double acc = o7 >= 0 ? eta[o7 + r] : 0.0;
+            for (int q = 0; q < c; ++q) {
+                const int j = cs + q;
+                const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
+                const double* e = eta + e3(p, j);
+                double s = 0.0;
+                for (int k = 0; k < nx; ++k) s = fma(M[k * nx + r], e[k], s);
+                acc += s;
+            }
+            z[p.X0 + (size_t)i * nx + r] = acc;
+        } else if (r < nx + nu) {
+            const int rr = r - nx;
+            double acc = o7 >= 0 ? eta[o7 + nx + rr] : 0.0;
+            for (int q = 0; q < c; ++q) {
+                const int j = cs + q;
+                const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
+                const double* e = eta + e4(p, j);
+                double s = 0.0;
+                for (int k = 0; k < nu; ++k) s = fma(M[k * nu + rr], e[k], s);
+                acc += s;
+            }
+            z[p.U0 + (size_t)i * nu + rr] = acc;
+        } else if (r < nx + nu + 2 * p.cmax + 1) {
+            const int k = r - nx - nu;
+            if (k < 2 * c + 1) {
+                const double b = k < c ? p.cond[cs + k] : (k < 2 * c ? 0.0 : 1.0);
+                z[p.Y0 + p.yrel[i] + k] = eta[p.E1 + p.yrel[i] + k] - b * eta[p.E2 + i];
+            }
+        } else if (r == nx + nu + 2 * p.cmax + 1) {
+            z[p.S0 + i] = eta[p.E2 + i];
+        } else {
+            const int q = r - (nx + nu + 2 * p.cmax + 2);
+            if (q < c) {
+                const int j = cs + q;
+                z[p.T0 + j] = 0.5 * (eta[p.E5 + j] + eta[p.E6 + j]);
+            }
+        }
+        return;
+    }
+    {
+        // leaf l: x = sqrtPf eta11 + eta14, s = (eta12 + eta13)/2
+        const int bid = blockIdx.x - nbA;
+        const int G = nx + 1;
+        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+        const int l = p.m + bid * per + gl;
+        if (gl >= per || l >= p.n) return;
+        if (r < nx) {
+            const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
+            const double* e = eta + e11(p, l);
+            double acc = 0.0;
+            for (int k = 0; k < nx; ++k) acc = fma(M[k * nx + r], e[k], acc);
+            const int o14 = p.e14off[l - p.m];
+            if (o14 >= 0) acc += eta[o14 + r];
+            z[p.X0 + (size_t)l * nx + r] = acc;
+        } else {
+            z[p.S0 + l] = 0.5 * (eta[p.E12 + l] + eta[p.E13 + l]);
+        }
+    }
+}
+
+// ==============================================================================
+// Dynamics projection (cache.py:259-288), one launch per stage.
+// Backward: for nonleaf i at stage t (children at t+1; a leaf child has q = -x):
+//   d_i = Rinv_i (u_i - sum_j B_j' q_j)
+//   q_i = -x_i + K_i'(d_i - u_i) + sum_j Abar_j'(P_j B_j d_i + q_j)
+// Forward: u_i = K_i x_i + d_i ; x_j = Abar_j x_i + B_j d_i (x_0 = x0bar).
+// ==============================================================================
+__global__ void __launch_bounds__(kBlock) k_dyn_back(Dev p, const int* __restrict__ kptr, const Ctl* __restrict__ ctl,
+                                                      double* const* zbuf, int zsel, double* __restrict__ qbuf,
+                                                      double* __restrict__ dbuf, int begin, int end) {
+    __shared__ double s_g[kBlock];
+    __shared__ double s_t[kBlock];
+    if (ctl && ctl->done) return;
+    const int kk = kptr ? *kptr : 0;
+    double* z = zbuf[(kk + zsel) % 3];
+    const int nx = p.nx, nu = p.nu;
+    const int G = nx > nu ? nx : nu;
+    const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+    const int i = begin + blockIdx.x * per + gl;
+    const bool live = gl < per && i < end;
+    const int base = gl * G;
+    int c = 0, cs = 0;
+    if (live) { c = p.nch[i]; cs = p.ch_start[i]; }
+    // (1) g = u - sum_j B_j' q_j
+    double g = 0.0;
+    if (live && r < nu) {
+        double sum = 0.0;
+        for (int q = 0; q < c; ++q) {
+            const int j = cs + q;
+            const double* B = p.Brm + (size_t)p.iB[j] * nx * nu;
+            double s = 0.0;
+            if (j >= p.m) {
+                const double* xj = z + p.X0 + (size_t)j * nx;
+                for (int k = 0; k < nx; ++k) s = fma(B[k * nu + r], -xj[k], s);
+            } else {
+                const double* qj = qbuf + (size_t)j * nx;
+                for (int k = 0; k < nx; ++k) s = fma(B[k * nu + r], qj[k], s);
+            }
+            sum += s;
+        }
+        g = z[p.U0 + (size_t)i * nu + r] - sum;
+    }
+    s_g[threadIdx.x] = g;
+    __syncthreads();
+    // (2) d = Rinv g
+    double dr = 0.0;
+    if (live && r < nu) {
+        const double* R = p.Rcm + (size_t)p.iK[i] * nu * nu;
+        for (int cc = 0; cc < nu; ++cc) dr = fma(R[cc * nu + r], s_g[base + cc], dr);
+        dbuf[(size_t)i * nu + r] = dr;
+    }
+    __syncthreads();
+    s_g[threadIdx.x] = dr;  // s_g now holds d
+    __syncthreads();
+    // (3) acc = sum_j Abar_j' (PB_j d + q_j)
+    double acc = 0.0;
+    const int cmax = p.cmax;
+    for (int q = 0; q < cmax; ++q) {
+        const bool has = live && q < c;
+        const int j = cs + q;
+        double t = 0.0;
+        if (has && r < nx) {
+            const double* PB = p.PBcm + (size_t)p.iPB[j] * nx * nu;
+            double s = 0.0;
+            for (int cc = 0; cc < nu; ++cc) s = fma(PB[cc * nx + r], s_g[base + cc], s);
+            const double qv = j >= p.m ? -z[p.X0 + (size_t)j * nx + r] : qbuf[(size_t)j * nx + r];
+            t = s + qv;
+        }
+        s_t[threadIdx.x] = t;
+        __syncthreads();
+        if (has && r < nx) {
+            const double* A = p.Arm + (size_t)p.iAbar[j] * nx * nx;
+            double s = 0.0;
+            for (int k = 0; k < nx; ++k) s = fma(A[k * nx + r], s_t[base + k], s);
+            acc += s;
+        }
+        __syncthreads();
+    }
+    // (4) q_i = -x_i + K'(d - u) + acc
+    if (live && r < nx) {
+        const double* K = p.Krm + (size_t)p.iK[i] * nu * nx;
+        const double* u = z + p.U0 + (size_t)i * nu;
+        double s = 0.0;
+        for (int cc = 0; cc < nu; ++cc) s = fma(K[cc * nx + r], s_g[base + cc] - u[cc], s);
+        qbuf[(size_t)i * nx + r] = (-z[p.X0 + (size_t)i * nx + r] + s) + acc;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_dyn_fwd(Dev p, const int* __restrict__ kptr, const Ctl* __restrict__ ctl,
+                                                     double* const* zbuf, int zsel, const double* __restrict__ dbuf,
+                                                     const double* __restrict__ x0, int pbegin, int pend, int nbU) {
+    if (ctl && ctl->done) return;
+    const int kk = kptr ? *kptr : 0;
+    double* z = zbuf[(kk + zsel) % 3];
+    const int nx = p.nx, nu = p.nu;
+    if ((int)blockIdx.x < nbU) {
+        // u_i = K_i x_i + d_i for parents at this stage
+        const int G = nu;
+        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+        const int i = pbegin + blockIdx.x * per + gl;
+        if (gl >= per || i >= pend) return;
+        const double* x = i == 0 ? x0 : z + p.X0 + (size_t)i * nx;
+        const double* K = p.Kcm + (size_t)p.iK[i] * nu * nx;
+        double s = 0.0;
+        for (int k = 0; k < nx; ++k) s = fma(K[k * nu + r], x[k], s);
+        z[p.U0 + (size_t)i * nu + r] = s + dbuf[(size_t)i * nu + r];
+        if (i == 0) {
+            // x_0 = x0bar (cache.py:282); lanes r < nu cover nx entries in strides
+            for (int k = r; k < nx; k += nu) z[p.X0 + k] = x0[k];
+        }
+        return;
+    }
+    {
+        // children j of the stage: x_j = Abar_j x_i + B_j d_i
+        const int G = nx;
+        const int bid = blockIdx.x - nbU;
+        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+        const int cbegin = p.ch_start[pbegin];
+        const int cend = p.ch_start[pend - 1] + p.nch[pend - 1];
+        const int j = cbegin + bid * per + gl;
+        if (gl >= per || j >= cend) return;
+        const int i = p.anc[j];
+        const double* x = i == 0 ? x0 : z + p.X0 + (size_t)i * nx;
+        const double* A = p.Acm + (size_t)p.iAbar[j] * nx * nx;
+        const double* B = p.Bcm + (size_t)p.iB[j] * nx * nu;
+        const double* d = dbuf + (size_t)i * nu;
+        double s = 0.0;
+        for (int k = 0; k < nx; ++k) s = fma(A[k * nx + r], x[k], s);
+        double s2 = 0.0;
+        for (int cc = 0; cc < nu; ++cc) s2 = fma(B[cc * nx + r], d[cc], s2);
+        z[p.X0 + (size_t)j * nx + r] = s + s2;
+    }
+}
+
+// ==============================================================================
+// AVaR kernel projection of (y_i, tau_children, s_children) (cache.py:290-317),
+// closed form: r_k = alpha y_k - y_{c+k} + y_{2c} - tau_k - s_k,
+// w = (r - 1 sum(r)/(a+c))/a with a = alpha^2 + 3; then
+// y_k -= alpha w_k, y_{c+k} += w_k, y_{2c} -= sum(w), tau_k += w_k, s_k += w_k.
+// Group per nonleaf: cmax lanes (one per child) + 1 lane for y_{2c}.
+// ==============================================================================
+__device__ __forceinline__ void kernel_proj_group(const Dev& p, int i, int c, int cs, int r, bool live, int base,
+                                                  double* s_x, double (&vals)[4], double& y2c) {
+    // vals = {y_k, y_{c+k}, tau_j, s_j} for lane r < c; y2c valid in lane cmax
+    // lanes with r outside [0, cmax] (x/u lanes of the fused kernel) only join the barriers
+    const int cmax = p.cmax;
+    const bool mine = r >= 0 && r <= cmax;
+    const double al = live ? p.alpha_r[i] : 0.0;
+    if (mine && r == cmax) s_x[base + cmax] = y2c;
+    __syncthreads();
+    double rk = 0.0;
+    if (live && r >= 0 && r < c) rk = al * vals[0] - vals[1] + s_x[base + cmax] - vals[2] - vals[3];
+    __syncthreads();
+    if (mine && r < cmax) s_x[base + r] = rk;
+    __syncthreads();
+    double sr = 0.0;
+    if (live) for (int q = 0; q < c; ++q) sr += s_x[base + q];
+    const double a = al * al + 3.0;
+    double w = 0.0;
+    if (live && r >= 0 && r < c) w = (rk - sr / (a + (double)c)) / a;
+    __syncthreads();
+    if (mine && r < cmax) s_x[base + r] = w;
+    __syncthreads();
+    if (live && r >= 0 && r < c) {
+        vals[0] -= al * w;
+        vals[1] += w;
+        vals[2] += w;
+        vals[3] += w;
+    }
+    if (live && r == cmax) {
+        double sw = 0.0;
+        for (int q = 0; q < c; ++q) sw += s_x[base + q];
+        y2c -= sw;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_kernel_proj(Dev p, double* __restrict__ z) {
+    __shared__ double s_x[kBlock];
+    const int G = p.cmax + 1;
+    GroupIdx g = group_index(G, 0, p.m);
+    const int i = g.node, r = g.r, base = g.gl * G;
+    int c = 0, cs = 0;
+    if (g.live) { c = p.nch[i]; cs = p.ch_start[i]; }
+    double vals[4] = {0, 0, 0, 0};
+    double y2c = 0.0;
+    double* y = z + p.Y0 + (g.live ? p.yrel[i] : 0);
+    if (g.live && r < c) {
+        const int j = cs + r;
+        vals[0] = y[r]; vals[1] = y[c + r]; vals[2] = z[p.T0 + j]; vals[3] = z[p.S0 + j];
+    }
+    if (g.live && r == p.cmax) y2c = y[2 * c];
+    kernel_proj_group(p, i, c, cs, r, g.live, base, s_x, vals, y2c);
+    if (g.live && r < c) {
+        const int j = cs + r;
+        y[r] = vals[0]; y[c + r] = vals[1]; z[p.T0 + j] = vals[2]; z[p.S0 + j] = vals[3];
+    }
+    if (g.live && r == p.cmax) y[2 * c] = y2c;
+}
+
+__global__ void k_relax_s0(Dev p, double* z, double alpha) { z[p.S0] -= alpha; }
+
+// ==============================================================================
+// CP primal kernel: z_half = p - alpha L^T(d), s_0 -= alpha, AVaR kernel projection
+// of (y, tau, s) fused (those are final after it); x, u go on to the dynamics sweep.
+// FULL: also finishes the previous iteration's residuals (solver.py:63-95):
+//   w = L^T(d_prev - eta+),  xi1 = (p_prev - z+)/alpha - w,  xi0 = xi1 + L^T xi2,
+//   delta1 = z+ - p_prev,    delta0 = delta1 + w   (== delta1 - L^T(eta+ - d_prev))
+// Buffers rotate with the iteration counter k (read from ctl):
+//   FULL=false (initial): p = Z[k], d = E[k], out -> Z[k+1]
+//   FULL=true (end of k): p_prev = Z[k], z+ = Z[k+1], d_prev = E[k], eta+ = E[k+1],
+//                         out z_half(k+1) -> Z[k+2]
+// Group types: nonleaf i (x rows, u rows, one lane per child for y/tau/s, one lane
+// for y_2c and the root's s_0), leaf l (x rows).
+// ==============================================================================
+struct LtIn {
+    const double* a;   // primary dual
+    const double* b;   // secondary (FULL: d_prev) -> w uses b - a
+    const double* c;   // xi2
+};
+
+template <bool FULL>
+__global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ ctl, double* const* zbuf,
+                                                       double* const* ebuf, const double* __restrict__ xi2,
+                                                       int nbA) {
+    __shared__ double s_x[kBlock];
+    __shared__ double s_red[4][kBlock / 64];
+    if (ctl->done) return;
+    const int kk = ctl->k;
+    const double alpha = ctl->alpha;
+    const double* pz = zbuf[kk % 3];                       // p (FULL: p_prev)
+    const double* zp = FULL ? zbuf[(kk + 1) % 3] : nullptr; // z+ (FULL)
+    double* out = FULL ? zbuf[(kk + 2) % 3] : zbuf[(kk + 1) % 3];
+    const double* dA = FULL ? ebuf[(kk + 1) % 2] : ebuf[kk % 2];   // dual whose L^T makes z_half
+    const double* dP = FULL ? ebuf[kk % 2] : nullptr;               // d_prev
+    const double* src = FULL ? zp : pz;                              // primal the half step starts from
+    const int nx = p.nx, nu = p.nu;
+    double m0 = 0.0, m1 = 0.0, m3 = 0.0, m4 = 0.0;   // |xi0| |xi1| |delta0| |delta1|
+    auto account = [&](int e, double lt_half, double w, double ltxi2) {
+        // e: flat primal index; lt_half = L^T(eta+) (FULL) ; returns nothing
+        (void)lt_half;
+        const double pp = pz[e], zz = zp[e];
+        const double x1 = (pp - zz) / alpha - w;
+        const double x0v = x1 + ltxi2;
+        const double dl1 = zz - pp;
+        const double dl0 = dl1 + w;
+        m0 = fmax(m0, fabs(x0v)); m1 = fmax(m1, fabs(x1)); m3 = fmax(m3, fabs(dl0)); m4 = fmax(m4, fabs(dl1));
+    };
+    if ((int)blockIdx.x < nbA) {
+        const int G = nx + nu + p.cmax + 1;
+        GroupIdx g = group_index(G, 0, p.m);
+        const int i = g.node, r = g.r, base = g.gl * G;
+        int c = 0, cs = 0, o7 = -1;
+        if (g.live) { c = p.nch[i]; cs = p.ch_start[i]; o7 = p.e7off[i]; }
+        if (g.live && r < nx + nu) {
+            // x / u rows: sum over children of sqrtQ_j eta3_j (sqrtR_j eta4_j) + Gamma' eta7
+            const bool isx = r < nx;
+            const int rr = isx ? r : r - nx;
+            const int dim = isx ? nx : nu;
+            double accA = 0.0, accW = 0.0, accC = 0.0;
+            if (o7 >= 0) {
+                const int e = o7 + (isx ? rr : nx + rr);
+                accA = dA[e];
+                if (FULL) { accW = dP[e] - dA[e]; accC = xi2[e]; }
+            }
+            for (int q = 0; q < c; ++q) {
+                const int j = cs + q;
+                const double* M = isx ? p.SQ + (size_t)p.iSQ[j] * nx * nx : p.SR + (size_t)p.iSR[j] * nu * nu;
+                const int eb = isx ? e3(p, j) : e4(p, j);
+                double sA = 0.0, sW = 0.0, sC = 0.0;
+                for (int k = 0; k < dim; ++k) {
+                    const double mk = M[k * dim + rr];
+                    const double va = dA[eb + k];
+                    sA = fma(mk, va, sA);
+                    if (FULL) { sW = fma(mk, dP[eb + k] - va, sW); sC = fma(mk, xi2[eb + k], sC); }
+                }
+                accA += sA;
+                if (FULL) { accW += sW; accC += sC; }
+            }
+            const int e = isx ? p.X0 + i * nx + rr : p.U0 + i * nu + rr;
+            out[e] = src[e] - alpha * accA;
+            if (FULL) account(e, accA, accW, accC);
+        }
+        // AVaR kernel block: lane r - (nx+nu) < cmax -> child; == cmax -> y_2c (and root s_0)
+        const int rk = r - (nx + nu);
+        double vals[4] = {0, 0, 0, 0};
+        double y2c = 0.0;
+        const int yo = g.live ? p.yrel[i] : 0;
+        const double e2A = g.live ? dA[p.E2 + i] : 0.0;
+        double e2W = 0.0, e2C = 0.0;
+        if (FULL && g.live) { e2W = dP[p.E2 + i] - dA[p.E2 + i]; e2C = xi2[p.E2 + i]; }
+        if (g.live && rk >= 0 && rk < c) {
+            const int j = cs + rk;
+            const double b = p.cond[j];
+            // y_k, y_{c+k}: eta1 - b eta2
+            const int ey0 = p.Y0 + yo + rk, ey1 = p.Y0 + yo + c + rk;
+            const int f0 = p.E1 + yo + rk, f1 = p.E1 + yo + c + rk;
+            const double lt0 = dA[f0] - b * e2A, lt1 = dA[f1] - 0.0 * e2A;
+            vals[0] = src[ey0] - alpha * lt0;
+            vals[1] = src[ey1] - alpha * lt1;
+            // tau_j = (eta5 + eta6)/2
+            const double ltt = 0.5 * (dA[p.E5 + j] + dA[p.E6 + j]);
+            vals[2] = src[p.T0 + j] - alpha * ltt;
+            // s_j = eta2_j (nonleaf child) or (eta12 + eta13)/2 (leaf child)
+            const double lts = j < p.m ? dA[p.E2 + j] : 0.5 * (dA[p.E12 + j] + dA[p.E13 + j]);
+            vals[3] = src[p.S0 + j] - alpha * lts;
+            if (FULL) {
+                const double w0 = (dP[f0] - dA[f0]) - b * e2W, c0 = xi2[f0] - b * e2C;
+                const double w1 = (dP[f1] - dA[f1]) - 0.0 * e2W, c1 = xi2[f1] - 0.0 * e2C;
+                const double wt = 0.5 * ((dP[p.E5 + j] - dA[p.E5 + j]) + (dP[p.E6 + j] - dA[p.E6 + j]));
+                const double ct = 0.5 * (xi2[p.E5 + j] + xi2[p.E6 + j]);
+                double ws, cs2;
+                if (j < p.m) { ws = dP[p.E2 + j] - dA[p.E2 + j]; cs2 = xi2[p.E2 + j]; }
+                else {
+                    ws = 0.5 * ((dP[p.E12 + j] - dA[p.E12 + j]) + (dP[p.E13 + j] - dA[p.E13 + j]));
+                    cs2 = 0.5 * (xi2[p.E12 + j] + xi2[p.E13 + j]);
+                }
+                account(ey0, 0, w0, c0);
+                account(ey1, 0, w1, c1);
+                account(p.T0 + j, 0, wt, ct);
+                account(p.S0 + j, 0, ws, cs2);
+            }
+        }
+        if (g.live && rk == p.cmax) {
+            const int f2 = p.E1 + yo + 2 * c, ey2 = p.Y0 + yo + 2 * c;
+            y2c = src[ey2] - alpha * (dA[f2] - 1.0 * e2A);
+            if (FULL) account(ey2, 0, (dP[f2] - dA[f2]) - 1.0 * e2W, xi2[f2] - 1.0 * e2C);
+            if (i == 0) {
+                // root s_0: L^T -> eta2_0 ; then the relaxation prox s_0 -= alpha (cache.py:253-257)
+                out[p.S0] = (src[p.S0] - alpha * e2A) - alpha;
+                if (FULL) account(p.S0, 0, e2W, e2C);
+            }
+        }
+        kernel_proj_group(p, i, c, cs, rk, g.live && rk >= 0, base + nx + nu, s_x, vals, y2c);
+        if (g.live && rk >= 0 && rk < c) {
+            const int j = cs + rk;
+            out[p.Y0 + yo + rk] = vals[0];
+            out[p.Y0 + yo + c + rk] = vals[1];
+            out[p.T0 + j] = vals[2];
+            out[p.S0 + j] = vals[3];
+        }
+        if (g.live && rk == p.cmax) out[p.Y0 + yo + 2 * c] = y2c;
+    } else {
+        // leaf l: x = sqrtPf eta11 + eta14
+        const int G = nx;
+        const int bid = blockIdx.x - nbA;
+        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+        const int l = p.m + bid * per + gl;
+        if (gl < per && l < p.n) {
+            const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
+            const int eb = e11(p, l);
+            double sA = 0.0, sW = 0.0, sC = 0.0;
+            for (int k = 0; k < nx; ++k) {
+                const double mk = M[k * nx + r];
+                const double va = dA[eb + k];
+                sA = fma(mk, va, sA);
+                if (FULL) { sW = fma(mk, dP[eb + k] - va, sW); sC = fma(mk, xi2[eb + k], sC); }
+            }
+            const int o14 = p.e14off[l - p.m];
+            if (o14 >= 0) {
+                sA += dA[o14 + r];
+                if (FULL) { sW += dP[o14 + r] - dA[o14 + r]; sC += xi2[o14 + r]; }
+            }
+            const int e = p.X0 + l * nx + r;
+            out[e] = src[e] - alpha * sA;
+            if (FULL) account(e, sA, sW, sC);
+        }
+    }
+    if (FULL) {
+        block_max_atomic(m0, &ctl->red[0], s_red[0]);
+        block_max_atomic(m1, &ctl->red[1], s_red[1]);
+        block_max_atomic(m3, &ctl->red[3], s_red[2]);
+        block_max_atomic(m4, &ctl->red[4], s_red[3]);
+    }
+}
+
+// ==============================================================================
+// CP dual kernel (solver.py:44-61 + cache.py:321-393 + residual part of 63-95):
+//   a = L(2 z+ - p), b = L(z+ - p), eta_half = d + alpha a,
+//   v = eta_half/alpha -+ 1/2 (eta5, eta12: -1/2; eta6, eta13: +1/2)
+//   eta+ = alpha (v - Pi(v)),   xi2 = (d - eta+)/alpha + b,   delta2 = eta+ - d
+// Pi: eta1 -> [max(0, .) (2c); identity], eta2 -> max(0, .), per child j the SOC on
+// (eta3, eta4, eta5 | eta6), eta7 box, per leaf SOC on (eta11, eta12 | eta13), eta14 box.
+// WITH_L = false is the standalone prox_gconj (Cache.proximal_of_g_conjugate) on `d`
+// in place (eta_half = d).
+// ==============================================================================
+__device__ __forceinline__ double soc_apply(double v, bool is_t, double nf, double t) {
+    // SecondOrderCone.project (cones.py:113-132) for one coordinate of the block
+    if (nf <= t) return v;
+    if (nf <= -t) return 0.0;
+    const double s = (nf + t) / 2.0;
+    return is_t ? s : s * (v / nf);
+}
+
+__device__ __forceinline__ double box_apply(double v, double lo, double hi, Ctl* ctl) {
+    // Rectangle._constrain (rectangle.py:50-59)
+    if (lo <= v && v <= hi) return v;
+    if (v <= lo) return lo;
+    if (v >= hi) return hi;
+    atomicOr(&ctl->flags, 1);
+    return v;
+}
+
+// mode (standalone only): bit0 PROX (scale, halves, Moreau output) else projection output Pi(d);
+// bit1 process the nonleaf part (eta1..eta7, SOC per child); bit2 the leaf part (eta11..eta14).
+enum { kDualProx = 1, kDualNonleaf = 2, kDualLeaf = 4, kDualAll = 7 };
+
+template <bool WITH_L>
+__global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl, double* const* zbuf,
+                                                     double* const* ebuf, double* __restrict__ xi2, double* dsolo,
+                                                     int nbA, int nbB, int mode) {
+    __shared__ double s_x[kBlock];
+    __shared__ double s_red[2][kBlock / 64];
+    if (WITH_L && ctl->done) return;
+    if (!WITH_L) {
+        const bool leafpart = (int)blockIdx.x >= nbA + nbB;
+        if (leafpart && !(mode & kDualLeaf)) return;
+        if (!leafpart && !(mode & kDualNonleaf)) return;
+    }
+    const bool prox = WITH_L || (mode & kDualProx);
+    const int kk = WITH_L ? ctl->k : 0;
+    const double alpha = ctl->alpha;
+    const double* pz = WITH_L ? zbuf[kk % 3] : nullptr;
+    const double* zp = WITH_L ? zbuf[(kk + 1) % 3] : nullptr;
+    const double* d = WITH_L ? ebuf[kk % 2] : dsolo;
+    double* eo = WITH_L ? ebuf[(kk + 1) % 2] : dsolo;
+    const int nx = p.nx, nu = p.nu;
+    double m2 = 0.0, m5 = 0.0;
+    // finalize one dual element given a = L(2z+ - p)[e], b = L(z+ - p)[e], projection result pv of v
+    auto finish = [&](int e, double v, double pv, double b) {
+        const double ep = prox ? alpha * (v - pv) : pv;
+        eo[e] = ep;
+        if (WITH_L) {
+            const double de = d[e];
+            const double x2 = (de - ep) / alpha + b;
+            xi2[e] = x2;
+            m2 = fmax(m2, fabs(x2));
+            m5 = fmax(m5, fabs(ep - de));
+        }
+    };
+    if ((int)blockIdx.x < nbA) {
+        // child block j: rows eta3 (nx), eta4 (nu), eta5, eta6 -> one SOC of dim nx+nu+2
+        const int G = nx + nu + 2;
+        GroupIdx g = group_index(G, 1, p.n);
+        const int j = g.node, r = g.r, base = g.gl * G;
+        double v = 0.0, bb = 0.0;
+        int e = -1;
+        if (g.live) {
+            const int a = p.anc[j];
+            double av = 0.0;
+            if (r < nx) {
+                e = e3(p, j) + r;
+                if (WITH_L) {
+                    const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
+                    const double* xz = zp + p.X0 + (size_t)a * nx;
+                    const double* xp = pz + p.X0 + (size_t)a * nx;
+                    for (int k = 0; k < nx; ++k) {
+                        const double mk = M[k * nx + r];
+                        const double zk = xz[k], pk = xp[k];
+                        av = fma(mk, 2.0 * zk - pk, av);
+                        bb = fma(mk, zk - pk, bb);
+                    }
+                }
+            } else if (r < nx + nu) {
+                const int rr = r - nx;
+                e = e4(p, j) + rr;
+                if (WITH_L) {
+                    const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
+                    const double* uz = zp + p.U0 + (size_t)a * nu;
+                    const double* up = pz + p.U0 + (size_t)a * nu;
+                    for (int k = 0; k < nu; ++k) {
+                        const double mk = M[k * nu + rr];
+                        const double zk = uz[k], pk = up[k];
+                        av = fma(mk, 2.0 * zk - pk, av);
+                        bb = fma(mk, zk - pk, bb);
+                    }
+                }
+            } else {
+                e = (r == nx + nu ? p.E5 : p.E6) + j;
+                if (WITH_L) {
+                    const double zt = zp[p.T0 + j], pt = pz[p.T0 + j];
+                    av = 0.5 * (2.0 * zt - pt);
+                    bb = 0.5 * (zt - pt);
+                }
+            }
+            const double eh = WITH_L ? d[e] + alpha * av : d[e];
+            v = prox ? eh / alpha : eh;
+            if (prox && r == nx + nu) v += -0.5;
+            if (prox && r == nx + nu + 1) v += 0.5;
+        }
+        // ||f||, f = rows 0..G-2, t = row G-1
+        s_x[threadIdx.x] = (g.live && r < G - 1) ? v * v : 0.0;
+        if (g.live && r == G - 1) s_x[threadIdx.x] = v;
+        __syncthreads();
+        if (g.live) {
+            double ss = 0.0;
+            for (int q = 0; q < G - 1; ++q) ss += s_x[base + q];
+            const double nf = sqrt(ss), t = s_x[base + G - 1];
+            finish(e, v, soc_apply(v, r == G - 1, nf, t), bb);
+        }
+    } else if ((int)blockIdx.x < nbA + nbB) {
+        // nonleaf i: eta1 (2c+1), eta2, eta7 (nx+nu)
+        const int G = 2 * p.cmax + 2 + nx + nu;
+        const int bid = blockIdx.x - nbA;
+        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+        const int i = bid * per + gl;
+        if (gl < per && i < p.m) {
+            const int c = p.nch[i], cs = p.ch_start[i];
+            const int yo = p.yrel[i];
+            if (r < 2 * c + 1) {
+                const int e = p.E1 + yo + r;
+                double av = 0.0, bb = 0.0;
+                if (WITH_L) {
+                    const double zy = zp[p.Y0 + yo + r], py = pz[p.Y0 + yo + r];
+                    av = 2.0 * zy - py;
+                    bb = zy - py;
+                }
+                const double v = prox ? (WITH_L ? d[e] + alpha * av : d[e]) / alpha : d[e];
+                const double pv = r < 2 * c ? fmax(v, 0.0) : v;
+                finish(e, v, pv, bb);
+            } else if (r == 2 * p.cmax + 1) {
+                const int e = p.E2 + i;
+                double av = 0.0, bb = 0.0;
+                if (WITH_L) {
+                    const double* yz = zp + p.Y0 + yo;
+                    const double* yp = pz + p.Y0 + yo;
+                    double bya = 0.0, byb = 0.0;
+                    for (int k = 0; k < c; ++k) {
+                        const double cp = p.cond[cs + k];
+                        bya = fma(cp, 2.0 * yz[k] - yp[k], bya);
+                        byb = fma(cp, yz[k] - yp[k], byb);
+                    }
+                    bya += 2.0 * yz[2 * c] - yp[2 * c];
+                    byb += yz[2 * c] - yp[2 * c];
+                    const double zs = zp[p.S0 + i], ps = pz[p.S0 + i];
+                    av = (2.0 * zs - ps) - bya;
+                    bb = (zs - ps) - byb;
+                }
+                const double v = prox ? (WITH_L ? d[e] + alpha * av : d[e]) / alpha : d[e];
+                finish(e, v, fmax(v, 0.0), bb);
+            } else if (r >= 2 * p.cmax + 2) {
+                const int rr = r - (2 * p.cmax + 2);
+                const int o7 = p.e7off[i];
+                if (o7 >= 0) {
+                    const int e = o7 + rr;
+                    double av = 0.0, bb = 0.0;
+                    if (WITH_L) {
+                        const int ez = rr < nx ? p.X0 + i * nx + rr : p.U0 + i * nu + rr - nx;
+                        av = 2.0 * zp[ez] - pz[ez];
+                        bb = zp[ez] - pz[ez];
+                    }
+                    const double v = prox ? (WITH_L ? d[e] + alpha * av : d[e]) / alpha : d[e];
+                    const int bi = p.iBnl[i];
+                    const double pv = box_apply(v, p.blo_nl[(size_t)bi * (nx + nu) + rr],
+                                                p.bhi_nl[(size_t)bi * (nx + nu) + rr], ctl);
+                    finish(e, v, pv, bb);
+                }
+            }
+        }
+    } else {
+        // leaf l: eta11 (nx), eta12, eta13 -> SOC of dim nx+2 ; eta14 (nx) box
+        const int G = 2 * nx + 2;
+        const int bid = blockIdx.x - nbA - nbB;
+        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
+        const int l = p.m + bid * per + gl;
+        const bool live = gl < per && l < p.n;
+        const int base = gl * G;
+        double v = 0.0, bb = 0.0;
+        int e = -1;
+        if (live) {
+            double av = 0.0;
+            if (r < nx) {
+                e = e11(p, l) + r;
+                if (WITH_L) {
+                    const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
+                    const double* xz = zp + p.X0 + (size_t)l * nx;
+                    const double* xp = pz + p.X0 + (size_t)l * nx;
+                    for (int k = 0; k < nx; ++k) {
+                        const double mk = M[k * nx + r];
+                        av = fma(mk, 2.0 * xz[k] - xp[k], av);
+                        bb = fma(mk, xz[k] - xp[k], bb);
+                    }
+                }
+            } else if (r < nx + 2) {
+                e = (r == nx ? p.E12 : p.E13) + l;
+                if (WITH_L) {
+                    const double zs = zp[p.S0 + l], ps = pz[p.S0 + l];
+                    av = 0.5 * (2.0 * zs - ps);
+                    bb = 0.5 * (zs - ps);
+                }
+            } else {
+                const int o14 = p.e14off[l - p.m];
+                if (o14 >= 0) {
+                    const int rr = r - nx - 2;
+                    e = o14 + rr;
+                    if (WITH_L) {
+                        const int ez = p.X0 + l * nx + rr;
+                        av = 2.0 * zp[ez] - pz[ez];
+                        bb = zp[ez] - pz[ez];
+                    }
+                }
+            }
+            if (e >= 0) {
+                v = prox ? (WITH_L ? d[e] + alpha * av : d[e]) / alpha : d[e];
+                if (prox && r == nx) v += -0.5;
+                if (prox && r == nx + 1) v += 0.5;
+            }
+        }
+        s_x[threadIdx.x] = (live && r < nx + 1) ? v * v : 0.0;
+        if (live && r == nx + 1) s_x[threadIdx.x] = v;
+        __syncthreads();
+        if (live && e >= 0) {
+            if (r < nx + 2) {
+                double ss = 0.0;
+                for (int q = 0; q < nx + 1; ++q) ss += s_x[base + q];
+                finish(e, v, soc_apply(v, r == nx + 1, sqrt(ss), s_x[base + nx + 1]), bb);
+            } else {
+                const int rr = r - nx - 2;
+                const int bi = p.iBl[l];
+                finish(e, v, box_apply(v, p.blo_l[(size_t)bi * nx + rr], p.bhi_l[(size_t)bi * nx + rr], ctl), bb);
+            }
+        }
+    }
+    if (WITH_L) {
+        block_max_atomic(m2, &ctl->red[2], s_red[0]);
+        block_max_atomic(m5, &ctl->red[5], s_red[1]);
+    }
+}
+
+// ---- element-wise dual sub-steps of prox_g* (cache.py:329-347, 392-393)
+__global__ void k_div(double* __restrict__ x, double a, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] = x[i] / a;
+}
+__global__ void k_add_const(double* __restrict__ x, double c, int begin, int end) {
+    for (int i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += gridDim.x * blockDim.x) x[i] = x[i] + c;
+}
+__global__ void k_moreau(double* __restrict__ x, const double* __restrict__ vhat, double a, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[i] = a * (vhat[i] - x[i]);
+}
+__global__ void k_zero_idx(double* __restrict__ x, const int* __restrict__ idx, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[idx[i]] = 0.0;
+}
+
+// end of iteration: record residuals, stopping test (solver.py:137-161)
+__global__ void k_cp_check(Ctl* ctl, double* hist) {
+    if (ctl->done) return;
+    const int k = ctl->k;
+    double e[6];
+    for (int q = 0; q < 6; ++q) {
+        e[q] = __longlong_as_double((long long)ctl->red[q]);
+        hist[(size_t)k * 6 + q] = e[q];
+        ctl->red[q] = 0ull;
+    }
+    const double err = fmax(fmax(e[0], e[1]), e[2]);
+    if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
+        ctl->done = 1;
+        ctl->final_k = k;
+    } else {
+        ctl->k = k + 1;
+    }
+}
+
+// ---- vector helpers for Lanczos (step size)
+__global__ void k_dot_partial(const double* __restrict__ a, const double* __restrict__ b, int n, double* part) {
+    __shared__ double s[kBlock / 64];
+    double acc = 0.0;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) acc = fma(a[i], b[i], acc);
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += s[w];
+        part[blockIdx.x] = t;
+    }
+}
+
+__global__ void k_dot_final(const double* part, int nb, double* out) {
+    __shared__ double s[kBlock];
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < nb; i += blockDim.x) acc += part[i];
+    s[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) s[threadIdx.x] += s[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = s[0];
+}
+
+// y = a*x + b*y
+__global__ void k_axpby(double a, const double* __restrict__ x, double b, double* __restrict__ y, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = a * x[i] + b * y[i];
+}
+
+__global__ void k_scale_copy(double s, const double* __restrict__ x, double* __restrict__ y, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = s * x[i];
+}
+
+}  // namespace raocp

@@ -1,0 +1,228 @@
+"""GPU parity: the HIP path (through the C-ABI, via the drop-in classes) against the
+golden fixtures produced by the reference (tests/golden/gen_golden.py) and against
+the oracle at sizes the oracle finishes in seconds.
+
+Tolerances: fp64 everywhere. Single operator applications 1e-12 relative (only the
+summation order differs from numpy/BLAS); CP residual traces 1e-8 relative per
+entry (BASELINE.json north_star: "within 1e-8 relative").
+"""
+import numpy as np
+import pytest
+
+import raocp.core as core
+from raocp.problems import build_problem, recipe_config
+from helpers import problem_from_golden, rel_err, trace_rel_err
+
+pytestmark = pytest.mark.gpu
+
+OPS = ["main", "ops2x2", "bin6", "c1n5"]
+PROX = ["main", "bin6", "cache3", "c1n5"]
+
+
+@pytest.fixture(scope="module")
+def ops_kat(golden):
+    return golden("ops_kat")
+
+
+@pytest.fixture(scope="module")
+def prox_kat(golden):
+    return golden("prox_kat")
+
+
+def _cache(z, name):
+    r, tree, prob = problem_from_golden(z, name)
+    return r, core.Cache(prob)
+
+
+@pytest.mark.parametrize("name", OPS)
+def test_ell_and_transpose_match_reference(ops_kat, name):
+    z = ops_kat
+    r, cache = _cache(z, name)
+    op = core.Operator(cache)
+    assert cache.primal_size == z[f"{name}/ops_z"].size and cache.dual_size == z[f"{name}/ops_eta"].size
+    lz = op.linop_ell(z[f"{name}/ops_z"].reshape(-1, 1)).reshape(-1)
+    assert rel_err(lz, z[f"{name}/ops_Lz"]) <= 1e-12
+    lte = op.linop_ell_transpose(z[f"{name}/ops_eta"].reshape(-1, 1)).reshape(-1)
+    assert rel_err(lte, z[f"{name}/ops_LTeta"]) <= 1e-12
+
+
+@pytest.mark.parametrize("name", OPS)
+def test_block_api_keeps_unwritten_template_slots(ops_kat, name):
+    z = ops_kat
+    r, cache = _cache(z, name)
+    op = core.Operator(cache)
+    prim = cache._blocks_p(z[f"{name}/ops_z"])
+    out_d = cache._blocks_d(z[f"{name}/ops_tmpl_dual"])
+    op.ell(prim, out_d)
+    assert rel_err(np.concatenate([b.ravel() for b in out_d]), z[f"{name}/ops_ell_out"]) <= 1e-12
+    dual = cache._blocks_d(z[f"{name}/ops_eta"])
+    out_p = cache._blocks_p(z[f"{name}/ops_tmpl_primal"])
+    op.ell_transpose(dual, out_p)
+    assert rel_err(np.concatenate([b.ravel() for b in out_p]), z[f"{name}/ops_ellT_out"]) <= 1e-12
+
+
+@pytest.mark.parametrize("name", OPS)
+def test_adjoint_identity(ops_kat, name):
+    # tests/test_operators.py:101-116 / 323-335: <z, L'eta> = <Lz, eta>
+    z = ops_kat
+    r, cache = _cache(z, name)
+    rng = np.random.default_rng(7)
+    for _ in range(3):
+        zz = rng.standard_normal(cache.primal_size)
+        ee = rng.standard_normal(cache.dual_size)
+        a = zz @ cache.native.ell_t(ee)
+        b = cache.native.ell(zz) @ ee
+        assert abs(a - b) <= 1e-10 * max(1.0, abs(a))
+
+
+@pytest.mark.parametrize("name", PROX)
+def test_prox_f_and_steps_match_reference(prox_kat, name):
+    z = prox_kat
+    r, cache = _cache(z, name)
+    alpha = float(z[f"{name}/prox_alpha"])
+    zin = z[f"{name}/prox_z"]
+    cache.cache_initial_state(r["x0"].reshape(-1, 1))
+    for op, key in (("dyn", "prox_dyn"), ("ker", "prox_kernel"), ("f", "prox_f")):
+        cache.set_primal_flat(zin)
+        if op == "dyn":
+            cache.project_on_dynamics()
+        elif op == "ker":
+            cache.project_on_kernel()
+        else:
+            cache.proximal_of_f(alpha)
+        got = cache.get_primal_flat()
+        assert rel_err(got, z[f"{name}/{key}"]) <= 1e-12, op
+
+
+@pytest.mark.parametrize("name", PROX)
+def test_prox_gconj_and_steps_match_reference(prox_kat, name):
+    z = prox_kat
+    r, cache = _cache(z, name)
+    alpha = float(z[f"{name}/prox_alpha"])
+    ein = z[f"{name}/prox_eta"]
+    cache.set_dual_flat(ein)
+    cache.proximal_of_g_conjugate(alpha)
+    assert rel_err(cache.get_dual_flat(), z[f"{name}/prox_gconj"]) <= 1e-12
+    cache.set_dual_flat(ein)
+    cache.project_on_constraints_nonleaf()
+    assert rel_err(cache.get_dual_flat(), z[f"{name}/prox_proj_nonleaf"]) <= 1e-12
+    cache.set_dual_flat(ein)
+    cache.project_on_constraints_leaf()
+    assert rel_err(cache.get_dual_flat(), z[f"{name}/prox_proj_leaf"]) <= 1e-12
+    cache.set_dual_flat(ein)
+    cache.modify_dual(alpha)
+    cache.add_halves()
+    assert rel_err(cache.get_dual_flat(), z[f"{name}/prox_modify_halves"]) <= 1e-15
+
+
+def _run_chock(z, name, pin):
+    r, tree, prob = problem_from_golden(z, name)
+    solver = core.Solver(problem_spec=prob)
+    alpha = float(z[f"{name}/cp_alpha"]) if pin else None
+    status = solver.chock(initial_state=r["x0"].reshape(-1, 1), max_iters=int(z[f"{name}/cp_max_iters"]),
+                          tol=float(z[f"{name}/cp_tol"]), step_size=alpha)
+    return solver, status
+
+
+@pytest.mark.parametrize("pin", [True, False])
+def test_main_py_trace(golden, pin):
+    """main.py end to end: 937 iterations, status 0, residual trace vs the reference's
+    (which itself matches the published 4-3-residuals.tex to 3.4e-12)."""
+    z = golden("main_trace")
+    solver, status = _run_chock(z, "main", pin)
+    assert status == int(z["main/cp_status"]) == 0
+    err = solver.error_cache
+    assert err.shape == z["main/cp_error"].shape == (937, 3)
+    assert trace_rel_err(err, z["main/cp_error"]) <= 1e-8
+    assert trace_rel_err(solver.delta_error_cache, z["main/cp_delta_error"]) <= 1e-8
+    assert trace_rel_err(err, z["main/tex_trace"]) <= 1e-8
+    zf = solver.cache.get_primal_flat()
+    ef = solver.cache.get_dual_flat()
+    assert rel_err(zf, z["main/cp_z"]) <= 1e-9 and rel_err(ef, z["main/cp_eta"]) <= 1e-9
+    if not pin:
+        assert abs(solver.step_size - float(z["main/cp_alpha"])) <= 1e-12 * float(z["main/cp_alpha"])
+
+
+@pytest.mark.parametrize("name", ["bin6", "c1n5", "ops2x2"])
+def test_small_trajectories(golden, name):
+    z = golden("traj_small")
+    solver, status = _run_chock(z, name, True)
+    assert status == int(z[f"{name}/cp_status"])
+    assert trace_rel_err(solver.error_cache, z[f"{name}/cp_error"]) <= 1e-8
+    assert trace_rel_err(solver.delta_error_cache, z[f"{name}/cp_delta_error"]) <= 1e-8
+    assert rel_err(solver.cache.get_primal_flat(), z[f"{name}/cp_z"]) <= 1e-9
+
+
+def test_step_size_matches_arpack(golden):
+    for f, names in (("main_trace", ["main"]), ("traj_small", ["bin6", "c1n5", "ops2x2"])):
+        z = golden(f)
+        for name in names:
+            r, tree, prob = problem_from_golden(z, name)
+            lam = core.Cache(prob).native.step_size()
+            assert abs(lam - float(z[f"{name}/cp_lambda"])) <= 1e-11 * lam, name
+
+
+def test_single_iteration_quirks(golden):
+    # max_iters=0 runs one iteration and returns 1; the error cache is 1-D (solver.py:148-153)
+    z = golden("main_trace")
+    r, tree, prob = problem_from_golden(z, "main")
+    s = core.Solver(problem_spec=prob)
+    assert s.chock(r["x0"].reshape(-1, 1), max_iters=0, tol=1e-3, step_size=float(z["main/cp_alpha"])) == 1
+    assert s.error_cache.shape == (3,)
+    assert trace_rel_err(s.error_cache, z["main/cp_error"][0]) <= 1e-10
+    # tol met exactly at k == max_iters returns 1
+    s2 = core.Solver(problem_spec=prob)
+    assert s2.chock(r["x0"].reshape(-1, 1), max_iters=936, tol=1e-3, step_size=float(z["main/cp_alpha"])) == 1
+    assert s2.error_cache.shape == (937, 3)
+
+
+def test_nan_in_box_raises(golden):
+    z = golden("prox_kat")
+    r, cache = _cache(z, "main")
+    e = z["main/prox_eta"].copy()
+    e[-1] = np.nan  # last slot is an eta14 entry (leaf box)
+    cache.set_dual_flat(e)
+    with pytest.raises(ValueError):
+        cache.project_on_constraints_leaf()
+
+
+# ---------------------------------------------------------------------------------------
+# the benchmark configuration (BASELINE configs[1]: 8,191 nodes, nx=20, nu=8) vs the oracle
+# ---------------------------------------------------------------------------------------
+@pytest.fixture(scope="module")
+def c2():
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    return r, prob, core.Cache(prob), OracleProblem(prob)
+
+
+def test_c2_operators_vs_oracle(c2):
+    r, prob, cache, orc = c2
+    rng = np.random.default_rng(11)
+    zz = rng.standard_normal(cache.primal_size)
+    ee = rng.standard_normal(cache.dual_size)
+    assert rel_err(cache.native.ell(zz), orc.ell(zz)) <= 1e-12
+    assert rel_err(cache.native.ell_t(ee), orc.ell_t(ee)) <= 1e-12
+    cache.cache_initial_state(r["x0"])
+    cache.set_primal_flat(zz)
+    cache.proximal_of_f(0.3)
+    assert rel_err(cache.get_primal_flat(), orc.prox_f(zz, 0.3, r["x0"])) <= 1e-11
+    cache.set_dual_flat(ee)
+    cache.proximal_of_g_conjugate(0.3)
+    assert rel_err(cache.get_dual_flat(), orc.prox_gconj(ee, 0.3)) <= 1e-12
+
+
+def test_c2_cp_trace_vs_oracle(c2):
+    r, prob, cache, orc = c2
+    lam = cache.native.step_size()
+    lam_o, _ = orc.step_size()
+    assert abs(lam - lam_o) <= 1e-11 * lam
+    alpha = 0.999 / lam
+    status, err, derr = cache.native.cp_run(r["x0"], 19, 0.0, alpha)
+    st_o, err_o, derr_o, z_o, e_o, _ = orc.chock(r["x0"], 19, 0.0, alpha=alpha)
+    assert status == st_o == 1 and err.shape == (20, 3)
+    assert trace_rel_err(err, err_o) <= 1e-8
+    assert trace_rel_err(derr, derr_o) <= 1e-8
+    assert rel_err(cache.get_primal_flat(), z_o) <= 1e-10
+    assert rel_err(cache.get_dual_flat(), e_o) <= 1e-10
