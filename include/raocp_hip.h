@@ -75,17 +75,18 @@ typedef struct {
     const double* box_l_lo;  const double* box_l_hi;    /* [n_box_l][nx] */
     const int32_t* i_box_nl;/* [m] -1 = No constraint */
     const int32_t* i_box_l; /* [n] (leaves used) -1 = No constraint */
-    /* dynamics projection offline products */
-    int32_t n_b, n_abar, n_pb, n_k;
-    const double* B;        /* [n_b][nx][nu]  control dynamics B_j */
-    const double* Abar;     /* [n_abar][nx][nx]  A_j + B_j K_anc(j) */
-    const double* PB;       /* [n_pb][nx][nu]  P_j B_j */
+    /* dynamics projection: per-mode A, B (state / control dynamics of node j) and,
+     * per subtree class (classes numbered by stage), the offline products
+     * K, Rinv = (I + sum_j B_j'P_j B_j)^-1 and M = K' + sum_j Abar_j' P_j B_j */
+    int32_t n_a, n_b, n_k;
+    const double* A;        /* [n_a][nx][nx] */
+    const double* B;        /* [n_b][nx][nu] */
     const double* K;        /* [n_k][nu][nx] */
-    const double* Rinv;     /* [n_k][nu][nu]  (I + sum B'PB)^-1 */
+    const double* Rinv;     /* [n_k][nu][nu] */
+    const double* M;        /* [n_k][nx][nu] */
+    const int32_t* i_a;     /* [n] */
     const int32_t* i_b;     /* [n] */
-    const int32_t* i_abar;  /* [n] */
-    const int32_t* i_pb;    /* [n] */
-    const int32_t* i_k;     /* [m] */
+    const int32_t* i_k;     /* [m] class of nonleaf node i */
 } raocp_problem_desc;
 
 /* Create a context on HIP device `device`: validates the tree, uploads all tables
@@ -156,6 +157,8 @@ int raocp_cp_bench(raocp_ctx* ctx, const double* x0, int iters, double alpha, fl
 /* Time `reps` back-to-back launches of L (op=0) or L^T (op=1) on device-resident
  * vectors with HIP events on the context's stream; returns average ms per launch. */
 int raocp_op_bench(raocp_ctx* ctx, int op, int reps, float* ms_per_launch);
+/* Diagnostics: one dynamics projection with in-kernel s_memrealtime stamps (100 MHz). */
+int raocp_debug_dyn_stamps(raocp_ctx* ctx, unsigned long long* stamps, int cap);
 
 #ifdef __cplusplus
 }

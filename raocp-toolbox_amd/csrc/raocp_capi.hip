@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -52,9 +53,7 @@ struct raocp_ctx {
     double* q = nullptr;
     double* d = nullptr;
     double* x0 = nullptr;
-    double** zbuf = nullptr;     // device array {Z0, Z1, Z2}
-    double** ebuf = nullptr;     // device array {E0, E1}
-    double** solo = nullptr;     // device array {cur, cur, cur} for standalone calls
+    raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
     Ctl* ctl = nullptr;
     Ctl* h_ctl = nullptr;        // pinned host mirror
     double* hist = nullptr;
@@ -65,6 +64,11 @@ struct raocp_ctx {
     double* tmpD = nullptr;
     double* part = nullptr;      // dot-product partials
     double* scal = nullptr;      // device scalars
+    int cut = 0;                 // dynamics cut stage (0: per-stage kernels)
+    std::vector<int> cls_ptr_h;  // first class id per stage
+    double* redpart = nullptr;   // per-block residual maxima [red_rows][6]
+    int red_rows = 0;
+    size_t lds_top = 0, lds_bb = 0, lds_bf = 0;
     const int* ph = nullptr;     // dual placeholder offsets
     int n_ph = 0;
     bool has_x0 = false;
@@ -147,77 +151,133 @@ int copy_out(raocp_ctx* c, double* dst, const double* src, size_t count, int fla
     return RAOCP_OK;
 }
 
+// ---- template dispatch on (nx, nu): exact sizes get fully unrolled kernels,
+// everything else runs the runtime-size instantiation <0, 0>.
+template <class F, class... A>
+void dispatch(int nx, int nu, F f, A... a) {
+    if (nx == 20 && nu == 8) f.template run<20, 8>(a...);
+    else if (nx == 32 && nu == 12) f.template run<32, 12>(a...);
+    else if (nx == 64 && nu == 16) f.template run<64, 16>(a...);
+    else if (nx == 3 && nu == 2) f.template run<3, 2>(a...);
+    else f.template run<0, 0>(a...);
+}
+
+template <class K>
+void allow_lds(K kernel, size_t bytes) {
+    if (bytes > 64 * 1024) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)bytes);
+}
+
 // ---- launches (all on c->stream)
-void launch_ell(raocp_ctx* c, const double* z, double* eta) {
-    const Launch a = groups(c->nx + c->nu + 2, c->n - 1);
-    const Launch b = groups(2 * c->cmax + 2 + c->nx + c->nu, c->m);
-    const Launch l = groups(2 * c->nx + 2, c->n - c->m);
-    const int grid = a.blocks + b.blocks + l.blocks;
-    if (grid) raocp::k_ell<<<grid, kBlock, 0, c->stream>>>(c->dev, z, eta, a.blocks, b.blocks);
-}
-
-void launch_ell_t(raocp_ctx* c, const double* eta, double* z) {
-    const Launch a = groups(c->nx + c->nu + 2 * c->cmax + 2 + c->cmax, c->m);
-    const Launch l = groups(c->nx + 1, c->n - c->m);
-    const int grid = a.blocks + l.blocks;
-    if (grid) raocp::k_ell_t<<<grid, kBlock, 0, c->stream>>>(c->dev, eta, z, a.blocks);
-}
-
-// dynamics sweeps on z = zbuf[(k + zsel) % 3] (k from ctl when kptr != null)
-void launch_dynamics(raocp_ctx* c, double* const* zbuf, int zsel, const int* kptr, const Ctl* ctl) {
-    const int G = std::max(c->nx, c->nu);
-    for (int t = c->N - 1; t >= 0; --t) {
-        const int b = c->stage_ptr[t], e = c->stage_ptr[t + 1];
-        const Launch L = groups(G, e - b);
-        if (L.blocks)
-            raocp::k_dyn_back<<<L.blocks, kBlock, 0, c->stream>>>(c->dev, kptr, ctl, zbuf, zsel, c->q, c->d, b, e);
+struct EllOp {
+    template <int NX, int NU>
+    void run(raocp_ctx* c, const double* z, double* eta) {
+        const Launch a = groups(c->nx + c->nu + 2, c->n - 1);
+        const Launch b = groups(2 * c->cmax + 2 + c->nx + c->nu, c->m);
+        const Launch l = groups(2 * c->nx + 2, c->n - c->m);
+        const int grid = a.blocks + b.blocks + l.blocks;
+        if (grid) raocp::k_ell<NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, z, eta, a.blocks, b.blocks);
     }
-    for (int t = 0; t < c->N; ++t) {
-        const int b = c->stage_ptr[t], e = c->stage_ptr[t + 1];
-        const int nkids = c->stage_ptr[t + 2] - c->stage_ptr[t + 1];
-        const Launch U = groups(c->nu, e - b);
-        const Launch X = groups(c->nx, nkids);
-        if (U.blocks + X.blocks)
-            raocp::k_dyn_fwd<<<U.blocks + X.blocks, kBlock, 0, c->stream>>>(c->dev, kptr, ctl, zbuf, zsel, c->d,
-                                                                             c->x0, b, e, U.blocks);
+};
+void launch_ell(raocp_ctx* c, const double* z, double* eta) { dispatch(c->nx, c->nu, EllOp{}, c, z, eta); }
+
+struct EllTOp {
+    template <int NX, int NU>
+    void run(raocp_ctx* c, const double* eta, double* z) {
+        const Launch a = groups(c->nx + c->nu + 2 * c->cmax + 2 + c->cmax, c->m);
+        const Launch l = groups(c->nx + 1, c->n - c->m);
+        const int grid = a.blocks + l.blocks;
+        if (grid) raocp::k_ell_t<NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, eta, z, a.blocks);
     }
+};
+void launch_ell_t(raocp_ctx* c, const double* eta, double* z) { dispatch(c->nx, c->nu, EllTOp{}, c, eta, z); }
+
+struct DynOp {
+    template <int NX, int NU>
+    void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl) {
+        const int s = c->cut;
+        if (s > 0) {
+            // subtree-blocked: bottom backward, top (backward + forward), bottom forward
+            const int nsub = c->stage_ptr[s + 1] - c->stage_ptr[s];
+            if (s < c->N) {
+                auto kb = raocp::k_dyn_bottom_back<NX, NU>;
+                allow_lds(kb, c->lds_bb);
+                kb<<<nsub, 512, c->lds_bb, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->d, s);
+            }
+            auto kt = raocp::k_dyn_top<NX, NU>;
+            allow_lds(kt, c->lds_top);
+            kt<<<1, 1024, c->lds_top, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->x0, s);
+            if (s < c->N) {
+                auto kf = raocp::k_dyn_bottom_fwd<NX, NU>;
+                allow_lds(kf, c->lds_bf);
+                kf<<<nsub, 512, c->lds_bf, c->stream>>>(c->dev, bf, ctl, zsel, c->d, s);
+            }
+            return;
+        }
+        const int G = std::max(c->nx, c->nu);
+        for (int t = c->N - 1; t >= 0; --t) {
+            const int b = c->stage_ptr[t], e = c->stage_ptr[t + 1];
+            const Launch L = groups(G, e - b);
+            if (L.blocks)
+                raocp::k_dyn_back_stage<NX, NU><<<L.blocks, kBlock, 0, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->d,
+                                                                                     b, e);
+        }
+        for (int t = 0; t < c->N; ++t) {
+            const int b = c->stage_ptr[t], e = c->stage_ptr[t + 1];
+            const int nkids = c->stage_ptr[t + 2] - c->stage_ptr[t + 1];
+            const int blocks = groups(c->nu, e - b).blocks + groups(c->nx, nkids).blocks;
+            raocp::k_dyn_fwd_stage<NX, NU><<<blocks, kBlock, 0, c->stream>>>(c->dev, bf, ctl, zsel, c->d, c->x0, b, e);
+        }
+    }
+};
+// dynamics projection on z = Z[(k + zsel) % 3] (k from ctl when ctl != null, else 0)
+void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl) {
+    dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl);
 }
 
-void launch_cp_primal(raocp_ctx* c, bool full) {
-    const Launch a = groups(c->nx + c->nu + c->cmax + 1, c->m);
-    const Launch l = groups(c->nx, c->n - c->m);
-    const int grid = a.blocks + l.blocks;
-    if (full)
-        raocp::k_cp_primal<true><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->zbuf, c->ebuf, c->XI2, a.blocks);
-    else
-        raocp::k_cp_primal<false><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->zbuf, c->ebuf, c->XI2, a.blocks);
-}
+struct CpPrimalOp {
+    template <int NX, int NU>
+    void run(raocp_ctx* c, bool full) {
+        const Launch a = groups(c->nx + c->nu + c->cmax + 1, c->m);
+        const Launch l = groups(c->nx, c->n - c->m);
+        const int grid = a.blocks + l.blocks;
+        if (full)
+            raocp::k_cp_primal<true, NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
+                                                                              c->redpart, a.blocks);
+        else
+            raocp::k_cp_primal<false, NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
+                                                                               c->redpart, a.blocks);
+    }
+};
+void launch_cp_primal(raocp_ctx* c, bool full) { dispatch(c->nx, c->nu, CpPrimalOp{}, c, full); }
 
+struct CpDualOp {
+    template <int NX, int NU>
+    void run(raocp_ctx* c, bool with_l, double* dsolo, int mode) {
+        const Launch a = groups(c->nx + c->nu + 2, c->n - 1);
+        const Launch b = groups(2 * c->cmax + 2 + c->nx + c->nu, c->m);
+        const Launch l = groups(2 * c->nx + 2, c->n - c->m);
+        const int grid = a.blocks + b.blocks + l.blocks;
+        if (with_l)
+            raocp::k_cp_dual<true, NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
+                                                                            nullptr, c->redpart, a.blocks, b.blocks,
+                                                                            raocp::kDualAll);
+        else
+            raocp::k_cp_dual<false, NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
+                                                                             dsolo, c->redpart, a.blocks, b.blocks, mode);
+    }
+};
 void launch_cp_dual(raocp_ctx* c, bool with_l, double* dsolo, int mode = raocp::kDualAll) {
-    const Launch a = groups(c->nx + c->nu + 2, c->n - 1);
-    const Launch b = groups(2 * c->cmax + 2 + c->nx + c->nu, c->m);
-    const Launch l = groups(2 * c->nx + 2, c->n - c->m);
-    const int grid = a.blocks + b.blocks + l.blocks;
-    if (with_l)
-        raocp::k_cp_dual<true><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->zbuf, c->ebuf, c->XI2, nullptr,
-                                                                a.blocks, b.blocks, raocp::kDualAll);
-    else
-        raocp::k_cp_dual<false><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->zbuf, c->ebuf, c->XI2, dsolo,
-                                                                 a.blocks, b.blocks, mode);
+    dispatch(c->nx, c->nu, CpDualOp{}, c, with_l, dsolo, mode);
 }
 
 void enqueue_cp_iteration(raocp_ctx* c) {
-    launch_dynamics(c, c->zbuf, 1, &c->ctl->k, c->ctl);
+    launch_dynamics(c, c->bufs, 1, c->ctl);
     launch_cp_dual(c, true, nullptr);
     launch_cp_primal(c, true);
-    raocp::k_cp_check<<<1, 1, 0, c->stream>>>(c->ctl, c->hist);
+    raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->red_rows);
 }
 
-int set_solo(raocp_ctx* c, double* cur) {
-    double* h[3] = {cur, cur, cur};
-    HIPCHK(hipMemcpyAsync(c->solo, h, sizeof(h), hipMemcpyHostToDevice, c->stream));
-    return RAOCP_OK;
-}
 
 int set_ctl_alpha(raocp_ctx* c, double alpha) {
     HIPCHK(hipMemcpyAsync(&c->ctl->alpha, &alpha, sizeof(double), hipMemcpyHostToDevice, c->stream));
@@ -427,18 +487,99 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         (rc = c->upload_vec(&D.blo_l, lo_l)) || (rc = c->upload_vec(&D.bhi_l, hi_l)) ||
         (rc = c->upload(&D.iBnl, pr->i_box_nl, m)) || (rc = c->upload(&D.iBl, pr->i_box_l, n)))
         return bail(rc);
-    // dynamics products
-    if ((rc = c->upload_vec(&D.Brm, copy_table(pr->B, (size_t)pr->n_b * nx * nu))) ||
-        (rc = c->upload_vec(&D.Bcm, to_colmajor(pr->B, pr->n_b, nx, nu))) ||
-        (rc = c->upload_vec(&D.Arm, copy_table(pr->Abar, (size_t)pr->n_abar * nx * nx))) ||
-        (rc = c->upload_vec(&D.Acm, to_colmajor(pr->Abar, pr->n_abar, nx, nx))) ||
-        (rc = c->upload_vec(&D.PBcm, to_colmajor(pr->PB, pr->n_pb, nx, nu))) ||
-        (rc = c->upload_vec(&D.Krm, copy_table(pr->K, (size_t)pr->n_k * nu * nx))) ||
-        (rc = c->upload_vec(&D.Kcm, to_colmajor(pr->K, pr->n_k, nu, nx))) ||
-        (rc = c->upload_vec(&D.Rcm, to_colmajor(pr->Rinv, pr->n_k, nu, nu))) ||
-        (rc = c->upload(&D.iB, pr->i_b, n)) || (rc = c->upload(&D.iAbar, pr->i_abar, n)) ||
-        (rc = c->upload(&D.iPB, pr->i_pb, n)) || (rc = c->upload(&D.iK, pr->i_k, m)))
-        return bail(rc);
+    // dynamics tables, padded for the lanes-over-rows access (raocp_dyn.hip header)
+    {
+        auto pad_rm = [](const double* src, int cnt, int rows, int cols) {  // [t][r][c] at r*(cols+1)+c
+            std::vector<double> out((size_t)cnt * rows * (cols + 1), 0.0);
+            for (int t = 0; t < cnt; ++t)
+                for (int r = 0; r < rows; ++r)
+                    for (int k = 0; k < cols; ++k)
+                        out[(size_t)t * rows * (cols + 1) + (size_t)r * (cols + 1) + k] =
+                            src[(size_t)t * rows * cols + (size_t)r * cols + k];
+            return out;
+        };
+        auto pad_cm = [](const double* src, int cnt, int rows, int cols) {  // [t] M(r,c) at c*(rows+1)+r
+            std::vector<double> out((size_t)cnt * cols * (rows + 1), 0.0);
+            for (int t = 0; t < cnt; ++t)
+                for (int r = 0; r < rows; ++r)
+                    for (int k = 0; k < cols; ++k)
+                        out[(size_t)t * cols * (rows + 1) + (size_t)k * (rows + 1) + r] =
+                            src[(size_t)t * rows * cols + (size_t)r * cols + k];
+            return out;
+        };
+        D.nA = pr->n_a;
+        D.nB = pr->n_b;
+        if ((rc = c->upload_vec(&D.Ap, pad_rm(pr->A, pr->n_a, nx, nx))) ||
+            (rc = c->upload_vec(&D.Bp, pad_rm(pr->B, pr->n_b, nx, nu))) ||
+            (rc = c->upload_vec(&D.Rp, pad_cm(pr->Rinv, pr->n_k, nu, nu))) ||
+            (rc = c->upload_vec(&D.Kp, pad_rm(pr->K, pr->n_k, nu, nx))) ||
+            (rc = c->upload_vec(&D.Mp, pad_cm(pr->M, pr->n_k, nx, nu))))
+            return bail(rc);
+        std::vector<raocp::Rec> ninfo(m), cinfo(n);
+        std::vector<int> cls_ptr(N + 1, pr->n_k);
+        for (int i = 0; i < m; ++i) ninfo[i] = raocp::Rec{t->ch_start[i], t->nch[i], pr->i_k[i], t->stage[i]};
+        cinfo[0] = raocp::Rec{0, 0, -1, 0};
+        for (int j = 1; j < n; ++j) cinfo[j] = raocp::Rec{pr->i_a[j], pr->i_b[j], t->anc[j], 0};
+        for (int i = m - 1; i >= 0; --i) {
+            if (i + 1 < m && pr->i_k[i] > pr->i_k[i + 1] && t->stage[i] < t->stage[i + 1])
+                return bail(fail(RAOCP_ERR_ARG, "classes must be numbered by stage"));
+            cls_ptr[t->stage[i]] = std::min(cls_ptr[t->stage[i]], pr->i_k[i]);
+        }
+        for (int st = N - 1; st >= 0; --st) cls_ptr[st] = std::min(cls_ptr[st], cls_ptr[st + 1]);
+        c->cls_ptr_h = cls_ptr;
+        if ((rc = c->upload_vec(&D.ninfo, ninfo)) || (rc = c->upload_vec(&D.cinfo, cinfo)) ||
+            (rc = c->upload_vec(&D.cls_ptr, cls_ptr)) || (rc = c->upload_vec(&D.stage_ptr, c->stage_ptr)))
+            return bail(rc);
+    }
+    D.N = N;
+
+    // ---- dynamics plan: cut stage s (top = stages < s in one workgroup, one workgroup
+    // per subtree below; matrices + top state in LDS). Per-stage launches otherwise.
+    {
+        const size_t kLds = 160 * 1024 - 1024;  // minus the static LDS of the kernels
+        const size_t SA = (size_t)nx * (nx + 1), SB = (size_t)nx * (nu + 1), SR = (size_t)nu * (nu + 1),
+                     SK = (size_t)nu * (nx + 1);
+        auto mats = [&](int c0, int c1) { return (size_t)pr->n_a * SA + pr->n_b * SB + (size_t)(c1 - c0) * (SR + 2 * SK); };
+        const std::vector<int>& cp = c->cls_ptr_h;
+        auto top_bytes = [&](int s) {
+            const size_t T = c->stage_ptr[s], nb = c->stage_ptr[s + 1] - T;
+            return 8 * (2 * 1024 + mats(0, cp[s]) + T * (2 * nx + 2 * nu) + nb * nx + 1) + 16 * (2 * T + nb);
+        };
+        auto sub_nonleaf = [&](int s) {  // max nonleaf count over the subtrees rooted at stage s
+            int best = 0;
+            for (int r = c->stage_ptr[s]; r < c->stage_ptr[s + 1]; ++r) {
+                int lo = r, hi = r + 1, acc = 0;
+                for (int st = s; st < N; ++st) {
+                    acc += hi - lo;
+                    const int nlo = t->ch_start[lo], nhi = t->ch_start[hi - 1] + t->nch[hi - 1];
+                    lo = nlo;
+                    hi = nhi;
+                }
+                best = std::max(best, acc);
+            }
+            return best;
+        };
+        c->cut = 0;
+        if (m <= 1024 && top_bytes(N) <= kLds) {
+            c->cut = N;
+        } else {
+            for (int s = 1; s < N; ++s) {
+                if (c->stage_ptr[s + 1] - c->stage_ptr[s] < 96 || N - s > raocp::kMaxLevels) continue;
+                if (top_bytes(s) > kLds) break;
+                const size_t snl = sub_nonleaf(s);
+                const size_t bb = 8 * (2 * 512 + mats(cp[s], cp[N]) + snl * nx);
+                const size_t bf = 8 * (mats(cp[s], cp[N]) + snl * (nx + nu));
+                if (bb > kLds || bf > kLds) continue;
+                c->cut = s;
+                c->lds_bb = bb;
+                c->lds_bf = bf;
+                break;
+            }
+        }
+        if (c->cut > 0) c->lds_top = top_bytes(c->cut);
+        if (const char* env = getenv("RAOCP_DYN_PER_STAGE"))
+            if (env[0] == '1') c->cut = 0;
+    }
 
     // ---- iterate and work buffers
     for (int b = 0; b < 3; ++b)
@@ -446,11 +587,19 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     for (int b = 0; b < 2; ++b)
         if ((rc = c->alloc(&c->E[b], c->D))) return bail(rc);
     if ((rc = c->alloc(&c->XI2, c->D)) || (rc = c->alloc(&c->q, (size_t)n * nx)) || (rc = c->alloc(&c->d, (size_t)m * nu)) ||
-        (rc = c->alloc(&c->x0, nx)) || (rc = c->alloc(&c->zbuf, 3)) || (rc = c->alloc(&c->ebuf, 2)) ||
-        (rc = c->alloc(&c->solo, 3)) || (rc = c->alloc(&c->ctl, 1)) || (rc = c->alloc(&c->tmpP, c->P)) ||
+        (rc = c->alloc(&c->x0, nx)) || (rc = c->alloc(&c->ctl, 1)) || (rc = c->alloc(&c->tmpP, c->P)) ||
         (rc = c->alloc(&c->tmpD, c->D)) || (rc = c->alloc(&c->part, 1024)) || (rc = c->alloc(&c->scal, 8)))
         return bail(rc);
     if (hipHostMalloc((void**)&c->h_ctl, sizeof(Ctl), 0) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "hipHostMalloc"));
+    {
+        const int g_dual = groups(nx + nu + 2, n - 1).blocks + groups(2 * cmax + 2 + nx + nu, m).blocks +
+                           groups(2 * nx + 2, n - m).blocks;
+        const int g_primal = groups(nx + nu + cmax + 1, m).blocks + groups(nx, n - m).blocks;
+        c->red_rows = std::max(g_dual, g_primal);
+        if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
+        if (hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)) != hipSuccess)
+            return bail(fail(RAOCP_ERR_HIP, "memset"));
+    }
     for (int b = 0; b < 3; ++b)
         if (hipMemset(c->Z[b], 0, c->P * sizeof(double)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
     for (int b = 0; b < 2; ++b)
@@ -459,8 +608,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         hipMemset(c->q, 0, (size_t)n * nx * sizeof(double)) != hipSuccess ||
         hipMemset(c->d, 0, (size_t)m * nu * sizeof(double)) != hipSuccess)
         return bail(fail(RAOCP_ERR_HIP, "memset"));
-    HIPCHK(hipMemcpy(c->zbuf, c->Z, sizeof(c->Z), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->ebuf, c->E, sizeof(c->E), hipMemcpyHostToDevice));
+    c->bufs = raocp::Bufs{c->Z[0], c->Z[1], c->Z[2], c->E[0], c->E[1]};
     c->cur_z = c->Z[0];
     c->cur_e = c->E[0];
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
@@ -557,9 +705,8 @@ int raocp_relax_s0(raocp_ctx* c, double alpha) {
 int raocp_project_on_dynamics(raocp_ctx* c) {
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     if (!c->has_x0) return fail(RAOCP_ERR_STATE, "initial state not cached (call cache_initial_state first)");
-    int rc = set_solo(c, c->cur_z);
-    if (rc) return rc;
-    launch_dynamics(c, c->solo, 0, nullptr, nullptr);
+    const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
+    launch_dynamics(c, solo, 0, nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return RAOCP_OK;
@@ -792,6 +939,25 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     if (c->h_ctl->final_k != iters - 1) return fail(RAOCP_ERR_STATE, "bench did not run the requested iterations");
     c->cur_z = c->Z[iters % 3];
     c->cur_e = c->E[iters % 2];
+    return RAOCP_OK;
+}
+
+// diagnostics: run the dynamics projection once on the current primal with in-kernel
+// stamps enabled (k_dyn_top: prologue, each backward / forward stage); returns up to
+// `cap` raw 100 MHz timestamps.
+int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
+    if (!c || !out || cap <= 0) return fail(RAOCP_ERR_ARG, "bad argument");
+    unsigned long long* st = nullptr;
+    int rc = c->alloc(&st, (size_t)cap);
+    if (rc) return rc;
+    HIPCHK(hipMemset(st, 0, cap * sizeof(unsigned long long)));
+    Dev saved = c->dev;
+    c->dev.stamps = st;
+    const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
+    launch_dynamics(c, solo, 0, nullptr);
+    c->dev = saved;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipMemcpy(out, st, cap * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return RAOCP_OK;
 }
 

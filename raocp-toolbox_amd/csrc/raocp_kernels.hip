@@ -33,6 +33,25 @@ struct Ctl {
     double tol;
 };
 
+// explicit address spaces: loads through these types are ds_read / global_load, never flat
+typedef __attribute__((address_space(3))) double ldsd;
+typedef __attribute__((address_space(1))) double glbd;
+// node records for the dynamics sweep: a builtin 4-int vector (usable in any address space)
+typedef int Rec __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const Rec glbrec;
+typedef __attribute__((address_space(3))) Rec ldsrec;
+
+// the rotating CP buffers: primal Z[k % 3], dual E[k % 2] (selected by the iteration counter)
+struct Bufs {
+    double* z0;
+    double* z1;
+    double* z2;
+    double* e0;
+    double* e1;
+};
+
+__device__ __forceinline__ glbd* pick2(const Bufs& bf, int k) { return (glbd*)((k & 1) ? bf.e1 : bf.e0); }
+
 // Device-side problem description (all pointers are HBM).
 struct Dev {
     int n, m, nx, nu, cmax;
@@ -51,26 +70,151 @@ struct Dev {
     const double* alpha_r; const double* cond;
     const double* blo_nl; const double* bhi_nl; const double* blo_l; const double* bhi_l;
     const int* iBnl; const int* iBl;
-    // dynamics offline products
-    const double* Brm;   // row-major  B[k*nu + c]
-    const double* Bcm;   // col-major  B[c*nx + k]
-    const double* Arm;   // Abar row-major [k*nx + r] = Abar_kr
-    const double* Acm;   // Abar col-major [k*nx + r] = Abar_rk
-    const double* PBcm;  // PB col-major [c*nx + k] = PB_kc
-    const double* Krm;   // K row-major [c*nx + r] = K_cr
-    const double* Kcm;   // K col-major [k*nu + r] = K_rk
-    const double* Rcm;   // Rinv col-major [c*nu + r] = Rinv_rc
-    const int* iB; const int* iAbar; const int* iPB; const int* iK;
+    // dynamics projection (raocp_dyn.hip): padded per-mode A, B and per-class Rinv, K, M
+    const double* Ap; const double* Bp; const double* Rp; const double* Kp; const double* Mp;
+    int nA, nB;
+    const Rec* ninfo;      // [m] {ch_start, nch, class, stage}
+    const Rec* cinfo;      // [n] {iA, iB, anc, 0} (node 0: unused)
+    const int* cls_ptr;    // [N+1] first class of each stage (classes numbered by stage)
+    const int* stage_ptr;  // [N+2] first node id of each stage (BFS numbering)
+    int N;                 // last stage
+    unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)
 };
+
+// diagnostic timestamp (100 MHz constant clock), thread 0 only, when enabled
+__device__ __forceinline__ void stamp(const Dev& p, int slot) {
+    if (p.stamps && threadIdx.x == 0 && blockIdx.x == 0) p.stamps[slot] = __builtin_amdgcn_s_memrealtime();
+}
+
 
 __device__ __forceinline__ int e3(const Dev& p, int j) { return p.E3 + 1 + (j - 1) * p.nx; }
 __device__ __forceinline__ int e4(const Dev& p, int j) { return p.E4 + 1 + (j - 1) * p.nu; }
 __device__ __forceinline__ int e11(const Dev& p, int l) { return p.E11 + p.m + (l - p.m) * p.nx; }
 
+__device__ __forceinline__ int cdiv_dev(int a, int b) { return (a + b - 1) / b; }
+
 __device__ __forceinline__ u64 dbits(double v) { return (u64)__double_as_longlong(v); }
 
-// block-wide max of non-negative doubles, one atomicMax per block
-__device__ void block_max_atomic(double v, u64* dst, double* s_red) {
+// ---- batched dot products ----------------------------------------------------------
+// All loads of a chunk are issued before its FMAs (a sched_barrier keeps hipcc from
+// interleaving each load with its FMA, which pays the memory latency per element);
+// two accumulators halve the dependent-FMA chain. N > 0: compile-time length (fully
+// unrolled); N == 0: runtime length n, plain loop.
+template <int N>
+struct Chunk {
+    static constexpr int C = N <= 24 ? N : 16;
+};
+
+// sum_k m[k*ms] * v[k]
+template <int N, class PM, class PV>
+__device__ __forceinline__ double dotb(PM m, int ms, PV v, int n) {
+    if constexpr (N == 0) {
+        double s = 0.0;
+        for (int k = 0; k < n; ++k) s = fma(m[k * ms], v[k], s);
+        return s;
+    } else {
+        constexpr int C = Chunk<N>::C;
+        double s0 = 0.0, s1 = 0.0;
+        _Pragma("unroll") for (int k0 = 0; k0 < N; k0 += C) {
+            double a[C], b[C];
+            _Pragma("unroll") for (int k = 0; k < C; ++k) if (k0 + k < N) {
+                a[k] = m[(k0 + k) * ms];
+                b[k] = v[k0 + k];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            _Pragma("unroll") for (int k = 0; k < C; ++k) if (k0 + k < N) {
+                if (k & 1) s1 = fma(a[k], b[k], s1);
+                else s0 = fma(a[k], b[k], s0);
+            }
+        }
+        return s0 + s1;
+    }
+}
+
+// a = sum_k m[k*ms] (2 z[k] - p[k]),  b = sum_k m[k*ms] (z[k] - p[k])   (L of 2z+ - p and z+ - p)
+template <int N, class PM, class PV>
+__device__ __forceinline__ void dot_zp(PM m, int ms, PV z, PV pp, int n, double& a, double& b) {
+    if constexpr (N == 0) {
+        double sa = 0.0, sb = 0.0;
+        for (int k = 0; k < n; ++k) {
+            const double mk = m[k * ms], zk = z[k], pk = pp[k];
+            sa = fma(mk, 2.0 * zk - pk, sa);
+            sb = fma(mk, zk - pk, sb);
+        }
+        a = sa;
+        b = sb;
+    } else {
+        constexpr int C = N <= 16 ? N : 12;
+        double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+        _Pragma("unroll") for (int k0 = 0; k0 < N; k0 += C) {
+            double mm[C], zz[C], qq[C];
+            _Pragma("unroll") for (int k = 0; k < C; ++k) if (k0 + k < N) {
+                mm[k] = m[(k0 + k) * ms];
+                zz[k] = z[k0 + k];
+                qq[k] = pp[k0 + k];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            _Pragma("unroll") for (int k = 0; k < C; ++k) if (k0 + k < N) {
+                const double w = 2.0 * zz[k] - qq[k], v = zz[k] - qq[k];
+                if (k & 1) { a1 = fma(mm[k], w, a1); b1 = fma(mm[k], v, b1); }
+                else { a0 = fma(mm[k], w, a0); b0 = fma(mm[k], v, b0); }
+            }
+        }
+        a = a0 + a1;
+        b = b0 + b1;
+    }
+}
+
+// L^T of three duals at once: sA = m.dA, sW = m.(dP - dA), sC = m.c
+template <int N, bool FULL, class PM, class PV>
+__device__ __forceinline__ void dot_lt3(PM m, int ms, PV dA, PV dP, PV cc, int n, double& sA, double& sW,
+                                        double& sC) {
+    if constexpr (N == 0) {
+        double a = 0.0, w = 0.0, c = 0.0;
+        for (int k = 0; k < n; ++k) {
+            const double mk = m[k * ms], va = dA[k];
+            a = fma(mk, va, a);
+            if (FULL) {
+                w = fma(mk, dP[k] - va, w);
+                c = fma(mk, cc[k], c);
+            }
+        }
+        sA = a;
+        sW = w;
+        sC = c;
+    } else {
+        constexpr int C = N <= 12 ? N : 10;
+        double a0 = 0.0, a1 = 0.0, w0 = 0.0, w1 = 0.0, c0 = 0.0, c1 = 0.0;
+        _Pragma("unroll") for (int k0 = 0; k0 < N; k0 += C) {
+            double mm[C], va[C], vp[C], vc[C];
+            _Pragma("unroll") for (int k = 0; k < C; ++k) if (k0 + k < N) {
+                mm[k] = m[(k0 + k) * ms];
+                va[k] = dA[k0 + k];
+                if (FULL) {
+                    vp[k] = dP[k0 + k];
+                    vc[k] = cc[k0 + k];
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            _Pragma("unroll") for (int k = 0; k < C; ++k) if (k0 + k < N) {
+                if (k & 1) {
+                    a1 = fma(mm[k], va[k], a1);
+                    if (FULL) { w1 = fma(mm[k], vp[k] - va[k], w1); c1 = fma(mm[k], vc[k], c1); }
+                } else {
+                    a0 = fma(mm[k], va[k], a0);
+                    if (FULL) { w0 = fma(mm[k], vp[k] - va[k], w0); c0 = fma(mm[k], vc[k], c0); }
+                }
+            }
+        }
+        sA = a0 + a1;
+        sW = w0 + w1;
+        sC = c0 + c1;
+    }
+}
+
+// block-wide max of non-negative doubles -> one plain store per block (the per-block
+// partials are reduced by k_cp_check; no atomics on a single hot address)
+__device__ void block_max_store(double v, double* dst, double* s_red) {
     for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
     const int w = threadIdx.x >> 6;
     __syncthreads();
@@ -79,7 +223,7 @@ __device__ void block_max_atomic(double v, u64* dst, double* s_red) {
     if (threadIdx.x == 0) {
         double b = s_red[0];
         for (int i = 1; i < (int)(blockDim.x >> 6); ++i) b = fmax(b, s_red[i]);
-        atomicMax(dst, dbits(b));
+        *dst = b;
     }
 }
 
@@ -102,9 +246,10 @@ __device__ __forceinline__ GroupIdx group_index(int G, int begin, int end) {
 // L (operators.py:19-53): eta <- L z on active slots only.
 // Three node types in one launch, block-uniform branch on blockIdx.x.
 // ==============================================================================
+template <int NXc, int NUc>
 __global__ void __launch_bounds__(kBlock) k_ell(Dev p, const double* __restrict__ z, double* __restrict__ eta,
                                                  int nbA, int nbB) {
-    const int nx = p.nx, nu = p.nu;
+    const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
     if ((int)blockIdx.x < nbA) {
         // child blocks j = 1..n-1: eta3 = sqrtQ_j x_anc, eta4 = sqrtR_j u_anc, eta5 = eta6 = tau_j/2
         GroupIdx g = group_index(nx + nu + 2, 1, p.n);
@@ -114,14 +259,14 @@ __global__ void __launch_bounds__(kBlock) k_ell(Dev p, const double* __restrict_
             const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
             const double* x = z + p.X0 + (size_t)a * nx;
             double acc = 0.0;
-            for (int k = 0; k < nx; ++k) acc = fma(M[k * nx + r], x[k], acc);
+            acc = dotb<NXc>(M + r, nx, x, nx);
             eta[e3(p, j) + r] = acc;
         } else if (r < nx + nu) {
             const int rr = r - nx;
             const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
             const double* u = z + p.U0 + (size_t)a * nu;
             double acc = 0.0;
-            for (int k = 0; k < nu; ++k) acc = fma(M[k * nu + rr], u[k], acc);
+            acc = dotb<NUc>(M + rr, nu, u, nu);
             eta[e4(p, j) + rr] = acc;
         } else {
             const double ht = 0.5 * z[p.T0 + j];
@@ -164,7 +309,7 @@ __global__ void __launch_bounds__(kBlock) k_ell(Dev p, const double* __restrict_
         if (r < nx) {
             const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
             double acc = 0.0;
-            for (int k = 0; k < nx; ++k) acc = fma(M[k * nx + r], x[k], acc);
+            acc = dotb<NXc>(M + r, nx, x, nx);
             eta[e11(p, l) + r] = acc;
         } else if (r < nx + 2) {
             eta[(r == nx ? p.E12 : p.E13) + l] = 0.5 * z[p.S0 + l];
@@ -178,9 +323,10 @@ __global__ void __launch_bounds__(kBlock) k_ell(Dev p, const double* __restrict_
 // ==============================================================================
 // L^T (operators.py:55-94): z <- L^T eta on every slot except tau_0.
 // ==============================================================================
+template <int NXc, int NUc>
 __global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restrict__ eta, double* __restrict__ z,
                                                    int nbA) {
-    const int nx = p.nx, nu = p.nu;
+    const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
     if ((int)blockIdx.x < nbA) {
         // nonleaf i: x, u (child sums), y = eta1 - b eta2, s = eta2, tau of the children
         const int G = nx + nu + (2 * p.cmax + 1) + 1 + p.cmax;
@@ -194,9 +340,7 @@ __global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restric
                 const int j = cs + q;
                 const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
                 const double* e = eta + e3(p, j);
-                double s = 0.0;
-                for (int k = 0; k < nx; ++k) s = fma(M[k * nx + r], e[k], s);
-                acc += s;
+                acc += dotb<NXc>(M + r, nx, e, nx);
             }
             z[p.X0 + (size_t)i * nx + r] = acc;
         } else if (r < nx + nu) {
@@ -206,9 +350,7 @@ __global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restric
                 const int j = cs + q;
                 const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
                 const double* e = eta + e4(p, j);
-                double s = 0.0;
-                for (int k = 0; k < nu; ++k) s = fma(M[k * nu + rr], e[k], s);
-                acc += s;
+                acc += dotb<NUc>(M + rr, nu, e, nu);
             }
             z[p.U0 + (size_t)i * nu + rr] = acc;
         } else if (r < nx + nu + 2 * p.cmax + 1) {
@@ -238,8 +380,7 @@ __global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restric
         if (r < nx) {
             const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
             const double* e = eta + e11(p, l);
-            double acc = 0.0;
-            for (int k = 0; k < nx; ++k) acc = fma(M[k * nx + r], e[k], acc);
+            double acc = dotb<NXc>(M + r, nx, e, nx);
             const int o14 = p.e14off[l - p.m];
             if (o14 >= 0) acc += eta[o14 + r];
             z[p.X0 + (size_t)l * nx + r] = acc;
@@ -249,139 +390,7 @@ __global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restric
     }
 }
 
-// ==============================================================================
-// Dynamics projection (cache.py:259-288), one launch per stage.
-// Backward: for nonleaf i at stage t (children at t+1; a leaf child has q = -x):
-//   d_i = Rinv_i (u_i - sum_j B_j' q_j)
-//   q_i = -x_i + K_i'(d_i - u_i) + sum_j Abar_j'(P_j B_j d_i + q_j)
-// Forward: u_i = K_i x_i + d_i ; x_j = Abar_j x_i + B_j d_i (x_0 = x0bar).
-// ==============================================================================
-__global__ void __launch_bounds__(kBlock) k_dyn_back(Dev p, const int* __restrict__ kptr, const Ctl* __restrict__ ctl,
-                                                      double* const* zbuf, int zsel, double* __restrict__ qbuf,
-                                                      double* __restrict__ dbuf, int begin, int end) {
-    __shared__ double s_g[kBlock];
-    __shared__ double s_t[kBlock];
-    if (ctl && ctl->done) return;
-    const int kk = kptr ? *kptr : 0;
-    double* z = zbuf[(kk + zsel) % 3];
-    const int nx = p.nx, nu = p.nu;
-    const int G = nx > nu ? nx : nu;
-    const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-    const int i = begin + blockIdx.x * per + gl;
-    const bool live = gl < per && i < end;
-    const int base = gl * G;
-    int c = 0, cs = 0;
-    if (live) { c = p.nch[i]; cs = p.ch_start[i]; }
-    // (1) g = u - sum_j B_j' q_j
-    double g = 0.0;
-    if (live && r < nu) {
-        double sum = 0.0;
-        for (int q = 0; q < c; ++q) {
-            const int j = cs + q;
-            const double* B = p.Brm + (size_t)p.iB[j] * nx * nu;
-            double s = 0.0;
-            if (j >= p.m) {
-                const double* xj = z + p.X0 + (size_t)j * nx;
-                for (int k = 0; k < nx; ++k) s = fma(B[k * nu + r], -xj[k], s);
-            } else {
-                const double* qj = qbuf + (size_t)j * nx;
-                for (int k = 0; k < nx; ++k) s = fma(B[k * nu + r], qj[k], s);
-            }
-            sum += s;
-        }
-        g = z[p.U0 + (size_t)i * nu + r] - sum;
-    }
-    s_g[threadIdx.x] = g;
-    __syncthreads();
-    // (2) d = Rinv g
-    double dr = 0.0;
-    if (live && r < nu) {
-        const double* R = p.Rcm + (size_t)p.iK[i] * nu * nu;
-        for (int cc = 0; cc < nu; ++cc) dr = fma(R[cc * nu + r], s_g[base + cc], dr);
-        dbuf[(size_t)i * nu + r] = dr;
-    }
-    __syncthreads();
-    s_g[threadIdx.x] = dr;  // s_g now holds d
-    __syncthreads();
-    // (3) acc = sum_j Abar_j' (PB_j d + q_j)
-    double acc = 0.0;
-    const int cmax = p.cmax;
-    for (int q = 0; q < cmax; ++q) {
-        const bool has = live && q < c;
-        const int j = cs + q;
-        double t = 0.0;
-        if (has && r < nx) {
-            const double* PB = p.PBcm + (size_t)p.iPB[j] * nx * nu;
-            double s = 0.0;
-            for (int cc = 0; cc < nu; ++cc) s = fma(PB[cc * nx + r], s_g[base + cc], s);
-            const double qv = j >= p.m ? -z[p.X0 + (size_t)j * nx + r] : qbuf[(size_t)j * nx + r];
-            t = s + qv;
-        }
-        s_t[threadIdx.x] = t;
-        __syncthreads();
-        if (has && r < nx) {
-            const double* A = p.Arm + (size_t)p.iAbar[j] * nx * nx;
-            double s = 0.0;
-            for (int k = 0; k < nx; ++k) s = fma(A[k * nx + r], s_t[base + k], s);
-            acc += s;
-        }
-        __syncthreads();
-    }
-    // (4) q_i = -x_i + K'(d - u) + acc
-    if (live && r < nx) {
-        const double* K = p.Krm + (size_t)p.iK[i] * nu * nx;
-        const double* u = z + p.U0 + (size_t)i * nu;
-        double s = 0.0;
-        for (int cc = 0; cc < nu; ++cc) s = fma(K[cc * nx + r], s_g[base + cc] - u[cc], s);
-        qbuf[(size_t)i * nx + r] = (-z[p.X0 + (size_t)i * nx + r] + s) + acc;
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) k_dyn_fwd(Dev p, const int* __restrict__ kptr, const Ctl* __restrict__ ctl,
-                                                     double* const* zbuf, int zsel, const double* __restrict__ dbuf,
-                                                     const double* __restrict__ x0, int pbegin, int pend, int nbU) {
-    if (ctl && ctl->done) return;
-    const int kk = kptr ? *kptr : 0;
-    double* z = zbuf[(kk + zsel) % 3];
-    const int nx = p.nx, nu = p.nu;
-    if ((int)blockIdx.x < nbU) {
-        // u_i = K_i x_i + d_i for parents at this stage
-        const int G = nu;
-        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-        const int i = pbegin + blockIdx.x * per + gl;
-        if (gl >= per || i >= pend) return;
-        const double* x = i == 0 ? x0 : z + p.X0 + (size_t)i * nx;
-        const double* K = p.Kcm + (size_t)p.iK[i] * nu * nx;
-        double s = 0.0;
-        for (int k = 0; k < nx; ++k) s = fma(K[k * nu + r], x[k], s);
-        z[p.U0 + (size_t)i * nu + r] = s + dbuf[(size_t)i * nu + r];
-        if (i == 0) {
-            // x_0 = x0bar (cache.py:282); lanes r < nu cover nx entries in strides
-            for (int k = r; k < nx; k += nu) z[p.X0 + k] = x0[k];
-        }
-        return;
-    }
-    {
-        // children j of the stage: x_j = Abar_j x_i + B_j d_i
-        const int G = nx;
-        const int bid = blockIdx.x - nbU;
-        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-        const int cbegin = p.ch_start[pbegin];
-        const int cend = p.ch_start[pend - 1] + p.nch[pend - 1];
-        const int j = cbegin + bid * per + gl;
-        if (gl >= per || j >= cend) return;
-        const int i = p.anc[j];
-        const double* x = i == 0 ? x0 : z + p.X0 + (size_t)i * nx;
-        const double* A = p.Acm + (size_t)p.iAbar[j] * nx * nx;
-        const double* B = p.Bcm + (size_t)p.iB[j] * nx * nu;
-        const double* d = dbuf + (size_t)i * nu;
-        double s = 0.0;
-        for (int k = 0; k < nx; ++k) s = fma(A[k * nx + r], x[k], s);
-        double s2 = 0.0;
-        for (int cc = 0; cc < nu; ++cc) s2 = fma(B[cc * nx + r], d[cc], s2);
-        z[p.X0 + (size_t)j * nx + r] = s + s2;
-    }
-}
+#include "raocp_dyn.hip"
 
 // ==============================================================================
 // AVaR kernel projection of (y_i, tau_children, s_children) (cache.py:290-317),
@@ -469,22 +478,23 @@ struct LtIn {
     const double* c;   // xi2
 };
 
-template <bool FULL>
-__global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ ctl, double* const* zbuf,
-                                                       double* const* ebuf, const double* __restrict__ xi2,
-                                                       int nbA) {
+template <bool FULL, int NXc, int NUc>
+__global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ ctl, Bufs bf,
+                                                       const double* __restrict__ xi2,
+                                                       double* __restrict__ part, int nbA) {
     __shared__ double s_x[kBlock];
     __shared__ double s_red[4][kBlock / 64];
     if (ctl->done) return;
     const int kk = ctl->k;
     const double alpha = ctl->alpha;
-    const double* pz = zbuf[kk % 3];                       // p (FULL: p_prev)
-    const double* zp = FULL ? zbuf[(kk + 1) % 3] : nullptr; // z+ (FULL)
-    double* out = FULL ? zbuf[(kk + 2) % 3] : zbuf[(kk + 1) % 3];
-    const double* dA = FULL ? ebuf[(kk + 1) % 2] : ebuf[kk % 2];   // dual whose L^T makes z_half
-    const double* dP = FULL ? ebuf[kk % 2] : nullptr;               // d_prev
-    const double* src = FULL ? zp : pz;                              // primal the half step starts from
-    const int nx = p.nx, nu = p.nu;
+    const glbd* pz = pick3(bf, kk);                        // p (FULL: p_prev)
+    const glbd* zp = pick3(bf, kk + 1);                    // z+ (FULL)
+    glbd* out = FULL ? pick3(bf, kk + 2) : pick3(bf, kk + 1);
+    const glbd* dA = FULL ? pick2(bf, kk + 1) : pick2(bf, kk);   // dual whose L^T makes z_half
+    const glbd* dP = pick2(bf, kk);                              // d_prev (FULL)
+    const glbd* src = FULL ? zp : pz;                            // primal the half step starts from
+    const glbd* xi2g = (const glbd*)xi2;
+    const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
     double m0 = 0.0, m1 = 0.0, m3 = 0.0, m4 = 0.0;   // |xi0| |xi1| |delta0| |delta1|
     auto account = [&](int e, double lt_half, double w, double ltxi2) {
         // e: flat primal index; lt_half = L^T(eta+) (FULL) ; returns nothing
@@ -506,7 +516,6 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
             // x / u rows: sum over children of sqrtQ_j eta3_j (sqrtR_j eta4_j) + Gamma' eta7
             const bool isx = r < nx;
             const int rr = isx ? r : r - nx;
-            const int dim = isx ? nx : nu;
             double accA = 0.0, accW = 0.0, accC = 0.0;
             if (o7 >= 0) {
                 const int e = o7 + (isx ? rr : nx + rr);
@@ -515,14 +524,15 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
             }
             for (int q = 0; q < c; ++q) {
                 const int j = cs + q;
-                const double* M = isx ? p.SQ + (size_t)p.iSQ[j] * nx * nx : p.SR + (size_t)p.iSR[j] * nu * nu;
-                const int eb = isx ? e3(p, j) : e4(p, j);
                 double sA = 0.0, sW = 0.0, sC = 0.0;
-                for (int k = 0; k < dim; ++k) {
-                    const double mk = M[k * dim + rr];
-                    const double va = dA[eb + k];
-                    sA = fma(mk, va, sA);
-                    if (FULL) { sW = fma(mk, dP[eb + k] - va, sW); sC = fma(mk, xi2[eb + k], sC); }
+                if (isx) {
+                    const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
+                    const int eb = e3(p, j);
+                    dot_lt3<NXc, FULL>(M + rr, nx, dA + eb, dP + eb, xi2g + eb, nx, sA, sW, sC);
+                } else {
+                    const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
+                    const int eb = e4(p, j);
+                    dot_lt3<NUc, FULL>(M + rr, nu, dA + eb, dP + eb, xi2g + eb, nu, sA, sW, sC);
                 }
                 accA += sA;
                 if (FULL) { accW += sW; accC += sC; }
@@ -600,12 +610,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
             const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
             const int eb = e11(p, l);
             double sA = 0.0, sW = 0.0, sC = 0.0;
-            for (int k = 0; k < nx; ++k) {
-                const double mk = M[k * nx + r];
-                const double va = dA[eb + k];
-                sA = fma(mk, va, sA);
-                if (FULL) { sW = fma(mk, dP[eb + k] - va, sW); sC = fma(mk, xi2[eb + k], sC); }
-            }
+            dot_lt3<NXc, FULL>(M + r, nx, dA + eb, dP + eb, xi2g + eb, nx, sA, sW, sC);
             const int o14 = p.e14off[l - p.m];
             if (o14 >= 0) {
                 sA += dA[o14 + r];
@@ -617,10 +622,11 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
         }
     }
     if (FULL) {
-        block_max_atomic(m0, &ctl->red[0], s_red[0]);
-        block_max_atomic(m1, &ctl->red[1], s_red[1]);
-        block_max_atomic(m3, &ctl->red[3], s_red[2]);
-        block_max_atomic(m4, &ctl->red[4], s_red[3]);
+        double* prow = part + (size_t)blockIdx.x * 6;
+        block_max_store(m0, prow + 0, s_red[0]);
+        block_max_store(m1, prow + 1, s_red[1]);
+        block_max_store(m3, prow + 3, s_red[2]);
+        block_max_store(m4, prow + 4, s_red[3]);
     }
 }
 
@@ -655,10 +661,10 @@ __device__ __forceinline__ double box_apply(double v, double lo, double hi, Ctl*
 // bit1 process the nonleaf part (eta1..eta7, SOC per child); bit2 the leaf part (eta11..eta14).
 enum { kDualProx = 1, kDualNonleaf = 2, kDualLeaf = 4, kDualAll = 7 };
 
-template <bool WITH_L>
-__global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl, double* const* zbuf,
-                                                     double* const* ebuf, double* __restrict__ xi2, double* dsolo,
-                                                     int nbA, int nbB, int mode) {
+template <bool WITH_L, int NXc, int NUc>
+__global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl, Bufs bf,
+                                                     double* __restrict__ xi2, double* dsolo,
+                                                     double* __restrict__ part, int nbA, int nbB, int mode) {
     __shared__ double s_x[kBlock];
     __shared__ double s_red[2][kBlock / 64];
     if (WITH_L && ctl->done) return;
@@ -670,11 +676,11 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
     const bool prox = WITH_L || (mode & kDualProx);
     const int kk = WITH_L ? ctl->k : 0;
     const double alpha = ctl->alpha;
-    const double* pz = WITH_L ? zbuf[kk % 3] : nullptr;
-    const double* zp = WITH_L ? zbuf[(kk + 1) % 3] : nullptr;
-    const double* d = WITH_L ? ebuf[kk % 2] : dsolo;
-    double* eo = WITH_L ? ebuf[(kk + 1) % 2] : dsolo;
-    const int nx = p.nx, nu = p.nu;
+    const glbd* pz = pick3(bf, kk);
+    const glbd* zp = pick3(bf, kk + 1);
+    const glbd* d = WITH_L ? pick2(bf, kk) : (const glbd*)dsolo;
+    glbd* eo = WITH_L ? pick2(bf, kk + 1) : (glbd*)dsolo;
+    const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
     double m2 = 0.0, m5 = 0.0;
     // finalize one dual element given a = L(2z+ - p)[e], b = L(z+ - p)[e], projection result pv of v
     auto finish = [&](int e, double v, double pv, double b) {
@@ -702,28 +708,18 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
                 e = e3(p, j) + r;
                 if (WITH_L) {
                     const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
-                    const double* xz = zp + p.X0 + (size_t)a * nx;
-                    const double* xp = pz + p.X0 + (size_t)a * nx;
-                    for (int k = 0; k < nx; ++k) {
-                        const double mk = M[k * nx + r];
-                        const double zk = xz[k], pk = xp[k];
-                        av = fma(mk, 2.0 * zk - pk, av);
-                        bb = fma(mk, zk - pk, bb);
-                    }
+                    const glbd* xz = zp + p.X0 + (size_t)a * nx;
+                    const glbd* xp = pz + p.X0 + (size_t)a * nx;
+                    dot_zp<NXc>(M + r, nx, xz, xp, nx, av, bb);
                 }
             } else if (r < nx + nu) {
                 const int rr = r - nx;
                 e = e4(p, j) + rr;
                 if (WITH_L) {
                     const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
-                    const double* uz = zp + p.U0 + (size_t)a * nu;
-                    const double* up = pz + p.U0 + (size_t)a * nu;
-                    for (int k = 0; k < nu; ++k) {
-                        const double mk = M[k * nu + rr];
-                        const double zk = uz[k], pk = up[k];
-                        av = fma(mk, 2.0 * zk - pk, av);
-                        bb = fma(mk, zk - pk, bb);
-                    }
+                    const glbd* uz = zp + p.U0 + (size_t)a * nu;
+                    const glbd* up = pz + p.U0 + (size_t)a * nu;
+                    dot_zp<NUc>(M + rr, nu, uz, up, nu, av, bb);
                 }
             } else {
                 e = (r == nx + nu ? p.E5 : p.E6) + j;
@@ -772,8 +768,8 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
                 const int e = p.E2 + i;
                 double av = 0.0, bb = 0.0;
                 if (WITH_L) {
-                    const double* yz = zp + p.Y0 + yo;
-                    const double* yp = pz + p.Y0 + yo;
+                    const glbd* yz = zp + p.Y0 + yo;
+                    const glbd* yp = pz + p.Y0 + yo;
                     double bya = 0.0, byb = 0.0;
                     for (int k = 0; k < c; ++k) {
                         const double cp = p.cond[cs + k];
@@ -823,13 +819,9 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
                 e = e11(p, l) + r;
                 if (WITH_L) {
                     const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
-                    const double* xz = zp + p.X0 + (size_t)l * nx;
-                    const double* xp = pz + p.X0 + (size_t)l * nx;
-                    for (int k = 0; k < nx; ++k) {
-                        const double mk = M[k * nx + r];
-                        av = fma(mk, 2.0 * xz[k] - xp[k], av);
-                        bb = fma(mk, xz[k] - xp[k], bb);
-                    }
+                    const glbd* xz = zp + p.X0 + (size_t)l * nx;
+                    const glbd* xp = pz + p.X0 + (size_t)l * nx;
+                    dot_zp<NXc>(M + r, nx, xz, xp, nx, av, bb);
                 }
             } else if (r < nx + 2) {
                 e = (r == nx ? p.E12 : p.E13) + l;
@@ -872,8 +864,9 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
         }
     }
     if (WITH_L) {
-        block_max_atomic(m2, &ctl->red[2], s_red[0]);
-        block_max_atomic(m5, &ctl->red[5], s_red[1]);
+        double* prow = part + (size_t)blockIdx.x * 6;
+        block_max_store(m2, prow + 2, s_red[0]);
+        block_max_store(m5, prow + 5, s_red[1]);
     }
 }
 
@@ -892,16 +885,24 @@ __global__ void k_zero_idx(double* __restrict__ x, const int* __restrict__ idx, 
 }
 
 // end of iteration: record residuals, stopping test (solver.py:137-161)
-__global__ void k_cp_check(Ctl* ctl, double* hist) {
+__global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, const double* __restrict__ part,
+                                                      int rows) {
+    __shared__ double s_m[6][kBlock];
     if (ctl->done) return;
-    const int k = ctl->k;
-    double e[6];
-    for (int q = 0; q < 6; ++q) {
-        e[q] = __longlong_as_double((long long)ctl->red[q]);
-        hist[(size_t)k * 6 + q] = e[q];
-        ctl->red[q] = 0ull;
+    double m[6] = {0, 0, 0, 0, 0, 0};
+    for (int r = threadIdx.x; r < rows; r += blockDim.x)
+        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = fmax(m[q], part[(size_t)r * 6 + q]);
+    _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = m[q];
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = fmax(s_m[q][threadIdx.x], s_m[q][threadIdx.x + w]);
+        __syncthreads();
     }
-    const double err = fmax(fmax(e[0], e[1]), e[2]);
+    if (threadIdx.x != 0) return;
+    const int k = ctl->k;
+    for (int q = 0; q < 6; ++q) hist[(size_t)k * 6 + q] = s_m[q][0];
+    const double err = fmax(fmax(s_m[0][0], s_m[1][0]), s_m[2][0]);
     if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
         ctl->done = 1;
         ctl->final_k = k;

@@ -24,7 +24,7 @@ EXPORTED_SYMBOLS = [
     "raocp_prox_f", "raocp_relax_s0", "raocp_project_on_dynamics", "raocp_project_on_kernel", "raocp_prox_gconj",
     "raocp_step_size", "raocp_cp_run", "raocp_cp_bench", "raocp_op_bench",
     "raocp_dual_scale", "raocp_dual_add_halves", "raocp_dual_project", "raocp_dual_moreau",
-    "raocp_device_synchronize",
+    "raocp_device_synchronize", "raocp_debug_dyn_stamps",
 ]
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -44,9 +44,9 @@ class ProblemDesc(ctypes.Structure):
                 ("n_box_nl", ctypes.c_int32), ("n_box_l", ctypes.c_int32),
                 ("box_nl_lo", _f64p), ("box_nl_hi", _f64p), ("box_l_lo", _f64p), ("box_l_hi", _f64p),
                 ("i_box_nl", _i32p), ("i_box_l", _i32p),
-                ("n_b", ctypes.c_int32), ("n_abar", ctypes.c_int32), ("n_pb", ctypes.c_int32), ("n_k", ctypes.c_int32),
-                ("B", _f64p), ("Abar", _f64p), ("PB", _f64p), ("K", _f64p), ("Rinv", _f64p),
-                ("i_b", _i32p), ("i_abar", _i32p), ("i_pb", _i32p), ("i_k", _i32p)]
+                ("n_a", ctypes.c_int32), ("n_b", ctypes.c_int32), ("n_k", ctypes.c_int32),
+                ("A", _f64p), ("B", _f64p), ("K", _f64p), ("Rinv", _f64p), ("M", _f64p),
+                ("i_a", _i32p), ("i_b", _i32p), ("i_k", _i32p)]
 
 
 class RaocpError(RuntimeError):
@@ -94,6 +94,7 @@ def load_library():
         "raocp_dual_project": (c_int, [vp, c_int]),
         "raocp_dual_moreau": (c_int, [vp, c_double, vp]),
         "raocp_device_synchronize": (c_int, [c_int]),
+        "raocp_debug_dyn_stamps": (c_int, [vp, vp, c_int]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)
@@ -138,8 +139,8 @@ class NativeContext:
             i(p.i_sq), i(p.i_sr), i(p.i_sp), f(p.alpha_r), f(p.cond),
             p.n_box_nl, p.n_box_l, f(p.box_nl_lo), f(p.box_nl_hi), f(p.box_l_lo), f(p.box_l_hi),
             i(p.i_box_nl), i(p.i_box_l),
-            p.B.shape[0], p.Abar.shape[0], p.PB.shape[0], p.K.shape[0],
-            f(p.B), f(p.Abar), f(p.PB), f(p.K), f(p.Rinv), i(p.i_b), i(p.i_abar), i(p.i_pb), i(p.i_k))
+            p.A.shape[0], p.B.shape[0], p.K.shape[0],
+            f(p.A), f(p.B), f(p.K), f(p.Rinv), f(p.M), i(p.i_a), i(p.i_b), i(p.i_k))
         self.device = _default_device() if device is None else device
         h = ctypes.c_void_p()
         self._check(self._lib.raocp_ctx_create(ctypes.byref(self.tree_desc), ctypes.byref(self.prob_desc),
@@ -272,6 +273,11 @@ class NativeContext:
         ms = ctypes.c_float()
         self._check(self._lib.raocp_cp_bench(self._h, _ptr(x0), int(iters), float(alpha), ctypes.byref(ms)))
         return ms.value
+
+    def debug_dyn_stamps(self, cap=128):
+        out = np.zeros(cap, dtype=np.uint64)
+        self._check(self._lib.raocp_debug_dyn_stamps(self._h, _ptr(out), int(cap)))
+        return out
 
     def op_bench(self, op, reps):
         ms = ctypes.c_float()

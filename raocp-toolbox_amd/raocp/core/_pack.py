@@ -13,10 +13,10 @@ What it produces
     from each node's risk object so the device sees the reference's exact doubles;
   * the offline products of the dynamics projection (cache.py:207-233): for every
     nonleaf node R~ = I + sum B'PB, K = -R~^-1 sum B'PA, Abar_j = A_j + B_j K,
-    P = I + K'K + sum Abar'P Abar. Nodes whose subtrees have the same signature
-    (same child dynamics, same child classes) get bit-identical results, so they
-    are computed once per class with the reference's numpy/
-    scipy calls and evaluation order (cho_factor / cho_solve).
+    P = I + K'K + sum Abar'P Abar, plus M = K' + sum Abar'PB. Nodes whose subtrees
+    have the same signature (same child dynamics, same child classes) get
+    bit-identical results, so they are computed once per class (SURVEY.md 8(f)
+    row 2) with the reference's numpy/scipy calls (cho_factor / cho_solve).
 """
 import numpy as np
 import scipy.linalg
@@ -151,15 +151,20 @@ def pack_problem(spec):
         i_box_l[l] = box_index(spec.leaf_constraint_at_node(l), nx, box_l, ids_l)
 
     # ---- offline dynamics products per subtree class (cache.py:207-233)
+    # For the device sweep (raocp_dyn.hip) the backward recursion is re-associated as
+    #   h = sum_j B_j' q_j,  a = sum_j A_j' q_j,  d = Rinv (u - h),
+    #   q = (-x + K'(h - u)) + a + M d,   M = K' + sum_j Abar_j' P_j B_j
+    # and the forward one as x_j = A_j x + B_j u (u = K x + d), so only the per-mode
+    # A, B and per-class Rinv, K, M are needed. Classes are numbered by stage.
     I_x, I_u = np.eye(nx), np.eye(nu)
     A_tab, B_tab = t_a.array(), t_b.array()
-    cls = np.zeros(n, dtype=np.int64)   # class 0: leaf, P = I
-    P_cls = [I_x]
-    K_cls, Rinv_cls = [np.zeros((nu, nx))], [np.zeros((nu, nu))]
-    memo, abar_memo, pb_memo = {}, {}, {}
-    abar_tab, pb_tab = [], []
-    i_abar = np.zeros(n, dtype=np.int64)
-    i_pb = np.zeros(n, dtype=np.int64)
+    cls = np.full(n, -1, dtype=np.int64)   # -1: leaf (P = I)
+    P_cls, K_cls, Rinv_cls, M_cls, stage_cls = [], [], [], [], []
+    memo = {}
+
+    def P_of(j):
+        return I_x if cls[j] < 0 else P_cls[cls[j]]
+
     for i in range(m - 1, -1, -1):
         kids = range(ch_start[i], ch_start[i] + nch[i])
         key = tuple((int(i_a[j]), int(i_b[j]), int(cls[j])) for j in kids)
@@ -167,35 +172,35 @@ def pack_problem(spec):
         if ci is None:
             sum_r, sum_k = 0, 0
             for j in kids:
-                Bj, Aj, Pj = B_tab[i_b[j]], A_tab[i_a[j]], P_cls[cls[j]]
+                Bj, Aj, Pj = B_tab[i_b[j]], A_tab[i_a[j]], P_of(j)
                 sum_r = sum_r + Bj.T @ Pj @ Bj
                 sum_k = sum_k + Bj.T @ Pj @ Aj
             cho = scipy.linalg.cho_factor(I_u + sum_r)
             K = scipy.linalg.cho_solve(cho, -sum_k)
             sum_p = 0
+            Mc = K.T.copy()
             for j in kids:
-                Bj, Aj, Pj = B_tab[i_b[j]], A_tab[i_a[j]], P_cls[cls[j]]
+                Bj, Aj, Pj = B_tab[i_b[j]], A_tab[i_a[j]], P_of(j)
                 Ab = Aj + Bj @ K
                 sum_p = sum_p + Ab.T @ Pj @ Ab
+                Mc = Mc + Ab.T @ (Pj @ Bj)
             ci = len(P_cls)
             memo[key] = ci
             P_cls.append(I_x + K.T @ K + sum_p)
             K_cls.append(K)
             Rinv_cls.append(scipy.linalg.cho_solve(cho, I_u))
+            M_cls.append(Mc)
+            stage_cls.append(int(stage[i]))
         cls[i] = ci
-        for j in kids:
-            akey = (int(i_a[j]), int(i_b[j]), int(ci))
-            if akey not in abar_memo:
-                abar_memo[akey] = len(abar_tab)
-                abar_tab.append(A_tab[i_a[j]] + B_tab[i_b[j]] @ K_cls[ci])
-            i_abar[j] = abar_memo[akey]
-    for j in range(1, n):
-        pkey = (int(cls[j]), int(i_b[j]))
-        if pkey not in pb_memo:
-            pb_memo[pkey] = len(pb_tab)
-            pb_tab.append(P_cls[cls[j]] @ B_tab[i_b[j]])
-        i_pb[j] = pb_memo[pkey]
-    i_k = cls[:m]
+    # renumber classes by stage (a class is stage-specific: equal subtree signature => equal height)
+    order = np.argsort(np.asarray(stage_cls), kind="stable")
+    new_id = np.empty(len(order), dtype=np.int64)
+    new_id[order] = np.arange(len(order))
+    i_k = new_id[cls[:m]]
+    K_tab = _f64(np.stack([K_cls[o] for o in order]))
+    Rinv_tab = _f64(np.stack([Rinv_cls[o] for o in order]))
+    M_tab = _f64(np.stack([M_cls[o] for o in order]))
+    class_stage = np.asarray(stage_cls, dtype=np.int64)[order]
 
     def stack(lst, shape):
         return _f64(np.stack(lst)) if lst else np.zeros((1,) + shape)
@@ -215,9 +220,8 @@ def pack_problem(spec):
         alpha_r=_f64(alpha_r), cond=_f64(cond),
         n_box_nl=len(box_nl), n_box_l=len(box_l), box_nl_lo=lo_nl, box_nl_hi=hi_nl, box_l_lo=lo_l, box_l_hi=hi_l,
         i_box_nl=_i32(i_box_nl), i_box_l=_i32(i_box_l),
-        B=B_tab, Abar=stack(abar_tab, (nx, nx)), PB=stack(pb_tab, (nx, nu)),
-        K=_f64(np.stack(K_cls)), Rinv=_f64(np.stack(Rinv_cls)),
-        i_b=_i32(i_b), i_abar=_i32(i_abar), i_pb=_i32(i_pb), i_k=_i32(i_k),
-        n_classes=len(P_cls),
+        A=A_tab, B=B_tab, K=K_tab, Rinv=Rinv_tab, M=M_tab,
+        i_a=_i32(i_a), i_b=_i32(i_b), i_k=_i32(i_k), class_stage=_i32(class_stage),
+        n_classes=len(order),
         l_error=t_sq.mismatch or t_sr.mismatch or t_sp.mismatch,
     )
