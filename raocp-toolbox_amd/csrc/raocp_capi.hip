@@ -50,8 +50,26 @@ struct raocp_ctx {
     double* Z[3] = {nullptr, nullptr, nullptr};
     double* E[2] = {nullptr, nullptr};
     double* XI2 = nullptr;
-    double* q = nullptr;
-    double* d = nullptr;
+    double* q = nullptr;         // q rows of the cut stage, padded (n x KP)
+    double* d = nullptr;         // d rows (m x nu)
+    // per-stage dynamics path: padded global rows
+    double* gXQ = nullptr;       // n x KP  (x, then q)
+    double* gU = nullptr;        // m x NUP
+    double* gXD = nullptr;       // m x KF  ([x | d | 0])
+    double* gP = nullptr;        // n x PS  (child products)
+    int KP = 0, KF = 0, NUP = 0, PS = 0;
+    int maxch_top = 0;
+    std::vector<int> cls_ptr;    // first class of each stage (size N+1)
+    std::vector<int> pair_ptr;   // first (kind, class) pair of each class (size n_k+1)
+    int nkind = 0;
+    bool f_lds_top = false;      // F table staged in LDS by k_dyn_top
+    struct TierPlan {            // a tier [s0, s1) below the top: one workgroup per subtree
+        int s0, s1, nsub, maxch;
+        size_t lds_b, lds_f;
+        bool fl;                 // F staged in LDS by the forward kernel
+        const raocp::Rec* lv;    // level ranges of its subtrees
+    };
+    std::vector<TierPlan> tiers;
     double* x0 = nullptr;
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
     Ctl* ctl = nullptr;
@@ -65,10 +83,10 @@ struct raocp_ctx {
     double* part = nullptr;      // dot-product partials
     double* scal = nullptr;      // device scalars
     int cut = 0;                 // dynamics cut stage (0: per-stage kernels)
-    std::vector<int> cls_ptr_h;  // first class id per stage
     double* redpart = nullptr;   // per-block residual maxima [red_rows][6]
     int red_rows = 0;
-    size_t lds_top = 0, lds_bb = 0, lds_bf = 0;
+    size_t lds_top = 0;
+    int dyn_block = 1024;
     const int* ph = nullptr;     // dual placeholder offsets
     int n_ph = 0;
     bool has_x0 = false;
@@ -196,37 +214,51 @@ struct DynOp {
     template <int NX, int NU>
     void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl) {
         const int s = c->cut;
+        const int B = c->dyn_block;
         if (s > 0) {
-            // subtree-blocked: bottom backward, top (backward + forward), bottom forward
-            const int nsub = c->stage_ptr[s + 1] - c->stage_ptr[s];
-            if (s < c->N) {
+            // tiers below the top, deepest first (backward), the top, then the tiers (forward)
+            for (int k = (int)c->tiers.size() - 1; k >= 0; --k) {
+                const auto& tp = c->tiers[k];
+                const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1];
                 auto kb = raocp::k_dyn_bottom_back<NX, NU>;
-                allow_lds(kb, c->lds_bb);
-                kb<<<nsub, 512, c->lds_bb, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->d, s);
+                allow_lds(kb, tp.lds_b);
+                kb<<<tp.nsub, B, tp.lds_b, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->d, tp.s0, tp.s1, tp.maxch, c0, c1,
+                                                        tp.lv);
             }
-            auto kt = raocp::k_dyn_top<NX, NU>;
-            allow_lds(kt, c->lds_top);
-            kt<<<1, 1024, c->lds_top, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->x0, s);
-            if (s < c->N) {
-                auto kf = raocp::k_dyn_bottom_fwd<NX, NU>;
-                allow_lds(kf, c->lds_bf);
-                kf<<<nsub, 512, c->lds_bf, c->stream>>>(c->dev, bf, ctl, zsel, c->d, s);
+            {
+                const int c1 = c->cls_ptr[s], p1 = c->pair_ptr[c1];
+                auto kt = c->f_lds_top ? raocp::k_dyn_top<NX, NU, true> : raocp::k_dyn_top<NX, NU, false>;
+                allow_lds(kt, c->lds_top);
+                const int T = c->stage_ptr[s], nb = c->stage_ptr[s + 1] - T;
+                kt<<<1, B, c->lds_top, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->x0, s, c->maxch_top, c1, p1, T, nb);
+            }
+            for (const auto& tp : c->tiers) {
+                const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1], p0 = c->pair_ptr[c0], p1 = c->pair_ptr[c1];
+                auto kf = tp.fl ? raocp::k_dyn_bottom_fwd<NX, NU, true> : raocp::k_dyn_bottom_fwd<NX, NU, false>;
+                allow_lds(kf, tp.lds_f);
+                kf<<<tp.nsub, B, tp.lds_f, c->stream>>>(c->dev, bf, ctl, zsel, c->d, tp.s0, tp.s1, c0, c1, p0, p1, tp.lv);
             }
             return;
         }
-        const int G = std::max(c->nx, c->nu);
+        // per-stage path on padded global rows
+        const int R = c->nu + c->nx;
+        raocp::k_dyn_gather<NX, NU><<<std::max(1, std::min(1024, cdiv(c->n * c->KP, kBlock))), kBlock, 0, c->stream>>>(
+            c->dev, bf, ctl, zsel, c->gXQ, c->gU, c->gXD);
         for (int t = c->N - 1; t >= 0; --t) {
             const int b = c->stage_ptr[t], e = c->stage_ptr[t + 1];
-            const Launch L = groups(G, e - b);
-            if (L.blocks)
-                raocp::k_dyn_back_stage<NX, NU><<<L.blocks, kBlock, 0, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->d,
-                                                                                     b, e);
+            const int cb = e, ce = c->stage_ptr[t + 2];
+            const int slots_a = B / (R * raocp::kKS), slots_b = B / R;
+            raocp::k_dyn_stage_a<NX, NU><<<cdiv(ce - cb, slots_a), B, 0, c->stream>>>(
+                c->dev, ctl, c->gXQ, c->gP, cb, ce, t + 1 == c->N ? -1.0 : 1.0);
+            raocp::k_dyn_stage_b<NX, NU><<<cdiv(e - b, slots_b), B, 0, c->stream>>>(c->dev, ctl, c->gXQ, c->gU,
+                                                                                         c->gP, c->gXD, c->d, b, e);
         }
+        const int per_node = c->nu * raocp::kKS + c->cmax * c->nx * raocp::kKS;
+        const int slots_f = std::max(1, B / per_node);
         for (int t = 0; t < c->N; ++t) {
             const int b = c->stage_ptr[t], e = c->stage_ptr[t + 1];
-            const int nkids = c->stage_ptr[t + 2] - c->stage_ptr[t + 1];
-            const int blocks = groups(c->nu, e - b).blocks + groups(c->nx, nkids).blocks;
-            raocp::k_dyn_fwd_stage<NX, NU><<<blocks, kBlock, 0, c->stream>>>(c->dev, bf, ctl, zsel, c->d, c->x0, b, e);
+            raocp::k_dyn_stage_f<NX, NU><<<cdiv(e - b, slots_f), B, 0, c->stream>>>(c->dev, bf, ctl, zsel, c->gXD,
+                                                                                         c->x0, b, e);
         }
     }
 };
@@ -487,98 +519,266 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         (rc = c->upload_vec(&D.blo_l, lo_l)) || (rc = c->upload_vec(&D.bhi_l, hi_l)) ||
         (rc = c->upload(&D.iBnl, pr->i_box_nl, m)) || (rc = c->upload(&D.iBl, pr->i_box_l, n)))
         return bail(rc);
-    // dynamics tables, padded for the lanes-over-rows access (raocp_dyn.hip header)
+    // dynamics tables (raocp_dyn.hip header): per child kind W = [B'; A'], per class
+    // RG = [R~^-1; G = M R~^-1 - K'] and K, per (kind, parent class) pair F = [A + B K | B]
+    const int R = nx + nu;
+    const int KP = raocp::rup(nx, 2 * raocp::kKS), KF = raocp::rup(nx + nu, 2 * raocp::kKS), NUP = raocp::rup(nu, 2);
+    c->KP = KP; c->KF = KF; c->NUP = NUP; c->PS = NUP + raocp::rup(nx, 2);
+    const int SKP = raocp::tstride(KP), SKF = raocp::tstride(KF), SNU = raocp::tstride(NUP);  // table row strides
+    if (R * raocp::kKS > raocp::kDynBlock)
+        return bail(fail(RAOCP_ERR_ARG, "nx + nu > 256 is not supported by the dynamics sweep"));
     {
-        auto pad_rm = [](const double* src, int cnt, int rows, int cols) {  // [t][r][c] at r*(cols+1)+c
-            std::vector<double> out((size_t)cnt * rows * (cols + 1), 0.0);
-            for (int t = 0; t < cnt; ++t)
-                for (int r = 0; r < rows; ++r)
-                    for (int k = 0; k < cols; ++k)
-                        out[(size_t)t * rows * (cols + 1) + (size_t)r * (cols + 1) + k] =
-                            src[(size_t)t * rows * cols + (size_t)r * cols + k];
-            return out;
-        };
-        auto pad_cm = [](const double* src, int cnt, int rows, int cols) {  // [t] M(r,c) at c*(rows+1)+r
-            std::vector<double> out((size_t)cnt * cols * (rows + 1), 0.0);
-            for (int t = 0; t < cnt; ++t)
-                for (int r = 0; r < rows; ++r)
-                    for (int k = 0; k < cols; ++k)
-                        out[(size_t)t * cols * (rows + 1) + (size_t)k * (rows + 1) + r] =
-                            src[(size_t)t * rows * cols + (size_t)r * cols + k];
-            return out;
-        };
-        D.nA = pr->n_a;
-        D.nB = pr->n_b;
-        if ((rc = c->upload_vec(&D.Ap, pad_rm(pr->A, pr->n_a, nx, nx))) ||
-            (rc = c->upload_vec(&D.Bp, pad_rm(pr->B, pr->n_b, nx, nu))) ||
-            (rc = c->upload_vec(&D.Rp, pad_cm(pr->Rinv, pr->n_k, nu, nu))) ||
-            (rc = c->upload_vec(&D.Kp, pad_rm(pr->K, pr->n_k, nu, nx))) ||
-            (rc = c->upload_vec(&D.Mp, pad_cm(pr->M, pr->n_k, nx, nu))))
+        const int nk = pr->n_k;
+        for (int j = 1; j < n; ++j)
+            if (pr->i_a[j] < 0 || pr->i_a[j] >= pr->n_a || pr->i_b[j] < 0 || pr->i_b[j] >= pr->n_b)
+                return bail(fail(RAOCP_ERR_ARG, "dynamics index out of range"));
+        for (int i = 0; i < m; ++i)
+            if (pr->i_k[i] < 0 || pr->i_k[i] >= nk) return bail(fail(RAOCP_ERR_ARG, "class index out of range"));
+        auto A = [&](int t, int r, int k) { return pr->A[((size_t)t * nx + r) * nx + k]; };
+        auto Bm = [&](int t, int r, int k) { return pr->B[((size_t)t * nx + r) * nu + k]; };
+        auto K = [&](int c_, int r, int k) { return pr->K[((size_t)c_ * nu + r) * nx + k]; };
+        auto Ri = [&](int c_, int r, int k) { return pr->Rinv[((size_t)c_ * nu + r) * nu + k]; };
+        auto M = [&](int c_, int r, int k) { return pr->M[((size_t)c_ * nx + r) * nu + k]; };
+        // child kinds (A, B index pairs) and (kind, parent class) pairs
+        std::vector<int> kind(n, 0), pair(n, 0);
+        std::vector<std::pair<int, int>> kinds, pairs;
+        {
+            std::vector<std::pair<std::pair<int, int>, int>> seen_k;
+            std::vector<std::pair<std::pair<int, int>, int>> seen_p;
+            auto find = [](std::vector<std::pair<std::pair<int, int>, int>>& v, std::pair<int, int> key, int next) {
+                for (auto& e : v)
+                    if (e.first == key) return e.second;
+                v.push_back({key, next});
+                return next;
+            };
+            for (int j = 1; j < n; ++j) {
+                const std::pair<int, int> kk{pr->i_a[j], pr->i_b[j]};
+                const int kid = find(seen_k, kk, (int)kinds.size());
+                if (kid == (int)kinds.size()) kinds.push_back(kk);
+                kind[j] = kid;
+                const std::pair<int, int> pk{kid, pr->i_k[t->anc[j]]};
+                const int pid = find(seen_p, pk, (int)pairs.size());
+                if (pid == (int)pairs.size()) pairs.push_back(pk);
+                pair[j] = pid;
+            }
+        }
+        // number pairs by parent class (so the pairs of a stage range are contiguous)
+        {
+            std::vector<int> order(pairs.size());
+            for (size_t q = 0; q < order.size(); ++q) order[q] = (int)q;
+            std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pairs[a].second < pairs[b].second; });
+            std::vector<int> newid(pairs.size());
+            std::vector<std::pair<int, int>> sorted(pairs.size());
+            for (size_t q = 0; q < order.size(); ++q) {
+                newid[order[q]] = (int)q;
+                sorted[q] = pairs[order[q]];
+            }
+            pairs = sorted;
+            for (int j = 1; j < n; ++j) pair[j] = newid[pair[j]];
+        }
+        // classes must be numbered by stage: stage t owns classes [cls_ptr[t], cls_ptr[t+1])
+        c->cls_ptr.assign(N + 1, nk);
+        for (int i = m - 1; i >= 0; --i) c->cls_ptr[t->stage[i]] = std::min(c->cls_ptr[t->stage[i]], pr->i_k[i]);
+        for (int st = N - 1; st >= 0; --st) c->cls_ptr[st] = std::min(c->cls_ptr[st], c->cls_ptr[st + 1]);
+        for (int i = 0; i < m; ++i)
+            if (pr->i_k[i] < c->cls_ptr[t->stage[i]] || pr->i_k[i] >= c->cls_ptr[t->stage[i] + 1])
+                return bail(fail(RAOCP_ERR_ARG, "classes must be numbered by stage"));
+        c->pair_ptr.assign(nk + 1, (int)pairs.size());
+        for (int q = (int)pairs.size() - 1; q >= 0; --q) c->pair_ptr[pairs[q].second] = q;
+        for (int c_ = nk - 1; c_ >= 0; --c_) c->pair_ptr[c_] = std::min(c->pair_ptr[c_], c->pair_ptr[c_ + 1]);
+        c->nkind = (int)kinds.size();
+        D.nkind = c->nkind;
+        std::vector<double> W(std::max<size_t>(1, kinds.size()) * R * SKP, 0.0);
+        for (size_t q = 0; q < kinds.size(); ++q)
+            for (int rho = 0; rho < R; ++rho)
+                for (int k = 0; k < nx; ++k)
+                    W[(q * R + rho) * SKP + k] =
+                        rho < nu ? Bm(kinds[q].second, k, rho) : A(kinds[q].first, k, rho - nu);  // B', A'
+        std::vector<double> RG((size_t)nk * R * SNU, 0.0), KM((size_t)nk * nu * SKP, 0.0);
+        for (int c_ = 0; c_ < nk; ++c_) {
+            for (int r = 0; r < nu; ++r) {
+                for (int k = 0; k < nu; ++k) RG[((size_t)c_ * R + r) * SNU + k] = Ri(c_, r, k);
+                for (int k = 0; k < nx; ++k) KM[((size_t)c_ * nu + r) * SKP + k] = K(c_, r, k);
+            }
+            for (int r = 0; r < nx; ++r)
+                for (int k = 0; k < nu; ++k) {
+                    double g = 0.0;
+                    for (int t2 = 0; t2 < nu; ++t2) g += M(c_, r, t2) * Ri(c_, t2, k);
+                    RG[((size_t)c_ * R + nu + r) * SNU + k] = g - K(c_, k, r);
+                }
+        }
+        std::vector<double> F(std::max<size_t>(1, pairs.size()) * nx * SKF, 0.0);
+        for (size_t q = 0; q < pairs.size(); ++q) {
+            const int ia = kinds[pairs[q].first].first, ib = kinds[pairs[q].first].second, c_ = pairs[q].second;
+            for (int r = 0; r < nx; ++r) {
+                for (int k = 0; k < nx; ++k) {
+                    double bk = 0.0;
+                    for (int t2 = 0; t2 < nu; ++t2) bk += Bm(ib, r, t2) * K(c_, t2, k);
+                    F[(q * nx + r) * SKF + k] = A(ia, r, k) + bk;  // Abar = A + B K (cache.py:226)
+                }
+                for (int k = 0; k < nu; ++k) F[(q * nx + r) * SKF + nx + k] = Bm(ib, r, k);
+            }
+        }
+        if ((rc = c->upload_vec(&D.dW, W)) || (rc = c->upload_vec(&D.dRG, RG)) || (rc = c->upload_vec(&D.dKM, KM)) ||
+            (rc = c->upload_vec(&D.dF, F)))
             return bail(rc);
         std::vector<raocp::Rec> ninfo(m), cinfo(n);
-        std::vector<int> cls_ptr(N + 1, pr->n_k);
         for (int i = 0; i < m; ++i) ninfo[i] = raocp::Rec{t->ch_start[i], t->nch[i], pr->i_k[i], t->stage[i]};
         cinfo[0] = raocp::Rec{0, 0, -1, 0};
-        for (int j = 1; j < n; ++j) cinfo[j] = raocp::Rec{pr->i_a[j], pr->i_b[j], t->anc[j], 0};
-        for (int i = m - 1; i >= 0; --i) {
-            if (i + 1 < m && pr->i_k[i] > pr->i_k[i + 1] && t->stage[i] < t->stage[i + 1])
-                return bail(fail(RAOCP_ERR_ARG, "classes must be numbered by stage"));
-            cls_ptr[t->stage[i]] = std::min(cls_ptr[t->stage[i]], pr->i_k[i]);
-        }
-        for (int st = N - 1; st >= 0; --st) cls_ptr[st] = std::min(cls_ptr[st], cls_ptr[st + 1]);
-        c->cls_ptr_h = cls_ptr;
+        for (int j = 1; j < n; ++j) cinfo[j] = raocp::Rec{kind[j], pair[j], t->anc[j], 0};
         if ((rc = c->upload_vec(&D.ninfo, ninfo)) || (rc = c->upload_vec(&D.cinfo, cinfo)) ||
-            (rc = c->upload_vec(&D.cls_ptr, cls_ptr)) || (rc = c->upload_vec(&D.stage_ptr, c->stage_ptr)))
+            (rc = c->upload_vec(&D.stage_ptr, c->stage_ptr)))
             return bail(rc);
     }
     D.N = N;
 
-    // ---- dynamics plan: cut stage s (top = stages < s in one workgroup, one workgroup
-    // per subtree below; matrices + top state in LDS). Per-stage launches otherwise.
+    // ---- dynamics plan. The stages are split into tiers 0 = s_0 < s_1 < ... < s_T = N:
+    // tier 0 (stages < s_1) runs backward + forward in ONE workgroup (k_dyn_top); every
+    // deeper tier [s_k, s_k+1) runs one workgroup per subtree rooted at stage s_k
+    // (k_dyn_bottom_back / _fwd), its boundary being the leaves or the next tier's roots.
+    // Vectors and matrix tables live in LDS (F when it fits). The cut list minimises a
+    // cost model: a level costs one unit per phase plus its lane work over 384, a tier
+    // kernel five units of launch + prologue. Per-stage launches when nothing fits.
     {
-        const size_t kLds = 160 * 1024 - 1024;  // minus the static LDS of the kernels
-        const size_t SA = (size_t)nx * (nx + 1), SB = (size_t)nx * (nu + 1), SR = (size_t)nu * (nu + 1),
-                     SK = (size_t)nu * (nx + 1);
-        auto mats = [&](int c0, int c1) { return (size_t)pr->n_a * SA + pr->n_b * SB + (size_t)(c1 - c0) * (SR + 2 * SK); };
-        const std::vector<int>& cp = c->cls_ptr_h;
-        auto top_bytes = [&](int s) {
-            const size_t T = c->stage_ptr[s], nb = c->stage_ptr[s + 1] - T;
-            return 8 * (2 * 1024 + mats(0, cp[s]) + T * (2 * nx + 2 * nu) + nb * nx + 1) + 16 * (2 * T + nb);
+        const size_t kLds = 160 * 1024 - 2 * 1024;  // minus the static LDS (Prologue, ~1.2 KB)
+        const size_t W1 = (size_t)R * SKP, RG1 = (size_t)R * SNU, KM1 = (size_t)nu * SKP, F1 = (size_t)nx * SKF;
+        const std::vector<int>& cp = c->cls_ptr;
+        const std::vector<int>& pp = c->pair_ptr;
+        const int PS = c->PS;
+        auto stage_n = [&](int st) { return c->stage_ptr[st + 1] - c->stage_ptr[st]; };
+        auto level_cost = [&](double P, double C) { return 3.0 + (C * R + P * R + P * nu + C * nx) / 384.0; };
+        auto recs = [](size_t cnt) { return 2 * cnt; };  // 16-B records in doubles
+        auto top_bytes = [&](int s_, int& maxch, bool fl) {
+            const size_t T = c->stage_ptr[s_], nb = stage_n(s_);
+            maxch = 0;
+            for (int st = 1; st <= s_; ++st) maxch = std::max(maxch, stage_n(st));
+            const size_t mats = c->nkind * W1 + cp[s_] * (RG1 + KM1) + (fl ? pp[cp[s_]] * F1 : 0);
+            const size_t stage = T * (nx + nu) + (s_ == N ? nb * nx : 0) + 12;  // raw rows for the repack
+            const size_t dbl = mats + T * KP + nb * KP + T * NUP + T * KF + raocp::rup(maxch * PS, 2) +
+                               recs(T + T + nb - 1) + stage;
+            return 8 * dbl;
         };
-        auto sub_nonleaf = [&](int s) {  // max nonleaf count over the subtrees rooted at stage s
-            int best = 0;
-            for (int r = c->stage_ptr[s]; r < c->stage_ptr[s + 1]; ++r) {
-                int lo = r, hi = r + 1, acc = 0;
-                for (int st = s; st < N; ++st) {
-                    acc += hi - lo;
+        struct Tier {
+            size_t nall = 0, nnl = 0;
+            int maxch = 0;
+            double cost = 0;
+            size_t bb = 0, bf = 0;
+            bool fl = true, ok = false;
+        };
+        auto tier = [&](int a, int b) {  // subtrees rooted at stage a, levels a..b-1, boundary b (worst case)
+            Tier w;
+            if (b - a > raocp::kMaxLevels) return w;
+            std::vector<double> lvl(b - a, 0.0);
+            for (int r = c->stage_ptr[a]; r < c->stage_ptr[a + 1]; ++r) {
+                int lo = r, hi = r + 1, mc = 0;
+                size_t nall = 0;
+                for (int st = a; st < b; ++st) {
+                    nall += hi - lo;
                     const int nlo = t->ch_start[lo], nhi = t->ch_start[hi - 1] + t->nch[hi - 1];
+                    lvl[st - a] = std::max(lvl[st - a], level_cost(hi - lo, nhi - nlo));
+                    mc = std::max(mc, nhi - nlo);
                     lo = nlo;
                     hi = nhi;
                 }
-                best = std::max(best, acc);
+                w.nnl = std::max(w.nnl, nall);
+                w.nall = std::max(w.nall, nall + (hi - lo));
+                w.maxch = std::max(w.maxch, mc);
             }
-            return best;
+            for (double v : lvl) w.cost += v;
+            const size_t ncl = cp[b] - cp[a], npr = pp[cp[b]] - pp[cp[a]];
+            const size_t st_b = w.nall * nx + w.nnl * nu + 4 * (b - a + 2);  // staging of raw rows
+            const size_t st_f = w.nnl * nu + nx + 4 * (b - a + 2);
+            w.bb = 8 * (c->nkind * W1 + ncl * RG1 + w.nall * KP + w.nnl * NUP + raocp::rup(w.maxch * PS, 2) +
+                        recs(w.nnl + w.nall - 1) + st_b);
+            w.bf = 8 * (ncl * KM1 + npr * F1 + w.nnl * KF + recs(w.nnl + w.nall - 1) + st_f);
+            if (w.bf > kLds) {
+                w.fl = false;
+                w.bf -= 8 * npr * F1;
+                w.cost += 2 * (b - a);
+            }
+            w.cost += 10.0;  // two launches and their prologues
+            w.ok = w.bb <= kLds && w.bf <= kLds;
+            return w;
         };
-        c->cut = 0;
-        if (m <= 1024 && top_bytes(N) <= kLds) {
-            c->cut = N;
-        } else {
-            for (int s = 1; s < N; ++s) {
-                if (c->stage_ptr[s + 1] - c->stage_ptr[s] < 96 || N - s > raocp::kMaxLevels) continue;
-                if (top_bytes(s) > kLds) break;
-                const size_t snl = sub_nonleaf(s);
-                const size_t bb = 8 * (2 * 512 + mats(cp[s], cp[N]) + snl * nx);
-                const size_t bf = 8 * (mats(cp[s], cp[N]) + snl * (nx + nu));
-                if (bb > kLds || bf > kLds) continue;
-                c->cut = s;
-                c->lds_bb = bb;
-                c->lds_bf = bf;
-                break;
+        // f[a]: best cost of tiers covering [a, N); nxt[a]: the end of the first of them
+        std::vector<double> f(N + 1, 1e300);
+        std::vector<int> nxt(N + 1, N);
+        f[N] = 0.0;
+        int forced = -1;
+        if (const char* env = getenv("RAOCP_DYN_CUT")) forced = atoi(env);  // tier depth (diagnostics)
+        for (int a = N - 1; a >= 1; --a)
+            for (int b = a + 1; b <= N; ++b) {
+                if (forced > 0 && b - a != forced && b != N) continue;
+                if (f[b] >= 1e299) continue;
+                const Tier w = tier(a, b);
+                if (!w.ok) continue;
+                if (w.cost + f[b] < f[a]) {
+                    f[a] = w.cost + f[b];
+                    nxt[a] = b;
+                }
+            }
+        double best = 1e300;
+        int best_s = 0;
+        double top_cost = 5.0;
+        for (int s_ = 1; s_ <= N && s_ <= raocp::kMaxTopStages; ++s_) {
+            top_cost += level_cost(stage_n(s_ - 1), stage_n(s_));
+            int mt = 0;
+            bool fl = true;
+            size_t tb = top_bytes(s_, mt, true);
+            if (tb > kLds) {
+                fl = false;
+                tb = top_bytes(s_, mt, false);
+            }
+            if (tb > kLds) break;
+            if (forced > 0 && s_ != std::min(forced, N)) continue;
+            const double cost = top_cost + (fl ? 0.0 : 2.0 * s_) + f[s_];
+            if (cost < best) {
+                best = cost;
+                best_s = s_;
+                c->lds_top = tb;
+                c->maxch_top = mt;
+                c->f_lds_top = fl;
             }
         }
-        if (c->cut > 0) c->lds_top = top_bytes(c->cut);
+        c->cut = best_s;
         if (const char* env = getenv("RAOCP_DYN_PER_STAGE"))
             if (env[0] == '1') c->cut = 0;
+        if (c->cut > 0 && f[c->cut] >= 1e299) c->cut = 0;
+        for (int a = c->cut; c->cut > 0 && a < N; a = nxt[a]) {
+            const int b = nxt[a], L = b - a;
+            const Tier w = tier(a, b);
+            raocp_ctx::TierPlan tp;
+            tp.s0 = a;
+            tp.s1 = b;
+            tp.nsub = stage_n(a);
+            tp.maxch = w.maxch;
+            tp.lds_b = w.bb;
+            tp.lds_f = w.bf;
+            tp.fl = w.fl;
+            std::vector<raocp::Rec> lv;  // level ranges {lo, hi, off} of every subtree of the tier
+            for (int r = c->stage_ptr[a]; r < c->stage_ptr[a + 1]; ++r) {
+                int lo = r, hi = r + 1, acc = 0;
+                for (int l = 0; l <= L; ++l) {
+                    lv.push_back(raocp::Rec{lo, hi, acc, 0});
+                    acc += hi - lo;
+                    if (l < L) {
+                        const int nlo = t->ch_start[lo], nhi = t->ch_start[hi - 1] + t->nch[hi - 1];
+                        lo = nlo;
+                        hi = nhi;
+                    }
+                }
+            }
+            if ((rc = c->upload_vec(&tp.lv, lv))) return bail(rc);
+            c->tiers.push_back(tp);
+        }
+        if (getenv("RAOCP_DYN_VERBOSE")) {
+            fprintf(stderr, "[raocp] dynamics plan: top stages [0,%d) lds %zu F%s", c->cut, c->lds_top,
+                    c->f_lds_top ? "(lds)" : "(global)");
+            for (const auto& tp : c->tiers)
+                fprintf(stderr, " | tier [%d,%d) x%d lds %zu/%zu F%s", tp.s0, tp.s1, tp.nsub, tp.lds_b, tp.lds_f,
+                        tp.fl ? "(lds)" : "(global)");
+            fprintf(stderr, "\n");
+        }
     }
 
     // ---- iterate and work buffers
@@ -586,7 +786,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         if ((rc = c->alloc(&c->Z[b], c->P))) return bail(rc);
     for (int b = 0; b < 2; ++b)
         if ((rc = c->alloc(&c->E[b], c->D))) return bail(rc);
-    if ((rc = c->alloc(&c->XI2, c->D)) || (rc = c->alloc(&c->q, (size_t)n * nx)) || (rc = c->alloc(&c->d, (size_t)m * nu)) ||
+    if ((rc = c->alloc(&c->XI2, c->D)) || (rc = c->alloc(&c->q, (size_t)n * c->KP)) || (rc = c->alloc(&c->d, (size_t)m * nu + 2)) ||
+        (rc = c->alloc(&c->gXQ, (size_t)n * c->KP)) || (rc = c->alloc(&c->gU, (size_t)m * c->NUP)) ||
+        (rc = c->alloc(&c->gXD, (size_t)m * c->KF)) || (rc = c->alloc(&c->gP, (size_t)n * c->PS)) ||
         (rc = c->alloc(&c->x0, nx)) || (rc = c->alloc(&c->ctl, 1)) || (rc = c->alloc(&c->tmpP, c->P)) ||
         (rc = c->alloc(&c->tmpD, c->D)) || (rc = c->alloc(&c->part, 1024)) || (rc = c->alloc(&c->scal, 8)))
         return bail(rc);
@@ -605,7 +807,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     for (int b = 0; b < 2; ++b)
         if (hipMemset(c->E[b], 0, c->D * sizeof(double)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
     if (hipMemset(c->XI2, 0, c->D * sizeof(double)) != hipSuccess || hipMemset(c->ctl, 0, sizeof(Ctl)) != hipSuccess ||
-        hipMemset(c->q, 0, (size_t)n * nx * sizeof(double)) != hipSuccess ||
+        hipMemset(c->q, 0, (size_t)n * c->KP * sizeof(double)) != hipSuccess ||
+        hipMemset(c->gP, 0, (size_t)n * c->PS * sizeof(double)) != hipSuccess ||
         hipMemset(c->d, 0, (size_t)m * nu * sizeof(double)) != hipSuccess)
         return bail(fail(RAOCP_ERR_HIP, "memset"));
     c->bufs = raocp::Bufs{c->Z[0], c->Z[1], c->Z[2], c->E[0], c->E[1]};

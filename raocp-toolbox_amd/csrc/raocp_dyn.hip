@@ -6,32 +6,123 @@
 //     d_i = R~^-1 (u_i - sum_j B_j' q_j)
 //     q_i = (-x_i + K_i'(d_i - u_i)) + sum_j Abar_j' (P_j B_j d_i + q_j)
 //   forward, stage 0 .. N-1:  x_0 = x0bar ; u_i = K_i x_i + d_i ; x_j = Abar_j x_i + B_j d_i.
-// Device form (same values, re-associated so only per-MODE A, B and per-CLASS
-// Rinv, K, M = K' + sum_j Abar_j' P_j B_j are stored, and each backward step needs
-// two group exchanges):
-//     h = sum_j B_j' q_j ,  a = sum_j A_j' q_j            (lanes r < nu / r < nx)
-//     d = Rinv (u - h) ,    w = (-x + K'(h - u)) + a      (exchange h)
-//     q = w + M d                                          (exchange d)
-//   forward: u = K x + d ; x_j = A_j x + B_j u            (exchange u)
+// Device form. With h = sum_j B_j' q_j, a = sum_j A_j' q_j, v = u - h and the per-class
+// M = K' + sum_j Abar_j' P_j B_j, G = M R~^-1 - K' (host, raocp_capi.hip):
+//     d = R~^-1 v ,  q = (-x + a) + G v                      (backward, 2 phases)
+//     u = K x + d ,  x_j = [Abar_j | B_j] [x; d]              (forward, 1 phase)
+// so a backward level is two phases and a forward level one, each ending in one
+// workgroup barrier. Tables (row-major, zero-padded, 16-B aligned rows):
+//   W [kind][nu+nx][KP]   rows B' then A' of the child's (A, B) pair
+//   RG[cls ][nu+nx][NUP]  rows R~^-1 then G
+//   KM[cls ][nu   ][KP]   K
+//   F [pair][nx   ][KF]   [Abar | B | 0] of (child kind, parent class)
+// KP = nx rounded up to 8, KF = nx + nu rounded up to 8, NUP = nu rounded up to 2.
 //
-// Launch structure. The recursion is sequential in the stage, so the number of
-// dependent steps, not bandwidth, sets the time. The tree is cut at a stage s:
+// Lane mapping ("split-k"): every output row of a dot product of length KP (or KF) is
+// produced by KS = 4 consecutive lanes, each reading one 16-B-aligned slice of the
+// matrix row (global, L1/L2-resident) and of the vector row (LDS) with 16-byte loads,
+// then reduced with two xor-shuffles. A child's rows are R = nu + nx consecutive
+// groups. This keeps each lane's dependent chain to KP/4 (KF/4) FMAs, which is what a
+// level costs when the tree is narrow (the top stages), and spreads wide levels over
+// all lanes of the workgroup.
+//
+// Launch structure (the recursion is sequential in the stage): the tree is cut at
+// stage s;
 //   k_dyn_bottom_back — one workgroup per subtree rooted at stage s, levels N-1..s;
 //   k_dyn_top        — ONE workgroup: stages s-1..0 backward, then 0..s-1 forward;
 //   k_dyn_bottom_fwd — one workgroup per subtree, levels s..N-1 forward.
-// Matrices of the stages a kernel covers are staged into LDS in its prologue (plus,
-// for the top, the node records and the x/u/q rows it reads), so the dependent
-// steps only touch LDS. Trees that do not fit fall back to one launch per stage
-// (k_dyn_back_stage / k_dyn_fwd_stage, everything from global memory).
-//
-// Every pointer carries its address space in its type (ldsd / glbd), so loads are
-// ds_read / global_load, never flat.
-//
-// Lane mapping: a node is handled by a group of G lanes (lane r owns row r).
-// Matrix layouts (padded leading dimension, conflict-free LDS reads):
-//   A[mode]  nx x (nx+1)  A(k, r) at k*(nx+1) + r      B[mode] nx x (nu+1)  B(k, c) at k*(nu+1) + c
-//   R[cls]   Rinv(r, c) at c*(nu+1) + r                 K[cls]  K(c, r) at c*(nx+1) + r
-//   M[cls]   M(r, c) at c*(nx+1) + r
+// Vectors of the nodes a kernel covers are staged into LDS in its prologue (padded
+// rows with zero tails), so the dependent steps only touch LDS for vectors.
+// Trees that do not fit run one launch per phase and stage on padded global rows
+// (k_dyn_gather, k_dyn_stage_a / _b / _f).
+
+constexpr int kKS = 4;
+constexpr int kDynBlock = 1024;
+
+typedef double d2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) d2v lds2;
+typedef __attribute__((address_space(1))) d2v glb2;
+
+__device__ __forceinline__ d2v ld2(const ldsd* p) { return *(const lds2*)p; }
+__device__ __forceinline__ d2v ld2(const glbd* p) { return *(const glb2*)p; }
+
+constexpr __host__ __device__ int rup(int a, int b) { return (a + b - 1) / b * b; }
+// row stride of a matrix table whose rows hold k (even) doubles: an odd number of 16-B
+// units, so the ds_read_b128 of lanes reading different rows spread over the banks
+constexpr __host__ __device__ int tstride(int k) { return (k / 2) % 2 == 0 ? k + 2 : k; }
+
+template <int NXc, int NUc>
+struct Geo {
+    int nx, nu, R, KP, KF, NUP, PH, PS, SKP, SKF, SNU;  // S*: table row strides
+    __device__ __forceinline__ Geo(const Dev& p) {
+        nx = NXc ? NXc : p.nx;
+        nu = NUc ? NUc : p.nu;
+        R = nu + nx;
+        KP = rup(nx, 2 * kKS);
+        KF = rup(nx + nu, 2 * kKS);
+        NUP = rup(nu, 2);
+        PH = NUP;                   // child product row: [h (NUP) | a (nx, even-padded)]
+        PS = NUP + rup(nx, 2);
+        SKP = tstride(KP);
+        SKF = tstride(KF);
+        SNU = tstride(NUP);
+    }
+    // compile-time padded lengths (0: runtime)
+    static constexpr int cKP = NXc ? rup(NXc, 2 * kKS) : 0;
+    static constexpr int cKF = NXc ? rup(NXc + NUc, 2 * kKS) : 0;
+    static constexpr int cNUP = NUc ? rup(NUc, 2) : 0;
+};
+
+// sum_k m[k] v[k] over kc (even) elements, both 16-B aligned; all loads issued first
+template <int KC, class PM, class PV>
+__device__ __forceinline__ double dot_slice(PM m, PV v, int kc) {
+    if constexpr (KC == 0) {
+        double s0 = 0.0, s1 = 0.0;
+        for (int k = 0; k < kc; k += 2) {
+            const d2v a = ld2(m + k), b = ld2(v + k);
+            s0 = fma(a.x, b.x, s0);
+            s1 = fma(a.y, b.y, s1);
+        }
+        return s0 + s1;
+    } else {
+        d2v a[KC / 2], b[KC / 2];
+        _Pragma("unroll") for (int t = 0; t < KC / 2; ++t) {
+            a[t] = ld2(m + 2 * t);
+            b[t] = ld2(v + 2 * t);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        double s0 = 0.0, s1 = 0.0;
+        _Pragma("unroll") for (int t = 0; t < KC / 2; ++t) {
+            s0 = fma(a[t].x, b[t].x, s0);
+            s1 = fma(a[t].y, b[t].y, s1);
+        }
+        return s0 + s1;
+    }
+}
+
+// xor-exchange within lane quads by DPP (VALU, no LDS round trip)
+template <int CTRL>
+__device__ __forceinline__ double dpp_quad(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// reduce over the KS consecutive lanes of a split-k group (all live or all idle)
+template <int KS>
+__device__ __forceinline__ double ks_reduce(double v) {
+    if constexpr (KS >= 2) v += dpp_quad<0xB1>(v);  // quad_perm [1,0,3,2]: lane ^ 1
+    if constexpr (KS >= 4) v += dpp_quad<0x4E>(v);  // quad_perm [2,3,0,1]: lane ^ 2
+    return v;
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations
+// (lgkmcnt) but not for its outstanding global stores (vmcnt) — __syncthreads() would
+// wait for every z / d store of the level to reach L2. No kernel here reads back,
+// within the launch, global data another lane wrote.
+__device__ __forceinline__ void lds_sync() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 template <class P>
 struct RowsT {
@@ -41,152 +132,168 @@ struct RowsT {
     __device__ __forceinline__ P operator()(int j) const { return base + (size_t)(j - off) * stride; }
 };
 typedef RowsT<ldsd*> LRows;
-
-// element-wise difference view a[k] - b[k] (for the batched dot products)
-template <class PA, class PB>
-struct Diff {
-    PA a;
-    PB b;
-    __device__ __forceinline__ double operator[](int k) const { return a[k] - b[k]; }
-};
 typedef RowsT<glbd*> GRows;
-
-template <class P>
-struct MatsT {
-    P A, B, R, K, M;
-    int cls0;  // class id of slot 0
-};
 
 template <class IP>
 struct InfoT {
     IP nl;  // nonleaf records {ch_start, nch, class, stage}
     int n0;
-    IP ch;  // child records {iA, iB, anc, 0}
+    IP ch;  // child records {kind, pair, anc, 0}
     int c0;
     __device__ __forceinline__ Rec nonleaf(int i) const { return nl[i - n0]; }
     __device__ __forceinline__ Rec child(int j) const { return ch[j - c0]; }
 };
 
-template <int NXc, int NUc>
-struct Dims {
-    int nx, nu, SA, SB, SR, SK;
-    __device__ __forceinline__ Dims(const Dev& p) {
-        nx = NXc ? NXc : p.nx;
-        nu = NUc ? NUc : p.nu;
-        SA = nx * (nx + 1);
-        SB = nx * (nu + 1);
-        SR = nu * (nu + 1);
-        SK = nu * (nx + 1);
-    }
+// matrix tables as seen by a kernel: W, RG, KM in one address space, F in another;
+// classes / pairs are rebased by c0 / p0 when a kernel stages only its stages' range
+template <class PW, class PF>
+struct TabsT {
+    PW W;
+    PW RG;
+    PW KM;
+    PF F;
+    int c0, p0;
 };
+typedef TabsT<const glbd*, const glbd*> GTabs;
+__device__ __forceinline__ GTabs dyn_tabs(const Dev& p) {
+    return GTabs{(const glbd*)p.dW, (const glbd*)p.dRG, (const glbd*)p.dKM, (const glbd*)p.dF, 0, 0};
+}
 
-// ---- backward step for nonleaf nodes [b, e) of one stage --------------------------
-// qin(j): rows of the children's q, or of their x when qsign = -1 (leaf children).
-template <int NXc, int NUc, class MT, class INF, class QI, class XI, class UI, class QO, class DO>
-__device__ __forceinline__ void back_step(const Dev& p, const MT& mt, const INF& inf, int b, int e, QI qin,
-                                          double qsign, XI xin, UI uin, QO qout, DO dout, ldsd* s_h, ldsd* s_d,
-                                          int pass0, int pstride) {
-    const Dims<NXc, NUc> D(p);
-    const int nx = D.nx, nu = D.nu;
-    const int G = nx > nu ? nx : nu;
-    const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G, base = gl * G;
-    for (int pass = pass0;; pass += pstride) {
-        const int first = b + pass * per;
-        if (first >= e) break;  // uniform over the workgroup
-        const int i = first + gl;
-        const bool live = gl < per && i < e;
-        Rec ni = {0, 0, 0, 0};
-        if (live) ni = inf.nonleaf(i);
-        const int cs = ni.x, c = ni.y, cl = ni.z - mt.cls0;
-        double h = 0.0, a = 0.0;
-        if (live) {
-            for (int q = 0; q < c; ++q) {
-                const int j = cs + q;
-                const Rec cj = inf.child(j);
-                const auto row = qin(j);
-                if (r < nu) {
-                    const auto Bm = mt.B + (size_t)cj.y * D.SB;
-                    h += dotb<NXc>(Bm + r, nu + 1, row, nx);
-                }
-                if (r < nx) {
-                    const auto Am = mt.A + (size_t)cj.x * D.SA;
-                    a += dotb<NXc>(Am + r, nx + 1, row, nx);
-                }
-            }
-            h *= qsign;
-            a *= qsign;
+// ---- backward phase A: child products p_j = sign [B' ; A'] q_j for children [cb, ce) --
+// qin(j): padded row (KP) of q_j (or x_j for leaf children, sign = -1); P(j): PS-row.
+// KS lanes per output row (split-k); the caller picks KS from the level's width.
+template <int KS, int NXc, int NUc, class TB, class INF, class QI, class PO>
+__device__ __forceinline__ void back_phase_a_ks(const Dev& p, const TB& tb, const INF& inf, int cb, int ce, QI qin,
+                                                double sign, PO pout, int tid, int nthr) {
+    const Geo<NXc, NUc> g(p);
+    constexpr int cKC = Geo<NXc, NUc>::cKP / KS;
+    const int KC = g.KP / KS;
+    const int per = g.R * KS;
+    const int slots = nthr / per;
+    const int slot = tid / per, rem = tid - slot * per, rho = rem / KS, sl = rem - rho * KS;
+    for (int first = cb; first < ce; first += slots) {
+        const int j = first + slot;
+        if (slot < slots && j < ce) {
+            const Rec cj = inf.child(j);
+            const auto w = tb.W + ((size_t)cj.x * g.R + rho) * g.SKP + sl * KC;
+            double acc = dot_slice<cKC>(w, qin(j) + sl * KC, KC);
+            acc = ks_reduce<KS>(acc) * sign;
+            if (sl == 0) pout(j)[rho < g.nu ? rho : g.PH + rho - g.nu] = acc;
         }
-        s_h[threadIdx.x] = h;
-        __syncthreads();
-        double dr = 0.0, w = 0.0;
-        if (live) {
-            const auto u = uin(i);
-            if (r < nu) {
-                const auto Rm = mt.R + (size_t)cl * D.SR;
-                dr = dotb<NUc>(Rm + r, nu + 1, Diff<decltype(u), ldsd*>{u, s_h + base}, nu);
-                dout(i)[r] = dr;
-            }
-            if (r < nx) {
-                const auto Km = mt.K + (size_t)cl * D.SK;
-                const double s = dotb<NUc>(Km + r, nx + 1, Diff<ldsd*, decltype(u)>{s_h + base, u}, nu);
-                w = (-xin(i)[r] + s) + a;
-            }
-        }
-        s_d[threadIdx.x] = dr;
-        __syncthreads();
-        if (live && r < nx) {
-            const auto Mm = mt.M + (size_t)cl * D.SK;
-            qout(i)[r] = w + dotb<NUc>(Mm + r, nx + 1, s_d + base, nu);
-        }
-        __syncthreads();
     }
 }
 
-// ---- forward step for nonleaf nodes [b, e): u_i, then x of all their children ------
-// xin must cover every parent (node 0 included: callers store x0bar there first);
-// uio(i): LDS rows receiving u (read back by the children's lanes after a barrier);
-// child rows also go to xout when XOUT.
-template <int NXc, int NUc, bool XOUT, class MT, class INF, class XI, class DI>
-__device__ __forceinline__ void fwd_step(const Dev& p, const MT& mt, const INF& inf, int b, int e, XI xin, DI din,
-                                         LRows uio, glbd* z, LRows xout) {
-    const Dims<NXc, NUc> D(p);
-    const int nx = D.nx, nu = D.nu;
-    {
-        const int per = blockDim.x / nu, gl = threadIdx.x / nu, r = threadIdx.x - gl * nu;
-        for (int first = b; first < e; first += per) {
-            const int i = first + gl;
-            if (gl < per && i < e) {
-                const int cl = inf.nonleaf(i).z - mt.cls0;
-                const auto x = xin(i);
-                const auto Km = mt.K + (size_t)cl * D.SK;
-                const double u = dotb<NXc>(Km + r * (nx + 1), 1, x, nx) + din(i)[r];
-                z[p.U0 + (size_t)i * nu + r] = u;
-                uio(i)[r] = u;
+template <int NXc, int NUc, class TB, class INF, class QI, class PO>
+__device__ __forceinline__ void back_phase_a(const Dev& p, const TB& tb, const INF& inf, int cb, int ce, QI qin,
+                                             double sign, PO pout, int tid, int nthr) {
+    const int items = (ce - cb) * (NXc ? NXc + NUc : p.nx + p.nu);
+    if (items * 4 <= nthr) back_phase_a_ks<4, NXc, NUc>(p, tb, inf, cb, ce, qin, sign, pout, tid, nthr);
+    else if (items * 2 <= nthr) back_phase_a_ks<2, NXc, NUc>(p, tb, inf, cb, ce, qin, sign, pout, tid, nthr);
+    else back_phase_a_ks<1, NXc, NUc>(p, tb, inf, cb, ce, qin, sign, pout, tid, nthr);
+}
+
+// ---- backward phase B: per node d = RG[0:nu] v, q = (-x + a) + RG[nu:] v ------------
+template <int NXc, int NUc, class TB, class INF, class PI, class XI, class UI, class QO, class DO>
+__device__ __forceinline__ void back_phase_b(const Dev& p, const TB& tb, const INF& inf, int b, int e, PI pin,
+                                             XI xin, UI uin, QO qout, DO dout, int tid, int nthr) {
+    const Geo<NXc, NUc> g(p);
+    constexpr int cNUP = Geo<NXc, NUc>::cNUP;
+    const int slots = nthr / g.R;
+    const int slot = tid / g.R, t = tid - slot * g.R;
+    for (int first = b; first < e; first += slots) {
+        const int i = first + slot;
+        if (slot < slots && i < e) {
+            const Rec ni = inf.nonleaf(i);
+            const auto u = uin(i);
+            const auto rg = tb.RG + ((size_t)(ni.z - tb.c0) * g.R + t) * g.SNU;
+            double out;
+            if constexpr (cNUP > 0) {
+                d2v v[cNUP / 2], m[cNUP / 2];
+                _Pragma("unroll") for (int k = 0; k < cNUP / 2; ++k) {
+                    m[k] = ld2(rg + 2 * k);
+                    v[k] = ld2(u + 2 * k);
+                }
+                for (int q = 0; q < ni.y; ++q) {
+                    const auto pr = pin(ni.x + q);
+                    _Pragma("unroll") for (int k = 0; k < cNUP / 2; ++k) v[k] -= ld2(pr + 2 * k);
+                }
+                double s0 = 0.0, s1 = 0.0;
+                _Pragma("unroll") for (int k = 0; k < cNUP / 2; ++k) {
+                    s0 = fma(m[k].x, v[k].x, s0);
+                    s1 = fma(m[k].y, v[k].y, s1);
+                }
+                out = s0 + s1;
+            } else {
+                double s0 = 0.0, s1 = 0.0;
+                for (int k = 0; k < g.NUP; k += 2) {
+                    d2v v = ld2(u + k);
+                    for (int q = 0; q < ni.y; ++q) v -= ld2(pin(ni.x + q) + k);
+                    const d2v m = ld2(rg + k);
+                    s0 = fma(m.x, v.x, s0);
+                    s1 = fma(m.y, v.y, s1);
+                }
+                out = s0 + s1;
+            }
+            if (t < g.nu) {
+                dout(i)[t] = out;
+            } else {
+                const int r = t - g.nu;
+                double a = 0.0;
+                for (int q = 0; q < ni.y; ++q) a += pin(ni.x + q)[g.PH + r];
+                qout(i)[r] = (-xin(i)[r] + a) + out;
             }
         }
     }
-    __syncthreads();
-    {
-        const int cb = inf.nonleaf(b).x;
-        const Rec last = inf.nonleaf(e - 1);
-        const int ce = last.x + last.y;
-        const int per = blockDim.x / nx, gl = threadIdx.x / nx, r = threadIdx.x - gl * nx;
-        for (int first = cb; first < ce; first += per) {
-            const int j = first + gl;
-            if (gl < per && j < ce) {
-                const Rec cj = inf.child(j);
-                const int i = cj.z;
-                const auto x = xin(i);
-                const ldsd* u = uio(i);
-                const auto Am = mt.A + (size_t)cj.x * D.SA;
-                const auto Bm = mt.B + (size_t)cj.y * D.SB;
-                const double v = dotb<NXc>(Am + r * (nx + 1), 1, x, nx) + dotb<NUc>(Bm + r * (nu + 1), 1, u, nu);
-                z[p.X0 + (size_t)j * nx + r] = v;
-                if (XOUT) xout(j)[r] = v;
+}
+
+// ---- forward: u_i = K x_i + d_i (nodes [b, e)), x_j = F [x_i; d_i] (their children) ---
+// xd(i): padded row [x_i | d_i | 0] (KF); child rows also go to xdo(j) when XOUT.
+template <int KS, int NXc, int NUc, bool XOUT, class TB, class INF, class XDI, class XDO>
+__device__ __forceinline__ void fwd_phase_ks(const Dev& p, const TB& tb, const INF& inf, int b, int e, int cb, int ce,
+                                             XDI xd, glbd* z, XDO xdo, int tid, int nthr) {
+    const Geo<NXc, NUc> g(p);
+    constexpr int cKCP = Geo<NXc, NUc>::cKP / KS, cKCF = Geo<NXc, NUc>::cKF / KS;
+    const int KCP = g.KP / KS, KCF = g.KF / KS;
+    const int nU = (e - b) * g.nu * KS;    // u items (lanes)
+    const int nX = (ce - cb) * g.nx * KS;  // x items (lanes)
+    for (int base = 0; base < nU + nX; base += nthr) {
+        const int vi = base + tid;
+        if (vi < nU) {
+            const int grp = vi / KS, sl = vi - grp * KS;
+            const int i = b + grp / g.nu, r = grp - (grp / g.nu) * g.nu;
+            const Rec ni = inf.nonleaf(i);
+            const auto row = xd(i);
+            const auto km = tb.KM + ((size_t)(ni.z - tb.c0) * g.nu + r) * g.SKP + sl * KCP;
+            double acc = dot_slice<cKCP>(km, row + sl * KCP, KCP);
+            acc = ks_reduce<KS>(acc);
+            if (sl == 0) z[p.U0 + (size_t)i * g.nu + r] = acc + row[g.nx + r];
+        } else if (vi < nU + nX) {
+            const int wi = vi - nU;
+            const int grp = wi / KS, sl = wi - grp * KS;
+            const int j = cb + grp / g.nx, r = grp - (grp / g.nx) * g.nx;
+            const Rec cj = inf.child(j);
+            const auto f = tb.F + ((size_t)(cj.y - tb.p0) * g.nx + r) * g.SKF + sl * KCF;
+            double acc = dot_slice<cKCF>(f, xd(cj.z) + sl * KCF, KCF);
+            acc = ks_reduce<KS>(acc);
+            if (sl == 0) {
+                z[p.X0 + (size_t)j * g.nx + r] = acc;
+                if (XOUT) xdo(j)[r] = acc;
             }
         }
     }
-    __syncthreads();
+}
+
+template <int NXc, int NUc, bool XOUT, class TB, class INF, class XDI, class XDO>
+__device__ __forceinline__ void fwd_phase(const Dev& p, const TB& tb, const INF& inf, int b, int e, XDI xd, glbd* z,
+                                          XDO xdo, int tid, int nthr) {
+    const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
+    const int cb = inf.nonleaf(b).x;
+    const Rec last = inf.nonleaf(e - 1);
+    const int ce = last.x + last.y;
+    const int items = (e - b) * nu + (ce - cb) * nx;
+    if (items * 4 <= nthr) fwd_phase_ks<4, NXc, NUc, XOUT>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
+    else if (items * 2 <= nthr) fwd_phase_ks<2, NXc, NUc, XOUT>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
+    else fwd_phase_ks<1, NXc, NUc, XOUT>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
 }
 
 __device__ __forceinline__ glbd* pick3(const Bufs& bf, int k) {
@@ -198,246 +305,432 @@ __device__ __forceinline__ glbd* dyn_z(const Bufs& bf, int zsel, const Ctl* ctl)
     return pick3(bf, (ctl ? ctl->k : 0) + zsel);
 }
 
-typedef MatsT<const glbd*> GMats;
-typedef MatsT<const ldsd*> LMats;
-
-__device__ __forceinline__ GMats global_mats(const Dev& p) {
-    return GMats{(const glbd*)p.Ap, (const glbd*)p.Bp, (const glbd*)p.Rp, (const glbd*)p.Kp, (const glbd*)p.Mp, 0};
-}
-
-// cooperative global -> LDS copy
-__device__ __forceinline__ void lds_copy(ldsd* dst, const glbd* src, size_t count) {
-    for (size_t t = threadIdx.x; t < count; t += blockDim.x) dst[t] = src[t];
-}
-
-// stage the A/B tables of every mode and the class tables [c0, c1) into LDS at `dst`
-template <int NXc, int NUc>
-__device__ __forceinline__ LMats stage_mats(const Dev& p, ldsd* dst, int c0, int c1, ldsd** end) {
-    const Dims<NXc, NUc> D(p);
-    const GMats g = global_mats(p);
-    ldsd* A = dst;
-    ldsd* B = A + (size_t)p.nA * D.SA;
-    ldsd* R = B + (size_t)p.nB * D.SB;
-    ldsd* K = R + (size_t)(c1 - c0) * D.SR;
-    ldsd* M = K + (size_t)(c1 - c0) * D.SK;
-    lds_copy(A, g.A, (size_t)p.nA * D.SA);
-    lds_copy(B, g.B, (size_t)p.nB * D.SB);
-    lds_copy(R, g.R + (size_t)c0 * D.SR, (size_t)(c1 - c0) * D.SR);
-    lds_copy(K, g.K + (size_t)c0 * D.SK, (size_t)(c1 - c0) * D.SK);
-    lds_copy(M, g.M + (size_t)c0 * D.SK, (size_t)(c1 - c0) * D.SK);
-    *end = M + (size_t)(c1 - c0) * D.SK;
-    return LMats{A, B, R, K, M, c0};
-}
-
-// ---- per-stage fallback (any tree) ------------------------------------------------
-template <int NXc, int NUc>
-__global__ void __launch_bounds__(kBlock) k_dyn_back_stage(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
-                                                            double* qbuf_, double* dbuf_, int b, int e) {
-    __shared__ double s_h[kBlock];
-    __shared__ double s_d[kBlock];
-    if (ctl && ctl->done) return;
-    glbd* z = dyn_z(bf, zsel, ctl);
-    glbd* qbuf = (glbd*)qbuf_;
-    glbd* dbuf = (glbd*)dbuf_;
-    const Dims<NXc, NUc> D(p);
-    const InfoT<glbrec*> inf{(glbrec*)p.ninfo, 0, (glbrec*)p.cinfo, 0};
-    const bool leaves = p.ninfo[b].x >= p.m;
-    const GRows qin = leaves ? GRows{z + p.X0, 0, D.nx} : GRows{qbuf, 0, D.nx};
-    back_step<NXc, NUc>(p, global_mats(p), inf, b, e, qin, leaves ? -1.0 : 1.0, GRows{z + p.X0, 0, D.nx},
-                        GRows{z + p.U0, 0, D.nu}, GRows{qbuf, 0, D.nx}, GRows{dbuf, 0, D.nu}, (ldsd*)s_h,
-                        (ldsd*)s_d, blockIdx.x, gridDim.x);
-}
-
-// forward, one stage, across workgroups: a child lane recomputes its parent's u = K x + d
-// (the same FMA chain as the parent's u lanes, so the values agree bit for bit)
-template <int NXc, int NUc>
-__global__ void __launch_bounds__(kBlock) k_dyn_fwd_stage(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
-                                                           const double* dbuf_, const double* x0_, int b, int e) {
-    if (ctl && ctl->done) return;
-    glbd* z = dyn_z(bf, zsel, ctl);
-    const glbd* dbuf = (const glbd*)dbuf_;
-    const glbd* x0 = (const glbd*)x0_;
-    const GMats g = global_mats(p);
-    const Dims<NXc, NUc> D(p);
-    const int nx = D.nx, nu = D.nu;
-    if (b == 0 && blockIdx.x == 0 && (int)threadIdx.x < nx) z[p.X0 + threadIdx.x] = x0[threadIdx.x];  // x_0 = x0bar
-    const int nuB = cdiv_dev(e - b, blockDim.x / nu);
-    if ((int)blockIdx.x < nuB) {
-        const int per = blockDim.x / nu, gl = threadIdx.x / nu, r = threadIdx.x - gl * nu;
-        const int i = b + blockIdx.x * per + gl;
-        if (gl < per && i < e) {
-            const glbd* x = i == 0 ? x0 : z + p.X0 + (size_t)i * nx;
-            const glbd* Km = g.K + (size_t)p.ninfo[i].z * D.SK;
-            double s = 0.0;
-            _Pragma("unroll") for (int k = 0; k < nx; ++k) s = fma(Km[r * (nx + 1) + k], x[k], s);
-            z[p.U0 + (size_t)i * nu + r] = s + dbuf[(size_t)i * nu + r];
+// copy `rows` rows of `cols` doubles (source stride sstride) into padded rows of stride
+// dstride, zero tail; loads batched so several are in flight per thread
+template <class PD, class PS>
+__device__ __forceinline__ void copy_rows(PD dst, int dstride, PS src, int sstride, int rows, int cols, int tid,
+                                          int nthr) {
+    const int total = rows * dstride;
+    constexpr int U = 8;
+    for (int base = tid; base < total; base += U * nthr) {
+        double v[U];
+        _Pragma("unroll") for (int k = 0; k < U; ++k) {
+            const int e = base + k * nthr;
+            const int r = e / dstride, c = e - r * dstride;
+            v[k] = (e < total && c < cols) ? (double)src[(size_t)r * sstride + c] : 0.0;
         }
-        return;
+        _Pragma("unroll") for (int k = 0; k < U; ++k) {
+            const int e = base + k * nthr;
+            if (e < total) dst[e] = v[k];
+        }
     }
-    const int cb = p.ninfo[b].x;
-    const int ce = p.ninfo[e - 1].x + p.ninfo[e - 1].y;
-    const int per = blockDim.x / nx, gl = threadIdx.x / nx, r = threadIdx.x - gl * nx;
-    const int j = cb + (blockIdx.x - nuB) * per + gl;
-    if (gl >= per || j >= ce) return;
-    const Rec cj = p.cinfo[j];
-    const int i = cj.z;
-    const glbd* x = i == 0 ? x0 : z + p.X0 + (size_t)i * nx;
-    const glbd* Km = g.K + (size_t)p.ninfo[i].z * D.SK;
-    const glbd* d = dbuf + (size_t)i * nu;
-    const glbd* Am = g.A + (size_t)cj.x * D.SA;
-    const glbd* Bm = g.B + (size_t)cj.y * D.SB;
-    double s = 0.0, s2 = 0.0;
-    _Pragma("unroll") for (int k = 0; k < nx; ++k) s = fma(Am[r * (nx + 1) + k], x[k], s);
-    for (int cc = 0; cc < nu; ++cc) {
-        double uc = 0.0;
-        _Pragma("unroll") for (int k = 0; k < nx; ++k) uc = fma(Km[cc * (nx + 1) + k], x[k], uc);
-        s2 = fma(Bm[r * (nu + 1) + cc], uc + d[cc], s2);
+}
+
+template <class PD>
+__device__ __forceinline__ void zero_fill(PD dst, int count, int tid, int nthr) {
+    for (int e = tid; e < count; e += nthr) dst[e] = 0.0;
+}
+
+// ---- per-stage path on padded global rows (any tree) ----------------------------------
+// gather: XQ[j] = x_j (padded KP), U[i] = u_i (padded NUP), XD[i] = [0 | 0 | 0]
+template <int NXc, int NUc>
+__global__ void __launch_bounds__(kBlock) k_dyn_gather(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                        double* xq_, double* u_, double* xd_) {
+    if (ctl && ctl->done) return;
+    const Geo<NXc, NUc> g(p);
+    const glbd* z = dyn_z(bf, zsel, ctl);
+    const int tid = blockIdx.x * blockDim.x + threadIdx.x, nthr = gridDim.x * blockDim.x;
+    copy_rows((glbd*)xq_, g.KP, z + p.X0, g.nx, p.n, g.nx, tid, nthr);
+    copy_rows((glbd*)u_, g.NUP, z + p.U0, g.nu, p.m, g.nu, tid, nthr);
+    zero_fill((glbd*)xd_, p.m * g.KF, tid, nthr);
+}
+
+template <int NXc, int NUc>
+__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_a(Dev p, const Ctl* __restrict__ ctl, const double* xq_,
+                                                         double* pb_, int cb, int ce, double sign) {
+    if (ctl && ctl->done) return;
+    const Geo<NXc, NUc> g(p);
+    const InfoT<glbrec*> inf{(glbrec*)p.ninfo, 0, (glbrec*)p.cinfo, 0};
+    const int per = g.R * kKS, slots = blockDim.x / per;
+    const int c0 = cb + blockIdx.x * slots;
+    back_phase_a<NXc, NUc>(p, dyn_tabs(p), inf, c0, min(ce, c0 + slots), GRows{(glbd*)xq_, 0, g.KP}, sign,
+                           GRows{(glbd*)pb_, 0, g.PS}, threadIdx.x, blockDim.x);
+}
+
+template <int NXc, int NUc>
+__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_b(Dev p, const Ctl* __restrict__ ctl, double* xq_,
+                                                         const double* u_, const double* pb_, double* xd_, double* d_,
+                                                         int b, int e) {
+    if (ctl && ctl->done) return;
+    const Geo<NXc, NUc> g(p);
+    const InfoT<glbrec*> inf{(glbrec*)p.ninfo, 0, (glbrec*)p.cinfo, 0};
+    const int slots = blockDim.x / g.R;
+    const int b0 = b + blockIdx.x * slots;
+    const GRows xq{(glbd*)xq_, 0, g.KP};
+    // d goes to the padded forward rows (XD cols nx..) and to the d buffer
+    struct DOut {
+        glbd* xd;
+        glbd* d;
+        int KF, nx, nu;
+        struct Ref {
+            glbd* a;
+            glbd* b;
+            __device__ __forceinline__ void operator=(double v) const { *a = v; *b = v; }
+        };
+        struct Row {
+            glbd* a;
+            glbd* b;
+            __device__ __forceinline__ Ref operator[](int r) const { return Ref{a + r, b + r}; }
+        };
+        __device__ __forceinline__ Row operator()(int i) const {
+            return Row{xd + (size_t)i * KF + nx, d + (size_t)i * nu};
+        }
+    } dout{(glbd*)xd_, (glbd*)d_, g.KF, g.nx, g.nu};
+    back_phase_b<NXc, NUc>(p, dyn_tabs(p), inf, b0, min(e, b0 + slots), GRows{(glbd*)pb_, 0, g.PS}, xq,
+                           RowsT<const glbd*>{(const glbd*)u_, 0, g.NUP}, xq, dout, threadIdx.x, blockDim.x);
+}
+
+template <int NXc, int NUc>
+__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_f(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                         double* xd_, const double* x0_, int b, int e) {
+    if (ctl && ctl->done) return;
+    const Geo<NXc, NUc> g(p);
+    glbd* z = dyn_z(bf, zsel, ctl);
+    glbd* xd = (glbd*)xd_;
+    const InfoT<glbrec*> inf{(glbrec*)p.ninfo, 0, (glbrec*)p.cinfo, 0};
+    if (b == 0) {  // x_0 = x0bar (cache.py:282): one workgroup, one node
+        if ((int)threadIdx.x < g.nx) {
+            const double v = ((const glbd*)x0_)[threadIdx.x];
+            xd[threadIdx.x] = v;
+            z[p.X0 + threadIdx.x] = v;
+        }
+        __syncthreads();
     }
-    z[p.X0 + (size_t)j * nx + r] = s + s2;
+    // blocks over (parent) nodes: each block takes whole parents so its children follow
+    const int per_node = g.nu * kKS + p.cmax * g.nx * kKS;
+    const int slots = max(1, (int)blockDim.x / per_node);
+    const int b0 = b + blockIdx.x * slots;
+    const int e0 = min(e, b0 + slots);
+    const bool xout = inf.nonleaf(b).w + 1 < p.N;
+    if (xout)
+        fwd_phase<NXc, NUc, true>(p, dyn_tabs(p), inf, b0, e0, GRows{xd, 0, g.KF}, z, GRows{xd, 0, g.KF}, threadIdx.x,
+                                  blockDim.x);
+    else
+        fwd_phase<NXc, NUc, false>(p, dyn_tabs(p), inf, b0, e0, GRows{xd, 0, g.KF}, z, GRows{xd, 0, g.KF},
+                                   threadIdx.x, blockDim.x);
 }
 
 // ---- subtree-blocked sweep ------------------------------------------------------------
-constexpr int kMaxLevels = 67;  // 3 int arrays of 68: keeps the dynamic-LDS base 16-B aligned
+constexpr int kMaxLevels = 31;    // tier depth limit (host plans within it)
+constexpr int kMaxTopStages = 62; // cut stage limit of k_dyn_top
 
-// descendant id ranges of `root` per level (level l <-> stage s + l), levels 0..L; off[l] =
-// LDS row offset of level l among the subtree's nonleaf nodes
-__device__ __forceinline__ void subtree_levels(const Dev& p, int root, int L, int* lo, int* hi, int* off) {
-    if (threadIdx.x == 0) {
-        lo[0] = root;
-        hi[0] = root + 1;
-        int acc = 0;
-        for (int l = 0; l < L; ++l) {
-            off[l] = acc;
-            acc += hi[l] - lo[l];
-            const Rec a = p.ninfo[lo[l]], zz = p.ninfo[hi[l] - 1];
-            lo[l + 1] = a.x;
-            hi[l + 1] = zz.x + zz.y;
-        }
-        off[L] = acc;
-    }
-    __syncthreads();
+struct Prologue {
+    int lo[kMaxLevels + 1], hi[kMaxLevels + 1], off[kMaxLevels + 1];
+    int sp[kMaxTopStages + 2];  // stage_ptr[0 .. s+1] (top)
+    unsigned long long ts[64];  // diagnostics (p.stamps != nullptr)
+};
+
+// diagnostics: thread 0 records the 100 MHz clock in LDS; flushed at the end of the kernel
+__device__ __forceinline__ void tstamp(const Dev& p, Prologue& pl, int slot) {
+    if (p.stamps && threadIdx.x == 0 && slot < 64) pl.ts[slot] = __builtin_amdgcn_s_memrealtime();
+}
+__device__ __forceinline__ void tflush(const Dev& p, const Prologue& pl, int n) {
+    if (p.stamps && threadIdx.x == 0 && blockIdx.x == 0)
+        for (int k = 0; k < n && k < 64; ++k) p.stamps[k] = pl.ts[k];
 }
 
+// Prologue copies are LDS-DMA (global_load_lds_dwordx4): every wave issues its share of
+// 16-B chunks of a contiguous global range straight into LDS, nothing waits until the
+// single vmcnt(0) at the end, so a prologue costs about one memory round trip.
+// dst and src are 16-B aligned; n (doubles) is rounded up to even (sources have slack).
+__device__ __forceinline__ void dma(ldsd* dst, const double* src, int n) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    const int chunks = (n + 1) >> 1;
+    for (int c0 = wave * 64; c0 < chunks; c0 += nw * 64) {
+        const int ch = c0 + lane;
+        if (ch < chunks) __builtin_amdgcn_global_load_lds((const glbd*)src + 2 * ch, dst + 2 * c0, 16, 0, 0);
+    }
+}
+// unaligned source: copy from the 16-B boundary below; returns the shift (0 or 1 double)
+__device__ __forceinline__ int dma_u(ldsd* dst, const double* src, int n) {
+    const int sh = (int)(((uintptr_t)src >> 3) & 1);
+    dma(dst, src - sh, n + sh);
+    return sh;
+}
+__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// staged raw rows (stride cols, shifted by sh) -> padded rows (stride w, zero tail)
+__device__ __forceinline__ void repack(ldsd* dst, int w, const ldsd* st, int sh, int cols, int rows, int tid, int nthr) {
+    for (int e = tid; e < rows * w; e += nthr) {
+        const int r = e / w, c = e - r * w;
+        dst[e] = c < cols ? st[sh + r * cols + c] : 0.0;
+    }
+}
+
+// per-subtree level ranges, precomputed on the host: {lo, hi, off, 0} per level
+__device__ __forceinline__ void load_level(Prologue& pl, Rec r, int l) {
+    pl.lo[l] = r.x;
+    pl.hi[l] = r.y;
+    pl.off[l] = r.z;
+}
+
+// table sizes in doubles (host mirrors these in raocp_capi.hip)
 template <int NXc, int NUc>
-__global__ void __launch_bounds__(512) k_dyn_bottom_back(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
-                                                          double* qbuf_, double* dbuf_, int s) {
+struct TabSize {
+    int W1, RG1, KM1, F1;  // per kind / class / class / pair
+    __device__ __forceinline__ TabSize(const Geo<NXc, NUc>& g) {
+        W1 = g.R * g.SKP;
+        RG1 = g.R * g.SNU;
+        KM1 = g.nu * g.SKP;
+        F1 = g.nx * g.SKF;
+    }
+};
+
+// LDS plan (doubles from the dynamic base), tier backward:
+//   [W (all kinds) | RG (classes c0..c1) | XQ rows (all subtree nodes, KP) | U rows (nonleaf, NUP)
+//    | P rows (maxch, PS) | NL records | CH records | staging: raw x rows, raw u rows]
+// The boundary level (s1) holds the leaves' x (q = -x) or q of the next tier's roots.
+template <int NXc, int NUc>
+__global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                                double* qbuf_, double* dbuf_, int s, int s1, int maxch,
+                                                                int c0, int c1, const Rec* __restrict__ sub_lv) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
-    __shared__ int lo[kMaxLevels + 1], hi[kMaxLevels + 1], off[kMaxLevels + 1];
-    if (ctl && ctl->done) return;
+    __shared__ Prologue pl;
+    const int done = ctl ? ctl->done : 0;
+    const Geo<NXc, NUc> g(p);
+    const TabSize<NXc, NUc> ts(g);
+    const int tid = threadIdx.x, nthr = blockDim.x;
     ldsd* smem = (ldsd*)smem_;
+    const int L = s1 - s;
+    const bool leaves = s1 == p.N;
+    const int oW = 0, oRG = oW + p.nkind * ts.W1, oXQ = oRG + (c1 - c0) * ts.RG1;
+    dma(smem + oW, p.dW, p.nkind * ts.W1);
+    dma(smem + oRG, p.dRG + (size_t)c0 * ts.RG1, (c1 - c0) * ts.RG1);
+    if (tid <= L) load_level(pl, sub_lv[(size_t)blockIdx.x * (L + 1) + tid], tid);
     glbd* z = dyn_z(bf, zsel, ctl);
-    glbd* qbuf = (glbd*)qbuf_;
-    glbd* dbuf = (glbd*)dbuf_;
-    const Dims<NXc, NUc> D(p);
-    const int nx = D.nx, nu = D.nu;
-    const int L = p.N - s;
-    const int root = p.stage_ptr[s] + blockIdx.x;
-    ldsd* s_h = smem;
-    ldsd* s_d = smem + blockDim.x;
-    ldsd* qL;
-    const LMats mt = stage_mats<NXc, NUc>(p, s_d + blockDim.x, p.cls_ptr[s], p.cls_ptr[p.N], &qL);
-    subtree_levels(p, root, L, lo, hi, off);  // ends with a barrier (also covers the staging)
-    const InfoT<glbrec*> inf{(glbrec*)p.ninfo, 0, (glbrec*)p.cinfo, 0};
-    const GRows xg{z + p.X0, 0, nx}, ug{z + p.U0, 0, nu}, dg{dbuf, 0, nu}, qroot{qbuf, 0, nx};
+    lds_sync();
+    const int nall = pl.off[L] + (pl.hi[L] - pl.lo[L]), nnl = pl.off[L];
+    ldsd* XQ = smem + oXQ;
+    ldsd* U = XQ + (size_t)nall * g.KP;
+    ldsd* PB = U + (size_t)nnl * g.NUP;
+    ldsd* NLd = PB + rup(maxch * g.PS, 2);
+    ldsd* CHd = NLd + 2 * nnl;
+    ldsd* ST = CHd + 2 * (nall - 1);  // staging, per level: x rows (+2 slack), then u rows (+2)
+    {
+        int so = 0;
+        for (int l = 0; l <= L; ++l) {
+            const int cnt = pl.hi[l] - pl.lo[l];
+            if (l < L || leaves) {
+                dma_u(ST + so, (const double*)z + p.X0 + (size_t)pl.lo[l] * g.nx, cnt * g.nx);
+                so += rup(cnt * g.nx + 2, 2);
+            } else {  // q rows of the next tier's roots, already padded
+                dma(XQ + (size_t)pl.off[l] * g.KP, qbuf_ + (size_t)pl.lo[l] * g.KP, cnt * g.KP);
+            }
+            if (l < L) {
+                dma_u(ST + so, (const double*)z + p.U0 + (size_t)pl.lo[l] * g.nu, cnt * g.nu);
+                so += rup(cnt * g.nu + 2, 2);
+                dma(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt);
+            }
+            if (l > 0) dma(CHd + 2 * (pl.off[l] - 1), (const double*)(p.cinfo + pl.lo[l]), 2 * cnt);
+        }
+    }
+    dma_wait();
+    lds_sync();
+    if (done) return;
+    {
+        int so = 0;
+        for (int l = 0; l <= L; ++l) {
+            const int cnt = pl.hi[l] - pl.lo[l];
+            if (l < L || leaves) {
+                const int sh = (int)(((uintptr_t)((const double*)z + p.X0 + (size_t)pl.lo[l] * g.nx) >> 3) & 1);
+                repack(XQ + (size_t)pl.off[l] * g.KP, g.KP, ST + so, sh, g.nx, cnt, tid, nthr);
+                so += rup(cnt * g.nx + 2, 2);
+            }
+            if (l < L) {
+                const int sh = (int)(((uintptr_t)((const double*)z + p.U0 + (size_t)pl.lo[l] * g.nu) >> 3) & 1);
+                repack(U + (size_t)pl.off[l] * g.NUP, g.NUP, ST + so, sh, g.nu, cnt, tid, nthr);
+                so += rup(cnt * g.nu + 2, 2);
+            }
+        }
+    }
+    zero_fill(PB, maxch * g.PS, tid, nthr);
+    lds_sync();
+    const ldsrec* NL = (const ldsrec*)NLd;
+    const ldsrec* CH = (const ldsrec*)CHd;
+    const TabsT<const ldsd*, const ldsd*> tb{smem + oW, smem + oRG, nullptr, nullptr, c0, 0};
+    const GRows dg{(glbd*)dbuf_, 0, g.nu};
     for (int l = L - 1; l >= 0; --l) {
-        const LRows qmine{qL + (size_t)off[l] * nx, lo[l], nx};
-        if (l + 1 == L) {  // children are leaves: q_j = -x_j
-            if (l == 0) back_step<NXc, NUc>(p, mt, inf, lo[l], hi[l], xg, -1.0, xg, ug, qroot, dg, s_h, s_d, 0, 1);
-            else back_step<NXc, NUc>(p, mt, inf, lo[l], hi[l], xg, -1.0, xg, ug, qmine, dg, s_h, s_d, 0, 1);
+        const InfoT<const ldsrec*> inf{NL + pl.off[l], pl.lo[l], CH + pl.off[l + 1] - 1, pl.lo[l + 1]};
+        const LRows xq_l{XQ + (size_t)pl.off[l] * g.KP, pl.lo[l], g.KP};
+        const LRows xq_c{XQ + (size_t)pl.off[l + 1] * g.KP, pl.lo[l + 1], g.KP};
+        const LRows pr{PB, pl.lo[l + 1], g.PS};
+        back_phase_a<NXc, NUc>(p, tb, inf, pl.lo[l + 1], pl.hi[l + 1], xq_c, (l + 1 == L && leaves) ? -1.0 : 1.0, pr,
+                               tid, nthr);
+        lds_sync();
+        const LRows ur{U + (size_t)pl.off[l] * g.NUP, pl.lo[l], g.NUP};
+        if (l > 0) {
+            back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, xq_l, dg, tid, nthr);
         } else {
-            const LRows qkids{qL + (size_t)off[l + 1] * nx, lo[l + 1], nx};
-            if (l == 0) back_step<NXc, NUc>(p, mt, inf, lo[l], hi[l], qkids, 1.0, xg, ug, qroot, dg, s_h, s_d, 0, 1);
-            else back_step<NXc, NUc>(p, mt, inf, lo[l], hi[l], qkids, 1.0, xg, ug, qmine, dg, s_h, s_d, 0, 1);
+            const GRows qroot{(glbd*)qbuf_, 0, g.KP};  // q of the subtree root, padded row
+            back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, qroot, dg, tid, nthr);
         }
+        lds_sync();
     }
 }
 
-template <int NXc, int NUc>
-__global__ void __launch_bounds__(512) k_dyn_bottom_fwd(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
-                                                         const double* dbuf_, int s) {
+// tier forward: [KM (classes c0..c1) | F (pairs p0..p1, if FL) | XD rows (nonleaf, KF) | NL | CH |
+//                staging: root x (+2), raw d rows per level (+2)]
+template <int NXc, int NUc, bool FL>
+__global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                               const double* dbuf_, int s, int s1, int c0, int c1,
+                                                               int p0, int p1, const Rec* __restrict__ sub_lv) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
-    __shared__ int lo[kMaxLevels + 1], hi[kMaxLevels + 1], off[kMaxLevels + 1];
-    if (ctl && ctl->done) return;
+    __shared__ Prologue pl;
+    const int done = ctl ? ctl->done : 0;
+    const Geo<NXc, NUc> g(p);
+    const TabSize<NXc, NUc> ts(g);
+    const int tid = threadIdx.x, nthr = blockDim.x;
     ldsd* smem = (ldsd*)smem_;
+    const int L = s1 - s;
+    const int oKM = 0, oF = oKM + (c1 - c0) * ts.KM1, oXD = oF + (FL ? (p1 - p0) * ts.F1 : 0);
+    dma(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1);
+    if (FL) dma(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
+    if (tid <= L) load_level(pl, sub_lv[(size_t)blockIdx.x * (L + 1) + tid], tid);
     glbd* z = dyn_z(bf, zsel, ctl);
-    const glbd* dbuf = (const glbd*)dbuf_;
-    const Dims<NXc, NUc> D(p);
-    const int nx = D.nx, nu = D.nu;
-    const int L = p.N - s;
-    const int root = p.stage_ptr[s] + blockIdx.x;
-    ldsd* xL;
-    const LMats mt = stage_mats<NXc, NUc>(p, smem, p.cls_ptr[s], p.cls_ptr[p.N], &xL);
-    subtree_levels(p, root, L, lo, hi, off);
-    ldsd* uL = xL + (size_t)off[L] * nx;
-    const InfoT<glbrec*> inf{(glbrec*)p.ninfo, 0, (glbrec*)p.cinfo, 0};
-    const RowsT<const glbd*> dg{dbuf, 0, nu};
-    const LRows none{nullptr, 0, 0};
+    lds_sync();
+    const int nall = pl.off[L] + (pl.hi[L] - pl.lo[L]), nnl = pl.off[L];
+    const int root = pl.lo[0];
+    ldsd* XD = smem + oXD;
+    ldsd* NLd = XD + (size_t)nnl * g.KF;
+    ldsd* CHd = NLd + 2 * nnl;
+    ldsd* ST = CHd + 2 * (nall - 1);
+    const double* xroot = (const double*)z + p.X0 + (size_t)root * g.nx;
+    const int shx = dma_u(ST, xroot, g.nx);
+    {
+        int so = rup(g.nx + 2, 2);
+        for (int l = 0; l < L; ++l) {
+            const int cnt = pl.hi[l] - pl.lo[l];
+            dma_u(ST + so, dbuf_ + (size_t)pl.lo[l] * g.nu, cnt * g.nu);
+            so += rup(cnt * g.nu + 2, 2);
+            dma(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt);
+            const int cc = pl.hi[l + 1] - pl.lo[l + 1];
+            dma(CHd + 2 * (pl.off[l + 1] - 1), (const double*)(p.cinfo + pl.lo[l + 1]), 2 * cc);
+        }
+    }
+    dma_wait();
+    lds_sync();
+    if (done) return;
+    // XD rows = [x (root only; others written by the sweep) | d | 0]
+    {
+        for (int e = tid; e < g.nx; e += nthr) XD[e] = ST[shx + e];
+        int so = rup(g.nx + 2, 2);
+        for (int l = 0; l < L; ++l) {
+            const int cnt = pl.hi[l] - pl.lo[l];
+            const int sh = (int)(((uintptr_t)(dbuf_ + (size_t)pl.lo[l] * g.nu) >> 3) & 1);
+            const int w = g.KF - g.nx;
+            for (int e = tid; e < cnt * w; e += nthr) {
+                const int r = e / w, c = e - r * w;
+                XD[(size_t)(pl.off[l] + r) * g.KF + g.nx + c] = c < g.nu ? ST[so + sh + r * g.nu + c] : 0.0;
+            }
+            so += rup(cnt * g.nu + 2, 2);
+        }
+    }
+    lds_sync();
+    const ldsrec* NL = (const ldsrec*)NLd;
+    const ldsrec* CH = (const ldsrec*)CHd;
+    typedef typename std::conditional<FL, const ldsd*, const glbd*>::type PF;
+    const TabsT<const ldsd*, PF> tb{nullptr, nullptr, smem + oKM,
+                                    FL ? (PF)(smem + oF) : (PF)((const glbd*)p.dF), c0, FL ? p0 : 0};
     for (int l = 0; l < L; ++l) {
-        const LRows uio{uL + (size_t)off[l] * nu, lo[l], nu};
-        const bool more = l + 1 < L;
-        const LRows xo = more ? LRows{xL + (size_t)off[l + 1] * nx, lo[l + 1], nx} : none;
-        if (l == 0) {
-            const GRows xin{z + p.X0, 0, nx};
-            if (more) fwd_step<NXc, NUc, true>(p, mt, inf, lo[l], hi[l], xin, dg, uio, z, xo);
-            else fwd_step<NXc, NUc, false>(p, mt, inf, lo[l], hi[l], xin, dg, uio, z, xo);
+        const InfoT<const ldsrec*> inf{NL + pl.off[l], pl.lo[l], CH + pl.off[l + 1] - 1, pl.lo[l + 1]};
+        const LRows xd_l{XD + (size_t)pl.off[l] * g.KF, pl.lo[l], g.KF};
+        if (l + 1 < L) {
+            const LRows xd_c{XD + (size_t)pl.off[l + 1] * g.KF, pl.lo[l + 1], g.KF};
+            fwd_phase<NXc, NUc, true>(p, tb, inf, pl.lo[l], pl.hi[l], xd_l, z, xd_c, tid, nthr);
         } else {
-            const LRows xin{xL + (size_t)off[l] * nx, lo[l], nx};
-            if (more) fwd_step<NXc, NUc, true>(p, mt, inf, lo[l], hi[l], xin, dg, uio, z, xo);
-            else fwd_step<NXc, NUc, false>(p, mt, inf, lo[l], hi[l], xin, dg, uio, z, xo);
+            fwd_phase<NXc, NUc, false>(p, tb, inf, pl.lo[l], pl.hi[l], xd_l, z, xd_l, tid, nthr);
         }
+        lds_sync();
     }
 }
 
-// the top of the tree (stages < s, nodes 0..T-1) in one workgroup, everything in LDS
-template <int NXc, int NUc>
-__global__ void __launch_bounds__(1024) k_dyn_top(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
-                                                   const double* qbuf_, const double* x0_, int s) {
+// the top of the tree (stages < s, nodes 0..T-1) in one workgroup, backward then forward:
+//   [W | RG | KM | F (if FL) | XQ (T, KP) | QB (boundary, KP) | U (T, NUP) | XD (T, KF) |
+//    P (maxch, PS) | NL (T) | CH (T + nb - 1) | staging: x rows (T, +2), boundary x (+2), u rows (+2)]
+template <int NXc, int NUc, bool FL>
+__global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                        const double* qbuf_, const double* x0_, int s, int maxch,
+                                                        int c1, int p1, int T, int nb) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
-    if (ctl && ctl->done) return;
-    stamp(p, 0);
+    __shared__ Prologue pl;
+    tstamp(p, pl, 0);
+    const int done = ctl ? ctl->done : 0;
+    const Geo<NXc, NUc> g(p);
+    const TabSize<NXc, NUc> ts(g);
+    const int tid = threadIdx.x, nthr = blockDim.x;
     ldsd* smem = (ldsd*)smem_;
-    glbd* z = dyn_z(bf, zsel, ctl);
-    const glbd* qbuf = (const glbd*)qbuf_;
-    const glbd* x0 = (const glbd*)x0_;
-    const Dims<NXc, NUc> D(p);
-    const int nx = D.nx, nu = D.nu;
-    const int T = p.stage_ptr[s];
-    const int nb = p.stage_ptr[s + 1] - T;  // boundary nodes (stage s)
     const bool leaves = s == p.N;
-    ldsd* s_h = smem;
-    ldsd* s_d = smem + blockDim.x;
-    ldsd* xS;
-    const LMats mt = stage_mats<NXc, NUc>(p, s_d + blockDim.x, 0, p.cls_ptr[s], &xS);  // x rows of the top
-    ldsd* uS = xS + (size_t)T * nx;  // u rows (inputs, then outputs)
-    ldsd* qT = uS + (size_t)T * nu;
-    ldsd* dT = qT + (size_t)T * nx;
-    ldsd* qB = dT + (size_t)T * nu;  // boundary rows: q of stage s (or x of the leaves)
-    ldsrec* nlS = (ldsrec*)(qB + (((size_t)nb * nx + 1) & ~(size_t)1));  // nonleaf records 0..T-1
-    ldsrec* chS = nlS + T;                                              // child records 1..T+nb-1
-    lds_copy(xS, z + p.X0, (size_t)T * nx);
-    lds_copy(uS, z + p.U0, (size_t)T * nu);
-    lds_copy(qB, leaves ? z + p.X0 + (size_t)T * nx : qbuf + (size_t)T * nx, (size_t)nb * nx);
-    for (int t = threadIdx.x; t < T; t += blockDim.x) nlS[t] = p.ninfo[t];
-    for (int t = threadIdx.x; t < T + nb - 1; t += blockDim.x) chS[t] = p.cinfo[t + 1];
-    __syncthreads();
-    stamp(p, 1);
-    const InfoT<const ldsrec*> inf{nlS, 0, chS, 1};
-    const LRows xr{xS, 0, nx}, ur{uS, 0, nu}, qr{qT, 0, nx}, dr{dT, 0, nu}, qbr{qB, T, nx};
+    const int oW = 0, oRG = oW + p.nkind * ts.W1, oKM = oRG + c1 * ts.RG1, oF = oKM + c1 * ts.KM1;
+    const int oXQ = oF + (FL ? p1 * ts.F1 : 0), oQB = oXQ + T * g.KP, oU = oQB + nb * g.KP, oXD = oU + T * g.NUP;
+    const int oP = oXD + T * g.KF, oNL = oP + rup(maxch * g.PS, 2), oCH = oNL + 2 * T, oST = oCH + 2 * (T + nb - 1);
+    dma(smem + oW, p.dW, p.nkind * ts.W1);
+    dma(smem + oRG, p.dRG, c1 * ts.RG1);
+    dma(smem + oKM, p.dKM, c1 * ts.KM1);
+    if (FL) dma(smem + oF, p.dF, p1 * ts.F1);
+    dma(smem + oNL, (const double*)p.ninfo, 2 * T);
+    dma(smem + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1));
+    if (tid <= s + 1) pl.sp[tid] = p.stage_ptr[tid];
+    glbd* z = dyn_z(bf, zsel, ctl);
+    ldsd* ST = smem + oST;
+    const int so_b = rup(T * g.nx + 2, 2), so_u = so_b + (leaves ? rup(nb * g.nx + 2, 2) : 0);
+    const int shx = dma_u(ST, (const double*)z + p.X0, T * g.nx);
+    int shb = 0;
+    if (leaves) shb = dma_u(ST + so_b, (const double*)z + p.X0 + (size_t)T * g.nx, nb * g.nx);
+    else dma(smem + oQB, qbuf_ + (size_t)T * g.KP, nb * g.KP);
+    const int shu = dma_u(ST + so_u, (const double*)z + p.U0, T * g.nu);
+    dma_wait();
+    lds_sync();
+    if (done) return;
+    tstamp(p, pl, 2 + 3 * s);
+    repack(smem + oXQ, g.KP, ST, shx, g.nx, T, tid, nthr);
+    if (leaves) repack(smem + oQB, g.KP, ST + so_b, shb, g.nx, nb, tid, nthr);
+    repack(smem + oU, g.NUP, ST + so_u, shu, g.nu, T, tid, nthr);
+    zero_fill(smem + oXD, T * g.KF, tid, nthr);
+    zero_fill(smem + oP, maxch * g.PS, tid, nthr);
+    lds_sync();
+    tstamp(p, pl, 1);
+    tstamp(p, pl, 3 + 3 * s);
+    typedef typename std::conditional<FL, const ldsd*, const glbd*>::type PF;
+    const TabsT<const ldsd*, PF> tb{smem + oW, smem + oRG, smem + oKM,
+                                    FL ? (PF)(smem + oF) : (PF)((const glbd*)p.dF), 0, 0};
+    const InfoT<const ldsrec*> inf{(const ldsrec*)(smem + oNL), 0, (const ldsrec*)(smem + oCH), 1};
+    ldsd* XD = smem + oXD;
+    const LRows xq{smem + oXQ, 0, g.KP}, qb{smem + oQB, T, g.KP}, ur{smem + oU, 0, g.NUP}, xd{XD, 0, g.KF};
+    const LRows dlds{XD + g.nx, 0, g.KF};  // d_i into XD row i, cols nx..
     for (int t = s - 1; t >= 0; --t) {
-        const int b = p.stage_ptr[t], e = p.stage_ptr[t + 1];
-        if (t + 1 < s) back_step<NXc, NUc>(p, mt, inf, b, e, qr, 1.0, xr, ur, qr, dr, s_h, s_d, 0, 1);
-        else back_step<NXc, NUc>(p, mt, inf, b, e, qbr, leaves ? -1.0 : 1.0, xr, ur, qr, dr, s_h, s_d, 0, 1);
-        stamp(p, 2 + (s - 1 - t));
+        const int b = pl.sp[t], e = pl.sp[t + 1];
+        const int cb = e, ce = pl.sp[t + 2];
+        const LRows pr{smem + oP, cb, g.PS};
+        if (t + 1 < s) back_phase_a<NXc, NUc>(p, tb, inf, cb, ce, xq, 1.0, pr, tid, nthr);
+        else back_phase_a<NXc, NUc>(p, tb, inf, cb, ce, qb, leaves ? -1.0 : 1.0, pr, tid, nthr);
+        lds_sync();
+        tstamp(p, pl, 2 + 2 * (s - 1 - t));
+        back_phase_b<NXc, NUc>(p, tb, inf, b, e, pr, xq, ur, xq, dlds, tid, nthr);
+        lds_sync();
+        tstamp(p, pl, 3 + 2 * (s - 1 - t));
     }
-    if ((int)threadIdx.x < nx) {
-        xS[threadIdx.x] = x0[threadIdx.x];
-        z[p.X0 + threadIdx.x] = x0[threadIdx.x];  // x_0 = x0bar (cache.py:282)
+    if (tid < g.nx) {
+        const double v = ((const glbd*)x0_)[tid];
+        XD[tid] = v;
+        z[p.X0 + tid] = v;  // x_0 = x0bar (cache.py:282)
     }
-    __syncthreads();
+    lds_sync();
     for (int t = 0; t < s; ++t) {
-        const int b = p.stage_ptr[t], e = p.stage_ptr[t + 1];
-        if (t + 1 < s) fwd_step<NXc, NUc, true>(p, mt, inf, b, e, xr, dr, ur, z, xr);
-        else fwd_step<NXc, NUc, false>(p, mt, inf, b, e, xr, dr, ur, z, xr);
-        stamp(p, 2 + s + t);
+        const int b = pl.sp[t], e = pl.sp[t + 1];
+        if (t + 1 < s) fwd_phase<NXc, NUc, true>(p, tb, inf, b, e, xd, z, xd, tid, nthr);
+        else fwd_phase<NXc, NUc, false>(p, tb, inf, b, e, xd, z, xd, tid, nthr);
+        lds_sync();
+        tstamp(p, pl, 2 + 2 * s + t);
     }
+    tflush(p, pl, 4 + 3 * s);
 }

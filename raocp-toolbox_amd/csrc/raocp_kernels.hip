@@ -14,6 +14,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 namespace raocp {
 
@@ -70,12 +71,12 @@ struct Dev {
     const double* alpha_r; const double* cond;
     const double* blo_nl; const double* bhi_nl; const double* blo_l; const double* bhi_l;
     const int* iBnl; const int* iBl;
-    // dynamics projection (raocp_dyn.hip): padded per-mode A, B and per-class Rinv, K, M
-    const double* Ap; const double* Bp; const double* Rp; const double* Kp; const double* Mp;
-    int nA, nB;
+    // dynamics projection (raocp_dyn.hip header): per child kind W = [B'; A'], per class
+    // RG = [R~^-1; G] and K, per (kind, parent class) pair F = [Abar | B]; padded rows
+    const double* dW; const double* dRG; const double* dKM; const double* dF;
+    int nkind;             // number of child kinds (rows of W)
     const Rec* ninfo;      // [m] {ch_start, nch, class, stage}
-    const Rec* cinfo;      // [n] {iA, iB, anc, 0} (node 0: unused)
-    const int* cls_ptr;    // [N+1] first class of each stage (classes numbered by stage)
+    const Rec* cinfo;      // [n] {kind, pair, anc, 0} (node 0: unused)
     const int* stage_ptr;  // [N+2] first node id of each stage (BFS numbering)
     int N;                 // last stage
     unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)

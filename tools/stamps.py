@@ -9,8 +9,14 @@ tree, prob = build_problem(r)
 cache = core.Cache(prob)
 cache.cache_initial_state(r["x0"])
 cache.set_primal_flat(np.random.default_rng(0).standard_normal(cache.primal_size))
-for rep in range(3):
+for rep in range(5):
     st = cache.native.debug_dyn_stamps(64).astype(np.int64)
-nz = st[st > 0]
-d = np.diff(st[:np.count_nonzero(st)]) * 10  # ns
-print("stamps (ns deltas):", d.tolist(), "total us", (nz[-1] - nz[0]) / 100)
+k = np.count_nonzero(st)
+s = (k - 4) // 3
+main = st[:2 + 3 * s]
+d = np.diff(main) * 10  # ns
+pro = (st[2 + 3 * s:4 + 3 * s] - st[0]) * 10
+print(f"top kernel (cut s={s}): prologue {d[0]} ns (segments built at {pro[0]}, gather done at {pro[1]})")
+print("  backward (phase A, phase B) per stage s-1..0:", [(int(d[1 + 2 * i]), int(d[2 + 2 * i])) for i in range(s)])
+print("  forward per stage 0..s-1:", [int(v) for v in d[1 + 2 * s:]])
+print("  total us", (main[-1] - main[0]) / 100)
