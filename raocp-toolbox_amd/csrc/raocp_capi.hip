@@ -37,6 +37,9 @@ int fail(int code, const std::string& msg) {
 
 int cdiv(int a, int b) { return b <= 0 ? 0 : (a + b - 1) / b; }
 
+// CP iterations per captured graph: a multiple of 6 (buffer rotation period, see rotated())
+constexpr int kGraphBatch = 24;
+
 }  // namespace
 
 struct raocp_ctx {
@@ -68,6 +71,7 @@ struct raocp_ctx {
         size_t lds_b, lds_f;
         bool fl;                 // F staged in LDS by the forward kernel
         const raocp::Rec* lv;    // level ranges of its subtrees
+        raocp::TierArg ta;       // the same, as a kernel argument, when the tier is regular
     };
     std::vector<TierPlan> tiers;
     double* x0 = nullptr;
@@ -215,6 +219,13 @@ struct DynOp {
     void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl) {
         const int s = c->cut;
         const int B = c->dyn_block;
+        // diagnostics: each launch stamps into its own 64-slot region
+        Dev dv = c->dev;
+        int slot = 0;
+        auto dev_for = [&]() {
+            if (c->dev.stamps) dv.stamps = c->dev.stamps + 64 * slot++;
+            return dv;
+        };
         if (s > 0) {
             // tiers below the top, deepest first (backward), the top, then the tiers (forward)
             for (int k = (int)c->tiers.size() - 1; k >= 0; --k) {
@@ -222,21 +233,22 @@ struct DynOp {
                 const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1];
                 auto kb = raocp::k_dyn_bottom_back<NX, NU>;
                 allow_lds(kb, tp.lds_b);
-                kb<<<tp.nsub, B, tp.lds_b, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->d, tp.s0, tp.s1, tp.maxch, c0, c1,
-                                                        tp.lv);
+                kb<<<tp.nsub, B, tp.lds_b, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->d, tp.s0, tp.s1, tp.maxch, c0, c1,
+                                                        tp.lv, tp.ta);
             }
             {
                 const int c1 = c->cls_ptr[s], p1 = c->pair_ptr[c1];
                 auto kt = c->f_lds_top ? raocp::k_dyn_top<NX, NU, true> : raocp::k_dyn_top<NX, NU, false>;
                 allow_lds(kt, c->lds_top);
                 const int T = c->stage_ptr[s], nb = c->stage_ptr[s + 1] - T;
-                kt<<<1, B, c->lds_top, c->stream>>>(c->dev, bf, ctl, zsel, c->q, c->x0, s, c->maxch_top, c1, p1, T, nb);
+                kt<<<1, B, c->lds_top, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->x0, s, c->maxch_top, c1, p1, T, nb);
             }
             for (const auto& tp : c->tiers) {
                 const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1], p0 = c->pair_ptr[c0], p1 = c->pair_ptr[c1];
                 auto kf = tp.fl ? raocp::k_dyn_bottom_fwd<NX, NU, true> : raocp::k_dyn_bottom_fwd<NX, NU, false>;
                 allow_lds(kf, tp.lds_f);
-                kf<<<tp.nsub, B, tp.lds_f, c->stream>>>(c->dev, bf, ctl, zsel, c->d, tp.s0, tp.s1, c0, c1, p0, p1, tp.lv);
+                kf<<<tp.nsub, B, tp.lds_f, c->stream>>>(dev_for(), bf, ctl, zsel, c->d, tp.s0, tp.s1, c0, c1, p0, p1, tp.lv,
+                                                        tp.ta);
             }
             return;
         }
@@ -303,10 +315,21 @@ void launch_cp_dual(raocp_ctx* c, bool with_l, double* dsolo, int mode = raocp::
     dispatch(c->nx, c->nu, CpDualOp{}, c, with_l, dsolo, mode);
 }
 
-void enqueue_cp_iteration(raocp_ctx* c) {
+// One CP iteration for iteration index `it` within a graph batch. Graph batches are a
+// multiple of 6 iterations and always start at k = 0 mod 6, so the buffer rotation
+// Z[k % 3], E[k % 2] is static per captured node: the kernels get the buffers already
+// rotated and never read the iteration counter to choose them.
+raocp::Bufs rotated(raocp_ctx* c, int it) {
+    return raocp::Bufs{c->Z[it % 3], c->Z[(it + 1) % 3], c->Z[(it + 2) % 3], c->E[it % 2], c->E[(it + 1) % 2]};
+}
+
+void enqueue_cp_iteration(raocp_ctx* c, int it) {
+    const raocp::Bufs keep = c->bufs;
+    c->bufs = rotated(c, it);
     launch_dynamics(c, c->bufs, 1, c->ctl);
     launch_cp_dual(c, true, nullptr);
     launch_cp_primal(c, true);
+    c->bufs = keep;
     raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->red_rows);
 }
 
@@ -365,7 +388,7 @@ int ensure_graph(raocp_ctx* c, int iters) {
     }
     hipGraph_t g = nullptr;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (int it = 0; it < iters; ++it) enqueue_cp_iteration(c);
+    for (int it = 0; it < iters; ++it) enqueue_cp_iteration(c, it);
     HIPCHK(hipStreamEndCapture(c->stream, &g));
     hipError_t e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
     (void)hipGraphDestroy(g);
@@ -653,9 +676,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             maxch = 0;
             for (int st = 1; st <= s_; ++st) maxch = std::max(maxch, stage_n(st));
             const size_t mats = c->nkind * W1 + cp[s_] * (RG1 + KM1) + (fl ? pp[cp[s_]] * F1 : 0);
-            const size_t stage = T * (nx + nu) + (s_ == N ? nb * nx : 0) + 12;  // raw rows for the repack
             const size_t dbl = mats + T * KP + nb * KP + T * NUP + T * KF + raocp::rup(maxch * PS, 2) +
-                               recs(T + T + nb - 1) + stage;
+                               recs(T + T + nb - 1);
             return 8 * dbl;
         };
         struct Tier {
@@ -686,8 +708,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             }
             for (double v : lvl) w.cost += v;
             const size_t ncl = cp[b] - cp[a], npr = pp[cp[b]] - pp[cp[a]];
-            const size_t st_b = w.nall * nx + w.nnl * nu + 4 * (b - a + 2);  // staging of raw rows
-            const size_t st_f = w.nnl * nu + nx + 4 * (b - a + 2);
+            const size_t st_b = 0, st_f = 0;
             w.bb = 8 * (c->nkind * W1 + ncl * RG1 + w.nall * KP + w.nnl * NUP + raocp::rup(w.maxch * PS, 2) +
                         recs(w.nnl + w.nall - 1) + st_b);
             w.bf = 8 * (ncl * KM1 + npr * F1 + w.nnl * KF + recs(w.nnl + w.nall - 1) + st_f);
@@ -769,6 +790,21 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 }
             }
             if ((rc = c->upload_vec(&tp.lv, lv))) return bail(rc);
+            // regular tier: every subtree has the same level sizes and consecutive ids
+            memset(&tp.ta, 0, sizeof(tp.ta));
+            tp.ta.regular = 1;
+            for (int l = 0; l <= L; ++l) {
+                tp.ta.lo0[l] = lv[l].x;
+                tp.ta.cnt[l] = lv[l].y - lv[l].x;
+            }
+            for (int r = 0; r < tp.nsub && tp.ta.regular; ++r)
+                for (int l = 0; l <= L; ++l) {
+                    const raocp::Rec& e = lv[(size_t)r * (L + 1) + l];
+                    if (e.x != tp.ta.lo0[l] + r * tp.ta.cnt[l] || e.y - e.x != tp.ta.cnt[l]) {
+                        tp.ta.regular = 0;
+                        break;
+                    }
+                }
             c->tiers.push_back(tp);
         }
         if (getenv("RAOCP_DYN_VERBOSE")) {
@@ -793,6 +829,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         (rc = c->alloc(&c->tmpD, c->D)) || (rc = c->alloc(&c->part, 1024)) || (rc = c->alloc(&c->scal, 8)))
         return bail(rc);
     if (hipHostMalloc((void**)&c->h_ctl, sizeof(Ctl), 0) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "hipHostMalloc"));
+    {
+        double* zp = nullptr;
+        if ((rc = c->alloc(&zp, 16))) return bail(rc);
+        if (hipMemset(zp, 0, 16 * sizeof(double)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
+        c->dev.zpage = zp;
+    }
     {
         const int g_dual = groups(nx + nu + 2, n - 1).blocks + groups(2 * cmax + 2 + nx + nu, m).blocks +
                            groups(2 * nx + 2, n - m).blocks;
@@ -1096,7 +1138,7 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     if ((rc = ensure_hist(c, (size_t)max_iters + 1))) return rc;
     if ((rc = raocp_set_initial_state(c, x0))) return rc;
     if ((rc = cp_init(c, x0, max_iters, tol, alpha))) return rc;
-    const int batch = 16;
+    const int batch = kGraphBatch;
     if ((rc = ensure_graph(c, batch))) return rc;
     for (;;) {
         HIPCHK(hipGraphLaunch(c->graph, c->stream));
@@ -1124,7 +1166,7 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     if (!c || !x0 || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
     int rc;
     if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
-    const int batch = 16;
+    const int batch = kGraphBatch;
     if ((rc = ensure_graph(c, batch))) return rc;
     if ((rc = cp_init(c, x0, iters - 1, 0.0, alpha))) return rc;
     hipEvent_t e0, e1;

@@ -301,9 +301,8 @@ __device__ __forceinline__ glbd* pick3(const Bufs& bf, int k) {
     return (glbd*)(w == 0 ? bf.z0 : (w == 1 ? bf.z1 : bf.z2));
 }
 
-__device__ __forceinline__ glbd* dyn_z(const Bufs& bf, int zsel, const Ctl* ctl) {
-    return pick3(bf, (ctl ? ctl->k : 0) + zsel);
-}
+// the iterate the sweep projects: buffers arrive rotated for the iteration, so no ctl read
+__device__ __forceinline__ glbd* dyn_z(const Bufs& bf, int zsel, const Ctl*) { return pick3(bf, zsel); }
 
 // copy `rows` rows of `cols` doubles (source stride sstride) into padded rows of stride
 // dstride, zero tail; loads batched so several are in flight per thread
@@ -440,38 +439,72 @@ __device__ __forceinline__ void tflush(const Dev& p, const Prologue& pl, int n) 
 }
 
 // Prologue copies are LDS-DMA (global_load_lds_dwordx4): every wave issues its share of
-// 16-B chunks of a contiguous global range straight into LDS, nothing waits until the
-// single vmcnt(0) at the end, so a prologue costs about one memory round trip.
-// dst and src are 16-B aligned; n (doubles) is rounded up to even (sources have slack).
-__device__ __forceinline__ void dma(ldsd* dst, const double* src, int n) {
+// 16-B chunks straight into LDS and nothing waits until the single vmcnt(0) at the end,
+// so a prologue costs about one memory round trip. The destination of one wave
+// instruction is linear (base + lane * 16 B), the source is per lane: padded rows are
+// filled chunk by chunk, tail chunks reading a page of zeros (p.zpage).
+template <class SrcF>
+__device__ __forceinline__ void dma_gen(ldsd* dst, int chunks, SrcF src) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    const int chunks = (n + 1) >> 1;
     for (int c0 = wave * 64; c0 < chunks; c0 += nw * 64) {
         const int ch = c0 + lane;
-        if (ch < chunks) __builtin_amdgcn_global_load_lds((const glbd*)src + 2 * ch, dst + 2 * c0, 16, 0, 0);
+        if (ch < chunks) __builtin_amdgcn_global_load_lds((const glbd*)src(ch), dst + 2 * c0, 16, 0, 0);
     }
 }
-// unaligned source: copy from the 16-B boundary below; returns the shift (0 or 1 double)
-__device__ __forceinline__ int dma_u(ldsd* dst, const double* src, int n) {
-    const int sh = (int)(((uintptr_t)src >> 3) & 1);
-    dma(dst, src - sh, n + sh);
-    return sh;
+// contiguous range of n (even) doubles, 16-B aligned at both ends
+__device__ __forceinline__ void dma(ldsd* dst, const double* src, int n) {
+    dma_gen(dst, n >> 1, [=](int ch) { return src + 2 * ch; });
+}
+// rows x cols (even) doubles, source row stride sstride (even, rows 16-B aligned) ->
+// LDS rows of w (even) doubles with a zero tail
+__device__ __forceinline__ void dma_rows(ldsd* dst, int w, const double* src, int sstride, int cols, int rows,
+                                         const double* zp) {
+    const int cpr = w >> 1, cc = cols >> 1;
+    dma_gen(dst, rows * cpr, [=](int ch) {
+        const int r = ch / cpr, c = ch - r * cpr;
+        return c < cc ? src + (size_t)r * sstride + 2 * c : zp;
+    });
 }
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// staged raw rows (stride cols, shifted by sh) -> padded rows (stride w, zero tail)
-__device__ __forceinline__ void repack(ldsd* dst, int w, const ldsd* st, int sh, int cols, int rows, int tid, int nthr) {
+// register path for odd sizes / unaligned rows (same result as dma_rows; used only when
+// nx or nu is odd)
+__device__ __forceinline__ void copy_rows_reg(ldsd* dst, int w, const double* src, int sstride, int cols, int rows,
+                                              int tid, int nthr) {
     for (int e = tid; e < rows * w; e += nthr) {
         const int r = e / w, c = e - r * w;
-        dst[e] = c < cols ? st[sh + r * cols + c] : 0.0;
+        dst[e] = c < cols ? ((const glbd*)src)[(size_t)r * sstride + c] : 0.0;
     }
 }
+__device__ __forceinline__ void rows_in(bool dmaok, ldsd* dst, int w, const double* src, int sstride, int cols,
+                                        int rows, const double* zp, int tid, int nthr) {
+    if (dmaok) dma_rows(dst, w, src, sstride, cols, rows, zp);
+    else copy_rows_reg(dst, w, src, sstride, cols, rows, tid, nthr);
+}
 
-// per-subtree level ranges, precomputed on the host: {lo, hi, off, 0} per level
-__device__ __forceinline__ void load_level(Prologue& pl, Rec r, int l) {
-    pl.lo[l] = r.x;
-    pl.hi[l] = r.y;
-    pl.off[l] = r.z;
+// level ranges of a tier's subtree: from the kernel argument when the tier is regular
+// (every subtree the same shape, ids consecutive), else from the host table
+struct TierArg {
+    int regular;
+    int lo0[kMaxLevels + 1];
+    int cnt[kMaxLevels + 1];
+};
+
+__device__ __forceinline__ void tier_levels(Prologue& pl, const TierArg& ta, const Rec* __restrict__ sub_lv, int L) {
+    const int l = threadIdx.x;
+    if (l > L) return;
+    if (ta.regular) {
+        int off = 0;
+        for (int k = 0; k < l; ++k) off += ta.cnt[k];
+        pl.lo[l] = ta.lo0[l] + blockIdx.x * ta.cnt[l];
+        pl.hi[l] = pl.lo[l] + ta.cnt[l];
+        pl.off[l] = off;
+    } else {
+        const Rec r = sub_lv[(size_t)blockIdx.x * (L + 1) + l];
+        pl.lo[l] = r.x;
+        pl.hi[l] = r.y;
+        pl.off[l] = r.z;
+    }
 }
 
 // table sizes in doubles (host mirrors these in raocp_capi.hip)
@@ -488,17 +521,20 @@ struct TabSize {
 
 // LDS plan (doubles from the dynamic base), tier backward:
 //   [W (all kinds) | RG (classes c0..c1) | XQ rows (all subtree nodes, KP) | U rows (nonleaf, NUP)
-//    | P rows (maxch, PS) | NL records | CH records | staging: raw x rows, raw u rows]
+//    | P rows (maxch, PS) | NL records | CH records]
 // The boundary level (s1) holds the leaves' x (q = -x) or q of the next tier's roots.
 template <int NXc, int NUc>
 __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
                                                                 double* qbuf_, double* dbuf_, int s, int s1, int maxch,
-                                                                int c0, int c1, const Rec* __restrict__ sub_lv) {
+                                                                int c0, int c1, const Rec* __restrict__ sub_lv,
+                                                                TierArg ta) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
+    tstamp(p, pl, 0);
     const int done = ctl ? ctl->done : 0;
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
+    const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
     const int tid = threadIdx.x, nthr = blockDim.x;
     ldsd* smem = (ldsd*)smem_;
     const int L = s1 - s;
@@ -506,55 +542,36 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     const int oW = 0, oRG = oW + p.nkind * ts.W1, oXQ = oRG + (c1 - c0) * ts.RG1;
     dma(smem + oW, p.dW, p.nkind * ts.W1);
     dma(smem + oRG, p.dRG + (size_t)c0 * ts.RG1, (c1 - c0) * ts.RG1);
-    if (tid <= L) load_level(pl, sub_lv[(size_t)blockIdx.x * (L + 1) + tid], tid);
+    tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
     lds_sync();
+    tstamp(p, pl, 1);
     const int nall = pl.off[L] + (pl.hi[L] - pl.lo[L]), nnl = pl.off[L];
     ldsd* XQ = smem + oXQ;
     ldsd* U = XQ + (size_t)nall * g.KP;
     ldsd* PB = U + (size_t)nnl * g.NUP;
     ldsd* NLd = PB + rup(maxch * g.PS, 2);
     ldsd* CHd = NLd + 2 * nnl;
-    ldsd* ST = CHd + 2 * (nall - 1);  // staging, per level: x rows (+2 slack), then u rows (+2)
-    {
-        int so = 0;
-        for (int l = 0; l <= L; ++l) {
-            const int cnt = pl.hi[l] - pl.lo[l];
-            if (l < L || leaves) {
-                dma_u(ST + so, (const double*)z + p.X0 + (size_t)pl.lo[l] * g.nx, cnt * g.nx);
-                so += rup(cnt * g.nx + 2, 2);
-            } else {  // q rows of the next tier's roots, already padded
-                dma(XQ + (size_t)pl.off[l] * g.KP, qbuf_ + (size_t)pl.lo[l] * g.KP, cnt * g.KP);
-            }
-            if (l < L) {
-                dma_u(ST + so, (const double*)z + p.U0 + (size_t)pl.lo[l] * g.nu, cnt * g.nu);
-                so += rup(cnt * g.nu + 2, 2);
-                dma(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt);
-            }
-            if (l > 0) dma(CHd + 2 * (pl.off[l] - 1), (const double*)(p.cinfo + pl.lo[l]), 2 * cnt);
+    for (int l = 0; l <= L; ++l) {
+        const int cnt = pl.hi[l] - pl.lo[l];
+        if (l < L || leaves)
+            rows_in(dmaok, XQ + (size_t)pl.off[l] * g.KP, g.KP, (const double*)z + p.X0 + (size_t)pl.lo[l] * g.nx,
+                    g.nx, g.nx, cnt, p.zpage, tid, nthr);
+        else  // q rows of the next tier's roots, already padded
+            dma(XQ + (size_t)pl.off[l] * g.KP, qbuf_ + (size_t)pl.lo[l] * g.KP, cnt * g.KP);
+        if (l < L) {
+            rows_in(dmaok, U + (size_t)pl.off[l] * g.NUP, g.NUP, (const double*)z + p.U0 + (size_t)pl.lo[l] * g.nu,
+                    g.nu, g.nu, cnt, p.zpage, tid, nthr);
+            dma(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt);
         }
-    }
-    dma_wait();
-    lds_sync();
-    if (done) return;
-    {
-        int so = 0;
-        for (int l = 0; l <= L; ++l) {
-            const int cnt = pl.hi[l] - pl.lo[l];
-            if (l < L || leaves) {
-                const int sh = (int)(((uintptr_t)((const double*)z + p.X0 + (size_t)pl.lo[l] * g.nx) >> 3) & 1);
-                repack(XQ + (size_t)pl.off[l] * g.KP, g.KP, ST + so, sh, g.nx, cnt, tid, nthr);
-                so += rup(cnt * g.nx + 2, 2);
-            }
-            if (l < L) {
-                const int sh = (int)(((uintptr_t)((const double*)z + p.U0 + (size_t)pl.lo[l] * g.nu) >> 3) & 1);
-                repack(U + (size_t)pl.off[l] * g.NUP, g.NUP, ST + so, sh, g.nu, cnt, tid, nthr);
-                so += rup(cnt * g.nu + 2, 2);
-            }
-        }
+        if (l > 0) dma(CHd + 2 * (pl.off[l] - 1), (const double*)(p.cinfo + pl.lo[l]), 2 * cnt);
     }
     zero_fill(PB, maxch * g.PS, tid, nthr);
+    dma_wait();
     lds_sync();
+    tstamp(p, pl, 2);
+    if (done) return;
+    tstamp(p, pl, 3);
     const ldsrec* NL = (const ldsrec*)NLd;
     const ldsrec* CH = (const ldsrec*)CHd;
     const TabsT<const ldsd*, const ldsd*> tb{smem + oW, smem + oRG, nullptr, nullptr, c0, 0};
@@ -567,6 +584,7 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
         back_phase_a<NXc, NUc>(p, tb, inf, pl.lo[l + 1], pl.hi[l + 1], xq_c, (l + 1 == L && leaves) ? -1.0 : 1.0, pr,
                                tid, nthr);
         lds_sync();
+        tstamp(p, pl, 4 + 2 * (L - 1 - l));
         const LRows ur{U + (size_t)pl.off[l] * g.NUP, pl.lo[l], g.NUP};
         if (l > 0) {
             back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, xq_l, dg, tid, nthr);
@@ -575,67 +593,73 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
             back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, qroot, dg, tid, nthr);
         }
         lds_sync();
+        tstamp(p, pl, 5 + 2 * (L - 1 - l));
     }
+    tflush(p, pl, 4 + 2 * L);
 }
 
-// tier forward: [KM (classes c0..c1) | F (pairs p0..p1, if FL) | XD rows (nonleaf, KF) | NL | CH |
-//                staging: root x (+2), raw d rows per level (+2)]
+// tier forward: [KM (classes c0..c1) | F (pairs p0..p1, if FL) | XD rows (nonleaf, KF) | NL | CH]
+// XD rows = [x (the root's; the others are written by the sweep) | d | 0]
 template <int NXc, int NUc, bool FL>
 __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
                                                                const double* dbuf_, int s, int s1, int c0, int c1,
-                                                               int p0, int p1, const Rec* __restrict__ sub_lv) {
+                                                               int p0, int p1, const Rec* __restrict__ sub_lv,
+                                                               TierArg ta) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
+    tstamp(p, pl, 0);
     const int done = ctl ? ctl->done : 0;
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
+    const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
     const int tid = threadIdx.x, nthr = blockDim.x;
     ldsd* smem = (ldsd*)smem_;
     const int L = s1 - s;
     const int oKM = 0, oF = oKM + (c1 - c0) * ts.KM1, oXD = oF + (FL ? (p1 - p0) * ts.F1 : 0);
     dma(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1);
     if (FL) dma(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
-    if (tid <= L) load_level(pl, sub_lv[(size_t)blockIdx.x * (L + 1) + tid], tid);
+    tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
     lds_sync();
+    tstamp(p, pl, 1);
     const int nall = pl.off[L] + (pl.hi[L] - pl.lo[L]), nnl = pl.off[L];
     const int root = pl.lo[0];
     ldsd* XD = smem + oXD;
     ldsd* NLd = XD + (size_t)nnl * g.KF;
     ldsd* CHd = NLd + 2 * nnl;
-    ldsd* ST = CHd + 2 * (nall - 1);
     const double* xroot = (const double*)z + p.X0 + (size_t)root * g.nx;
-    const int shx = dma_u(ST, xroot, g.nx);
-    {
-        int so = rup(g.nx + 2, 2);
-        for (int l = 0; l < L; ++l) {
-            const int cnt = pl.hi[l] - pl.lo[l];
-            dma_u(ST + so, dbuf_ + (size_t)pl.lo[l] * g.nu, cnt * g.nu);
-            so += rup(cnt * g.nu + 2, 2);
-            dma(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt);
-            const int cc = pl.hi[l + 1] - pl.lo[l + 1];
-            dma(CHd + 2 * (pl.off[l + 1] - 1), (const double*)(p.cinfo + pl.lo[l + 1]), 2 * cc);
+    const double* zp = p.zpage;
+    for (int l = 0; l < L; ++l) {
+        const int cnt = pl.hi[l] - pl.lo[l];
+        ldsd* xd = XD + (size_t)pl.off[l] * g.KF;
+        const double* dl = dbuf_ + (size_t)pl.lo[l] * g.nu;
+        if (dmaok) {
+            const int cpr = g.KF >> 1, cx = g.nx >> 1, cd = (g.nx + g.nu) >> 1;
+            const bool first = l == 0;
+            dma_gen(xd, cnt * cpr, [=](int ch) {
+                const int r = ch / cpr, c = ch - r * cpr;
+                if (c < cx) return (first && r == 0) ? xroot + 2 * c : zp;
+                if (c < cd) return dl + (size_t)r * g.nu + 2 * (c - cx);
+                return zp;
+            });
+        } else {
+            for (int e = tid; e < cnt * g.KF; e += nthr) {
+                const int r = e / g.KF, c = e - r * g.KF;
+                double v = 0.0;
+                if (c < g.nx) v = (l == 0 && r == 0) ? ((const glbd*)xroot)[c] : 0.0;
+                else if (c < g.nx + g.nu) v = ((const glbd*)dl)[(size_t)r * g.nu + c - g.nx];
+                xd[e] = v;
+            }
         }
+        dma(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt);
+        const int cc = pl.hi[l + 1] - pl.lo[l + 1];
+        dma(CHd + 2 * (pl.off[l + 1] - 1), (const double*)(p.cinfo + pl.lo[l + 1]), 2 * cc);
     }
     dma_wait();
     lds_sync();
+    tstamp(p, pl, 2);
     if (done) return;
-    // XD rows = [x (root only; others written by the sweep) | d | 0]
-    {
-        for (int e = tid; e < g.nx; e += nthr) XD[e] = ST[shx + e];
-        int so = rup(g.nx + 2, 2);
-        for (int l = 0; l < L; ++l) {
-            const int cnt = pl.hi[l] - pl.lo[l];
-            const int sh = (int)(((uintptr_t)(dbuf_ + (size_t)pl.lo[l] * g.nu) >> 3) & 1);
-            const int w = g.KF - g.nx;
-            for (int e = tid; e < cnt * w; e += nthr) {
-                const int r = e / w, c = e - r * w;
-                XD[(size_t)(pl.off[l] + r) * g.KF + g.nx + c] = c < g.nu ? ST[so + sh + r * g.nu + c] : 0.0;
-            }
-            so += rup(cnt * g.nu + 2, 2);
-        }
-    }
-    lds_sync();
+    tstamp(p, pl, 3);
     const ldsrec* NL = (const ldsrec*)NLd;
     const ldsrec* CH = (const ldsrec*)CHd;
     typedef typename std::conditional<FL, const ldsd*, const glbd*>::type PF;
@@ -651,12 +675,14 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
             fwd_phase<NXc, NUc, false>(p, tb, inf, pl.lo[l], pl.hi[l], xd_l, z, xd_l, tid, nthr);
         }
         lds_sync();
+        tstamp(p, pl, 4 + l);
     }
+    tflush(p, pl, 4 + L);
 }
 
 // the top of the tree (stages < s, nodes 0..T-1) in one workgroup, backward then forward:
 //   [W | RG | KM | F (if FL) | XQ (T, KP) | QB (boundary, KP) | U (T, NUP) | XD (T, KF) |
-//    P (maxch, PS) | NL (T) | CH (T + nb - 1) | staging: x rows (T, +2), boundary x (+2), u rows (+2)]
+//    P (maxch, PS) | NL (T) | CH (T + nb - 1)]
 template <int NXc, int NUc, bool FL>
 __global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
                                                         const double* qbuf_, const double* x0_, int s, int maxch,
@@ -667,12 +693,13 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl
     const int done = ctl ? ctl->done : 0;
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
+    const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
     const int tid = threadIdx.x, nthr = blockDim.x;
     ldsd* smem = (ldsd*)smem_;
     const bool leaves = s == p.N;
     const int oW = 0, oRG = oW + p.nkind * ts.W1, oKM = oRG + c1 * ts.RG1, oF = oKM + c1 * ts.KM1;
     const int oXQ = oF + (FL ? p1 * ts.F1 : 0), oQB = oXQ + T * g.KP, oU = oQB + nb * g.KP, oXD = oU + T * g.NUP;
-    const int oP = oXD + T * g.KF, oNL = oP + rup(maxch * g.PS, 2), oCH = oNL + 2 * T, oST = oCH + 2 * (T + nb - 1);
+    const int oP = oXD + T * g.KF, oNL = oP + rup(maxch * g.PS, 2), oCH = oNL + 2 * T;
     dma(smem + oW, p.dW, p.nkind * ts.W1);
     dma(smem + oRG, p.dRG, c1 * ts.RG1);
     dma(smem + oKM, p.dKM, c1 * ts.KM1);
@@ -681,24 +708,20 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl
     dma(smem + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1));
     if (tid <= s + 1) pl.sp[tid] = p.stage_ptr[tid];
     glbd* z = dyn_z(bf, zsel, ctl);
-    ldsd* ST = smem + oST;
-    const int so_b = rup(T * g.nx + 2, 2), so_u = so_b + (leaves ? rup(nb * g.nx + 2, 2) : 0);
-    const int shx = dma_u(ST, (const double*)z + p.X0, T * g.nx);
-    int shb = 0;
-    if (leaves) shb = dma_u(ST + so_b, (const double*)z + p.X0 + (size_t)T * g.nx, nb * g.nx);
-    else dma(smem + oQB, qbuf_ + (size_t)T * g.KP, nb * g.KP);
-    const int shu = dma_u(ST + so_u, (const double*)z + p.U0, T * g.nu);
+    rows_in(dmaok, smem + oXQ, g.KP, (const double*)z + p.X0, g.nx, g.nx, T, p.zpage, tid, nthr);
+    if (leaves)
+        rows_in(dmaok, smem + oQB, g.KP, (const double*)z + p.X0 + (size_t)T * g.nx, g.nx, g.nx, nb, p.zpage, tid,
+                nthr);
+    else
+        dma(smem + oQB, qbuf_ + (size_t)T * g.KP, nb * g.KP);
+    rows_in(dmaok, smem + oU, g.NUP, (const double*)z + p.U0, g.nu, g.nu, T, p.zpage, tid, nthr);
+    zero_fill(smem + oXD, T * g.KF, tid, nthr);
+    zero_fill(smem + oP, maxch * g.PS, tid, nthr);
     dma_wait();
     lds_sync();
     if (done) return;
-    tstamp(p, pl, 2 + 3 * s);
-    repack(smem + oXQ, g.KP, ST, shx, g.nx, T, tid, nthr);
-    if (leaves) repack(smem + oQB, g.KP, ST + so_b, shb, g.nx, nb, tid, nthr);
-    repack(smem + oU, g.NUP, ST + so_u, shu, g.nu, T, tid, nthr);
-    zero_fill(smem + oXD, T * g.KF, tid, nthr);
-    zero_fill(smem + oP, maxch * g.PS, tid, nthr);
-    lds_sync();
     tstamp(p, pl, 1);
+    tstamp(p, pl, 2 + 3 * s);
     tstamp(p, pl, 3 + 3 * s);
     typedef typename std::conditional<FL, const ldsd*, const glbd*>::type PF;
     const TabsT<const ldsd*, PF> tb{smem + oW, smem + oRG, smem + oKM,

@@ -75,6 +75,7 @@ struct Dev {
     // RG = [R~^-1; G] and K, per (kind, parent class) pair F = [Abar | B]; padded rows
     const double* dW; const double* dRG; const double* dKM; const double* dF;
     int nkind;             // number of child kinds (rows of W)
+    const double* zpage;   // 16 doubles of zeros (LDS-DMA source of padding)
     const Rec* ninfo;      // [m] {ch_start, nch, class, stage}
     const Rec* cinfo;      // [n] {kind, pair, anc, 0} (node 0: unused)
     const int* stage_ptr;  // [N+2] first node id of each stage (BFS numbering)
@@ -486,7 +487,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
     __shared__ double s_x[kBlock];
     __shared__ double s_red[4][kBlock / 64];
     if (ctl->done) return;
-    const int kk = ctl->k;
+    const int kk = 0;  // buffers arrive rotated for this iteration (enqueue_cp_iteration)
     const double alpha = ctl->alpha;
     const glbd* pz = pick3(bf, kk);                        // p (FULL: p_prev)
     const glbd* zp = pick3(bf, kk + 1);                    // z+ (FULL)
@@ -675,7 +676,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
         if (!leafpart && !(mode & kDualNonleaf)) return;
     }
     const bool prox = WITH_L || (mode & kDualProx);
-    const int kk = WITH_L ? ctl->k : 0;
+    const int kk = 0;  // buffers arrive rotated for this iteration (enqueue_cp_iteration)
     const double alpha = ctl->alpha;
     const glbd* pz = pick3(bf, kk);
     const glbd* zp = pick3(bf, kk + 1);
