@@ -91,6 +91,10 @@ struct raocp_ctx {
     int red_rows = 0;
     size_t lds_top = 0;
     int dyn_block = 1024;
+    // node-block CP kernels (raocp_cp.hip): family / leaf block sizes, grid, LDS bytes
+    int cp_FB = 1, cp_LB = 1, cp_nbF = 0, cp_nbL = 0;
+    size_t lds_cpd = 0, lds_cpp = 0;
+    int cp_rows = 0;             // residual partial rows the CP iteration writes
     const int* ph = nullptr;     // dual placeholder offsets
     int n_ph = 0;
     bool has_x0 = false;
@@ -104,7 +108,7 @@ struct raocp_ctx {
     int alloc(T** p, size_t count) {
         void* v = nullptr;
         if (count == 0) count = 1;
-        hipError_t e = hipMalloc(&v, count * sizeof(T));
+        hipError_t e = hipMalloc(&v, count * sizeof(T) + 64);  // slack: LDS-DMA reads whole 16-B chunks
         if (e != hipSuccess) return fail(RAOCP_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
         allocs.push_back(v);
         *p = (T*)v;
@@ -279,40 +283,48 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl) {
     dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl);
 }
 
+// role: 0 all blocks; 1 nonleaf blocks only; 2 leaf blocks only (op_bench timing)
 struct CpPrimalOp {
     template <int NX, int NU>
-    void run(raocp_ctx* c, bool full) {
+    void run(raocp_ctx* c, bool full, int role) {
         const Launch a = groups(c->nx + c->nu + c->cmax + 1, c->m);
         const Launch l = groups(c->nx, c->n - c->m);
-        const int grid = a.blocks + l.blocks;
+        int grid = a.blocks + l.blocks, blk0 = 0;
+        if (role == 1) grid = a.blocks;
+        if (role == 2) { grid = l.blocks; blk0 = a.blocks; }
         if (full)
             raocp::k_cp_primal<true, NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
-                                                                              c->redpart, a.blocks);
+                                                                              c->redpart, a.blocks, blk0);
         else
             raocp::k_cp_primal<false, NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
-                                                                               c->redpart, a.blocks);
+                                                                               c->redpart, a.blocks, blk0);
     }
 };
-void launch_cp_primal(raocp_ctx* c, bool full) { dispatch(c->nx, c->nu, CpPrimalOp{}, c, full); }
+void launch_cp_primal(raocp_ctx* c, bool full, int role = 0) { dispatch(c->nx, c->nu, CpPrimalOp{}, c, full, role); }
 
+// role: 0 all blocks; 1 child; 2 nonleaf; 3 leaf blocks only (op_bench timing)
 struct CpDualOp {
     template <int NX, int NU>
-    void run(raocp_ctx* c, bool with_l, double* dsolo, int mode) {
+    void run(raocp_ctx* c, bool with_l, double* dsolo, int mode, int role) {
         const Launch a = groups(c->nx + c->nu + 2, c->n - 1);
         const Launch b = groups(2 * c->cmax + 2 + c->nx + c->nu, c->m);
         const Launch l = groups(2 * c->nx + 2, c->n - c->m);
-        const int grid = a.blocks + b.blocks + l.blocks;
+        int grid = a.blocks + b.blocks + l.blocks, blk0 = 0;
+        if (role == 1) grid = a.blocks;
+        if (role == 2) { grid = b.blocks; blk0 = a.blocks; }
+        if (role == 3) { grid = l.blocks; blk0 = a.blocks + b.blocks; }
         if (with_l)
             raocp::k_cp_dual<true, NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
                                                                             nullptr, c->redpart, a.blocks, b.blocks,
-                                                                            raocp::kDualAll);
+                                                                            raocp::kDualAll, blk0);
         else
             raocp::k_cp_dual<false, NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
-                                                                             dsolo, c->redpart, a.blocks, b.blocks, mode);
+                                                                             dsolo, c->redpart, a.blocks, b.blocks, mode,
+                                                                             blk0);
     }
 };
-void launch_cp_dual(raocp_ctx* c, bool with_l, double* dsolo, int mode = raocp::kDualAll) {
-    dispatch(c->nx, c->nu, CpDualOp{}, c, with_l, dsolo, mode);
+void launch_cp_dual(raocp_ctx* c, bool with_l, double* dsolo, int mode = raocp::kDualAll, int role = 0) {
+    dispatch(c->nx, c->nu, CpDualOp{}, c, with_l, dsolo, mode, role);
 }
 
 // One CP iteration for iteration index `it` within a graph batch. Graph batches are a
@@ -323,14 +335,35 @@ raocp::Bufs rotated(raocp_ctx* c, int it) {
     return raocp::Bufs{c->Z[it % 3], c->Z[(it + 1) % 3], c->Z[(it + 2) % 3], c->E[it % 2], c->E[(it + 1) % 2]};
 }
 
+struct CpdOp {
+    template <int NX, int NU>
+    void run(raocp_ctx* c) {
+        auto k = raocp::k_cpd<NX, NU>;
+        allow_lds(k, c->lds_cpd);
+        k<<<c->cp_nbF + c->cp_nbL, kBlock, c->lds_cpd, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2, c->redpart,
+                                                                     c->cp_nbF, c->cp_FB, c->cp_LB);
+    }
+};
+struct CppOp {
+    template <int NX, int NU>
+    void run(raocp_ctx* c) {
+        auto k = raocp::k_cpp<NX, NU>;
+        allow_lds(k, c->lds_cpp);
+        k<<<c->cp_nbF + c->cp_nbL, kBlock, c->lds_cpp, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2, c->redpart,
+                                                                     c->cp_nbF, c->cp_FB, c->cp_LB);
+    }
+};
+void launch_cpd(raocp_ctx* c) { dispatch(c->nx, c->nu, CpdOp{}, c); }
+void launch_cpp(raocp_ctx* c) { dispatch(c->nx, c->nu, CppOp{}, c); }
+
 void enqueue_cp_iteration(raocp_ctx* c, int it) {
     const raocp::Bufs keep = c->bufs;
     c->bufs = rotated(c, it);
     launch_dynamics(c, c->bufs, 1, c->ctl);
-    launch_cp_dual(c, true, nullptr);
-    launch_cp_primal(c, true);
+    launch_cpd(c);
+    launch_cpp(c);
     c->bufs = keep;
-    raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->red_rows);
+    raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
 }
 
 
@@ -526,6 +559,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         (rc = c->upload_vec(&D.SP, to_colmajor(pr->sqrt_pf, pr->n_sp, nx, nx))) ||
         (rc = c->upload(&D.iSQ, pr->i_sq, n)) || (rc = c->upload(&D.iSR, pr->i_sr, n)) ||
         (rc = c->upload(&D.iSP, pr->i_sp, n)) || (rc = c->upload(&D.alpha_r, pr->alpha_r, m)) ||
+        ((D.nSQ = pr->n_sq), (D.nSR = pr->n_sr), (D.nSP = pr->n_sp), false) ||
         (rc = c->upload(&D.cond, pr->cond, n)))
         return bail(rc);
     const int nbn = std::max(1, pr->n_box_nl), nbl = std::max(1, pr->n_box_l);
@@ -649,6 +683,24 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         for (int i = 0; i < m; ++i) ninfo[i] = raocp::Rec{t->ch_start[i], t->nch[i], pr->i_k[i], t->stage[i]};
         cinfo[0] = raocp::Rec{0, 0, -1, 0};
         for (int j = 1; j < n; ++j) cinfo[j] = raocp::Rec{kind[j], pair[j], t->anc[j], 0};
+        // CP child blocks (k_cp_dual): child records and each block's parent range
+        {
+            std::vector<raocp::Rec> crec(n, raocp::Rec{0, 0, 0, 0});
+            for (int j = 1; j < n; ++j) crec[j] = raocp::Rec{t->anc[j], pr->i_sq[j], pr->i_sr[j], 0};
+            const int per = kBlock / (nx + nu + 2);
+            std::vector<raocp::Rec> dblk;
+            for (int j0 = 1; j0 < n; j0 += per) {
+                const int j1 = std::min(n, j0 + per), J = j1 - j0;
+                const int a0 = t->anc[j0], a1 = t->anc[j1 - 1], na = a1 - a0 + 1;
+                auto reg = [](int cnt) { return (cnt + 1) / 2 * 2 + 2; };
+                const int need = 2 * reg(na * nx) + 2 * reg(na * nu) + 2 * reg(J) + reg(J * nx) + reg(J * nu) +
+                                 2 * reg(J) + reg(2 * J);
+                if (need > raocp::kStageDual)
+                    return bail(fail(RAOCP_ERR_ARG, "dual child block staging exceeds the LDS buffer"));
+                dblk.push_back(raocp::Rec{a0, a1, 0, 0});
+            }
+            if ((rc = c->upload_vec(&D.crec, crec)) || (rc = c->upload_vec(&D.dblk, dblk))) return bail(rc);
+        }
         if ((rc = c->upload_vec(&D.ninfo, ninfo)) || (rc = c->upload_vec(&D.cinfo, cinfo)) ||
             (rc = c->upload_vec(&D.stage_ptr, c->stage_ptr)))
             return bail(rc);
@@ -817,6 +869,99 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         }
     }
 
+    // ---- node-block CP kernels (raocp_cp.hip): records, block tables, block sizes
+    {
+        std::vector<int> pos7(m + 1), pos14(n - m + 1);
+        {
+            int o = D.E7;
+            for (int i = 0; i < m; ++i) { pos7[i] = o; o += e7off[i] >= 0 ? nx + nu : 1; }
+            pos7[m] = o;
+            o = D.E14 + m;  // the E14 segment has one placeholder per nonleaf node first
+            for (int l = m; l < n; ++l) { pos14[l - m] = o; o += e14off[l - m] >= 0 ? nx : 1; }
+            pos14[n - m] = o;
+        }
+        std::vector<raocp::Rec> frec(m), lrec(n - m);
+        for (int i = 0; i < m; ++i) frec[i] = raocp::Rec{yrel[i], t->nch[i], t->ch_start[i], e7off[i]};
+        for (int l = m; l < n; ++l) lrec[l - m] = raocp::Rec{pr->i_sp[l], pr->i_box_l[l] >= 0 ? pr->i_box_l[l] : 0, e14off[l - m], 0};
+        D.nBnl = nbn;
+        D.nBl = nbl;
+        auto dbl = [](long cnt) { return (cnt + 1) / 2 * 2 + 2; };
+        auto recs = [](long cnt) { return 2 * cnt + 2; };
+        auto ints = [](long cnt) { return (cnt * 4 + 22) / 8 / 2 * 2 + 4; };
+        const long nQ = (long)pr->n_sq * nx * nx, nR = (long)pr->n_sr * nu * nu, nP = (long)pr->n_sp * nx * nx;
+        const long nBx = (long)nbn * (nx + nu), nBlx = (long)nbl * nx;
+        struct Fam { int cb, ce, y0, y1, e7a, e7b; };
+        auto fam = [&](int i0, int i1) {
+            Fam f;
+            f.cb = t->ch_start[i0];
+            f.ce = t->ch_start[i1 - 1] + t->nch[i1 - 1];
+            f.y0 = yrel[i0];
+            f.y1 = yrel[i1 - 1] + 2 * t->nch[i1 - 1] + 1;
+            f.e7a = pos7[i0];
+            f.e7b = pos7[i1];
+            return f;
+        };
+        auto fam_need = [&](int FB_) {  // max LDS doubles of a family block, k_cpd and k_cpp
+            long a = 0, b = 0;
+            for (int i0 = 0; i0 < m; i0 += FB_) {
+                const int i1 = std::min(m, i0 + FB_), P = i1 - i0;
+                const Fam f = fam(i0, i1);
+                const long C = f.ce - f.cb, Y = f.y1 - f.y0, E7n = f.e7b - f.e7a;
+                const long nd = 2 * dbl(P * nx) + 2 * dbl(P * nu) + 2 * dbl(Y) + 2 * dbl(P) + 2 * dbl(C) + dbl(C) +
+                                dbl(Y) + dbl(P) + dbl(E7n) + dbl(C * nx) + dbl(C * nu) + 2 * dbl(C) + recs(P) +
+                                recs(C) + ints(P) + dbl(nQ) + dbl(nR) + 2 * dbl(nBx);
+                const long npp = 3 * (dbl(Y) + dbl(P) + dbl(C * nx) + dbl(C * nu) + 2 * dbl(C) + dbl(E7n) + 3 * dbl(C)) +
+                                 2 * dbl(P * nx) + 2 * dbl(P * nu) + 2 * dbl(Y) + 2 * dbl(C) + 2 * dbl(C) + dbl(C) +
+                                 dbl(P) + recs(P) + recs(C) + dbl(nQ) + dbl(nR);
+                a = std::max(a, nd);
+                b = std::max(b, npp);
+            }
+            return std::make_pair(a, b);
+        };
+        auto leaf_need = [&](int LB_) {
+            long a = 0, b = 0;
+            for (int l0 = m; l0 < n; l0 += LB_) {
+                const int l1 = std::min(n, l0 + LB_), Lc = l1 - l0;
+                const long E14n = pos14[l1 - m] - pos14[l0 - m];
+                const long nd = 2 * dbl((long)Lc * nx) + 2 * dbl(Lc) + dbl((long)Lc * nx) + 2 * dbl(Lc) + dbl(E14n) +
+                                recs(Lc) + dbl(nP) + 2 * dbl(nBlx);
+                const long npp = 3 * (dbl((long)Lc * nx) + dbl(E14n)) + 2 * dbl((long)Lc * nx) + recs(Lc) + dbl(nP);
+                a = std::max(a, nd);
+                b = std::max(b, npp);
+            }
+            return std::make_pair(a, b);
+        };
+        const long kCpLds = 64 * 1024 / 8;  // doubles: keeps >= 2 blocks per CU
+        int FB = std::max(1, (m + 255) / 256), LB = std::max(1, (n - m + 255) / 256);
+        while (FB > 1 && std::max(fam_need(FB).first, fam_need(FB).second) > kCpLds) FB = FB * 3 / 4;
+        while (LB > 1 && std::max(leaf_need(LB).first, leaf_need(LB).second) > kCpLds) LB = LB * 3 / 4;
+        const auto fn = fam_need(FB), ln = leaf_need(LB);
+        const long need_d = std::max(fn.first, ln.first), need_p = std::max(fn.second, ln.second);
+        if (std::max(need_d, need_p) * 8 > 150 * 1024)
+            return bail(fail(RAOCP_ERR_ARG, "CP node block does not fit LDS (nx, nu or branching too large)"));
+        std::vector<raocp::Rec> tab;
+        int nbF = 0, nbL = 0;
+        for (int i0 = 0; i0 < m; i0 += FB, ++nbF) {
+            const Fam f = fam(i0, std::min(m, i0 + FB));
+            tab.push_back(raocp::Rec{f.cb, f.ce, f.y0, f.y1});
+            tab.push_back(raocp::Rec{f.e7a, f.e7b, 0, 0});
+        }
+        for (int l0 = m; l0 < n; l0 += LB, ++nbL) {
+            const int l1 = std::min(n, l0 + LB);
+            tab.push_back(raocp::Rec{pos14[l0 - m], pos14[l1 - m], 0, 0});
+        }
+        c->cp_FB = FB;
+        c->cp_LB = LB;
+        c->cp_nbF = nbF;
+        c->cp_nbL = nbL;
+        c->lds_cpd = (size_t)need_d * 8;
+        c->lds_cpp = (size_t)need_p * 8;
+        c->cp_rows = nbF + nbL;
+        if ((rc = c->upload_vec(&D.frec, frec)) || (rc = c->upload_vec(&D.lrec, lrec)) ||
+            (rc = c->upload_vec(&D.cpd_tab, tab)))
+            return bail(rc);
+    }
+
     // ---- iterate and work buffers
     for (int b = 0; b < 3; ++b)
         if ((rc = c->alloc(&c->Z[b], c->P))) return bail(rc);
@@ -839,7 +984,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         const int g_dual = groups(nx + nu + 2, n - 1).blocks + groups(2 * cmax + 2 + nx + nu, m).blocks +
                            groups(2 * nx + 2, n - m).blocks;
         const int g_primal = groups(nx + nu + cmax + 1, m).blocks + groups(nx, n - m).blocks;
-        c->red_rows = std::max(g_dual, g_primal);
+        c->red_rows = std::max(std::max(g_dual, g_primal), c->cp_rows);
         if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
         if (hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)) != hipSuccess)
             return bail(fail(RAOCP_ERR_HIP, "memset"));
@@ -951,7 +1096,15 @@ int raocp_project_on_dynamics(raocp_ctx* c) {
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     if (!c->has_x0) return fail(RAOCP_ERR_STATE, "initial state not cached (call cache_initial_state first)");
     const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
-    launch_dynamics(c, solo, 0, nullptr);
+    const char* which = getenv("RAOCP_STAMP_KERNEL");
+    if (which && which[0] == 'p') {  // k_cpp on a valid control block (diagnostics)
+        std::vector<double> x0(c->nx, 0.0);
+        int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
+        if (rc2) return rc2;
+        launch_cpp(c);
+    } else {
+        launch_dynamics(c, solo, 0, nullptr);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return RAOCP_OK;
@@ -1199,7 +1352,15 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
     Dev saved = c->dev;
     c->dev.stamps = st;
     const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
-    launch_dynamics(c, solo, 0, nullptr);
+    const char* which = getenv("RAOCP_STAMP_KERNEL");
+    if (which && which[0] == 'p') {  // k_cpp on a valid control block (diagnostics)
+        std::vector<double> x0(c->nx, 0.0);
+        int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
+        if (rc2) return rc2;
+        launch_cpp(c);
+    } else {
+        launch_dynamics(c, solo, 0, nullptr);
+    }
     c->dev = saved;
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(out, st, cap * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -1218,19 +1379,33 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
     HIPCHK(hipMemcpy(c->tmpD, he.data(), c->D * sizeof(double), hipMemcpyHostToDevice));
     double* outP = c->Z[2];
     double* outD = c->E[1];
-    // warm-up
-    for (int i = 0; i < 3; ++i) {
-        if (op == 0) launch_ell(c, c->tmpP, outD);
-        else launch_ell_t(c, c->tmpD, outP);
+    // ops >= 2 time the CP kernels (or one role of them) on a valid control block
+    if (op >= 2) {
+        if (int rh = ensure_hist(c, (size_t)reps + 16)) return rh;
+        std::vector<double> x0(c->nx, 0.0);
+        int rc = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
+        if (rc) return rc;
+        for (int b = 0; b < 3; ++b) HIPCHK(hipMemcpyAsync(c->Z[b], c->tmpP, c->P * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        for (int b = 0; b < 2; ++b) HIPCHK(hipMemcpyAsync(c->E[b], c->tmpD, c->D * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     }
+    auto run = [&]() {
+        switch (op) {
+            case 0: launch_ell(c, c->tmpP, outD); break;
+            case 1: launch_ell_t(c, c->tmpD, outP); break;
+            case 2: launch_cpd(c); break;
+            case 3: case 4: case 5: launch_cp_dual(c, true, nullptr, raocp::kDualAll, op - 2); break;
+            case 6: launch_cpp(c); break;
+            case 7: case 8: launch_cp_primal(c, true, op - 6); break;
+            case 9: launch_dynamics(c, c->bufs, 1, c->ctl); break;
+            default: raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
+        }
+    };
+    for (int i = 0; i < 3; ++i) run();  // warm-up
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, c->stream));
-    for (int i = 0; i < reps; ++i) {
-        if (op == 0) launch_ell(c, c->tmpP, outD);
-        else launch_ell_t(c, c->tmpD, outP);
-    }
+    for (int i = 0; i < reps; ++i) run();
     HIPCHK(hipEventRecord(e1, c->stream));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0;

@@ -68,6 +68,7 @@ struct Dev {
     // L / L^T weights, column-major: M[k*rows + r] = M_rk
     const double* SQ; const double* SR; const double* SP;
     const int* iSQ; const int* iSR; const int* iSP;
+    int nSQ, nSR, nSP;   // table counts
     const double* alpha_r; const double* cond;
     const double* blo_nl; const double* bhi_nl; const double* blo_l; const double* bhi_l;
     const int* iBnl; const int* iBl;
@@ -76,6 +77,12 @@ struct Dev {
     const double* dW; const double* dRG; const double* dKM; const double* dF;
     int nkind;             // number of child kinds (rows of W)
     const double* zpage;   // 16 doubles of zeros (LDS-DMA source of padding)
+    const Rec* crec;       // [n] {anc, iSQ, iSR, 0} (node 0: unused) — CP child blocks
+    const Rec* frec;       // [m] {yrel, nch, ch_start, e7off} — CP family blocks (raocp_cp.hip)
+    const Rec* lrec;       // [n-m] {iSP, iBl, e14off, 0} — CP leaf blocks
+    const Rec* cpd_tab;    // per CP block: family {cb, ce, y0, y1}, {e7a, e7b}; leaf {e14a, e14b}
+    int nBnl, nBl;         // box table counts
+    const Rec* dblk;       // [child blocks of the CP kernels] {first parent, last parent, 0, 0}
     const Rec* ninfo;      // [m] {ch_start, nch, class, stage}
     const Rec* cinfo;      // [n] {kind, pair, anc, 0} (node 0: unused)
     const int* stage_ptr;  // [N+2] first node id of each stage (BFS numbering)
@@ -104,7 +111,7 @@ __device__ __forceinline__ u64 dbits(double v) { return (u64)__double_as_longlon
 // unrolled); N == 0: runtime length n, plain loop.
 template <int N>
 struct Chunk {
-    static constexpr int C = N <= 24 ? N : 16;
+    static constexpr int C = N <= 8 ? N : 8;
 };
 
 // sum_k m[k*ms] * v[k]
@@ -146,7 +153,7 @@ __device__ __forceinline__ void dot_zp(PM m, int ms, PV z, PV pp, int n, double&
         a = sa;
         b = sb;
     } else {
-        constexpr int C = N <= 16 ? N : 12;
+        constexpr int C = N <= 4 ? N : 4;
         double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
         _Pragma("unroll") for (int k0 = 0; k0 < N; k0 += C) {
             double mm[C], zz[C], qq[C];
@@ -185,7 +192,7 @@ __device__ __forceinline__ void dot_lt3(PM m, int ms, PV dA, PV dP, PV cc, int n
         sW = w;
         sC = c;
     } else {
-        constexpr int C = N <= 12 ? N : 10;
+        constexpr int C = N <= 4 ? N : 4;
         double a0 = 0.0, a1 = 0.0, w0 = 0.0, w1 = 0.0, c0 = 0.0, c1 = 0.0;
         _Pragma("unroll") for (int k0 = 0; k0 < N; k0 += C) {
             double mm[C], va[C], vp[C], vc[C];
@@ -234,12 +241,12 @@ struct GroupIdx {
     bool live;
 };
 
-__device__ __forceinline__ GroupIdx group_index(int G, int begin, int end) {
+__device__ __forceinline__ GroupIdx group_index(int G, int begin, int end, int bid = -1) {
     GroupIdx g;
     g.per = blockDim.x / G;
     g.gl = threadIdx.x / G;
     g.r = threadIdx.x - g.gl * G;
-    g.node = begin + blockIdx.x * g.per + g.gl;
+    g.node = begin + (bid < 0 ? (int)blockIdx.x : bid) * g.per + g.gl;
     g.live = g.gl < g.per && g.node < end;
     return g;
 }
@@ -394,6 +401,20 @@ __global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restric
 
 #include "raocp_dyn.hip"
 
+// ---- LDS-DMA staging for the CP kernels (see raocp_dyn.hip: dma_gen) ----------------
+// copy nbytes from an arbitrarily aligned global address into LDS at dst (16-B aligned):
+// chunks start at the 16-B boundary below src; returns the shift in doubles (0 or 1) at
+// which the data starts in dst. Sources have >= 16 B of slack after their end.
+template <class PT>
+__device__ __forceinline__ int dma_any(ldsd* dst, PT src, int nbytes) {
+    const uintptr_t a = (uintptr_t)src;
+    const int sh = (int)(a & 15);
+    const char* s0 = (const char*)(a - sh);
+    const int chunks = (sh + nbytes + 15) >> 4;
+    dma_gen(dst, chunks, [=](int ch) { return (const double*)(s0 + 16 * ch); });
+    return sh >> 3;
+}
+
 // ==============================================================================
 // AVaR kernel projection of (y_i, tau_children, s_children) (cache.py:290-317),
 // closed form: r_k = alpha y_k - y_{c+k} + y_{2c} - tau_k - s_k,
@@ -483,9 +504,10 @@ struct LtIn {
 template <bool FULL, int NXc, int NUc>
 __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ ctl, Bufs bf,
                                                        const double* __restrict__ xi2,
-                                                       double* __restrict__ part, int nbA) {
+                                                       double* __restrict__ part, int nbA, int blk0) {
     __shared__ double s_x[kBlock];
     __shared__ double s_red[4][kBlock / 64];
+    const int bid = blockIdx.x + blk0;  // blk0: role offset (op_bench times one role alone)
     if (ctl->done) return;
     const int kk = 0;  // buffers arrive rotated for this iteration (enqueue_cp_iteration)
     const double alpha = ctl->alpha;
@@ -508,9 +530,9 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
         const double dl0 = dl1 + w;
         m0 = fmax(m0, fabs(x0v)); m1 = fmax(m1, fabs(x1)); m3 = fmax(m3, fabs(dl0)); m4 = fmax(m4, fabs(dl1));
     };
-    if ((int)blockIdx.x < nbA) {
+    if (bid < nbA) {
         const int G = nx + nu + p.cmax + 1;
-        GroupIdx g = group_index(G, 0, p.m);
+        GroupIdx g = group_index(G, 0, p.m, bid);
         const int i = g.node, r = g.r, base = g.gl * G;
         int c = 0, cs = 0, o7 = -1;
         if (g.live) { c = p.nch[i]; cs = p.ch_start[i]; o7 = p.e7off[i]; }
@@ -605,9 +627,9 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
     } else {
         // leaf l: x = sqrtPf eta11 + eta14
         const int G = nx;
-        const int bid = blockIdx.x - nbA;
+        const int lb = bid - nbA;
         const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-        const int l = p.m + bid * per + gl;
+        const int l = p.m + lb * per + gl;
         if (gl < per && l < p.n) {
             const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
             const int eb = e11(p, l);
@@ -624,7 +646,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
         }
     }
     if (FULL) {
-        double* prow = part + (size_t)blockIdx.x * 6;
+        double* prow = part + (size_t)bid * 6;
         block_max_store(m0, prow + 0, s_red[0]);
         block_max_store(m1, prow + 1, s_red[1]);
         block_max_store(m3, prow + 3, s_red[2]);
@@ -662,16 +684,20 @@ __device__ __forceinline__ double box_apply(double v, double lo, double hi, Ctl*
 // mode (standalone only): bit0 PROX (scale, halves, Moreau output) else projection output Pi(d);
 // bit1 process the nonleaf part (eta1..eta7, SOC per child); bit2 the leaf part (eta11..eta14).
 enum { kDualProx = 1, kDualNonleaf = 2, kDualLeaf = 4, kDualAll = 7 };
+constexpr int kStageDual = 1536;  // doubles of LDS staging per dual block (host checks the need)
+constexpr int kStageMat = 2048;   // doubles of LDS for the L weight tables when they fit
 
 template <bool WITH_L, int NXc, int NUc>
 __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl, Bufs bf,
                                                      double* __restrict__ xi2, double* dsolo,
-                                                     double* __restrict__ part, int nbA, int nbB, int mode) {
+                                                     double* __restrict__ part, int nbA, int nbB, int mode, int blk0) {
+    const int bid = blockIdx.x + blk0;  // blk0: role offset (op_bench times one role alone)
     __shared__ double s_x[kBlock];
     __shared__ double s_red[2][kBlock / 64];
+    __shared__ __attribute__((aligned(16))) double s_stage[kStageDual + kStageMat];
     if (WITH_L && ctl->done) return;
     if (!WITH_L) {
-        const bool leafpart = (int)blockIdx.x >= nbA + nbB;
+        const bool leafpart = bid >= nbA + nbB;
         if (leafpart && !(mode & kDualLeaf)) return;
         if (!leafpart && !(mode & kDualNonleaf)) return;
     }
@@ -696,10 +722,100 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
             m5 = fmax(m5, fabs(ep - de));
         }
     };
-    if ((int)blockIdx.x < nbA) {
+    if (WITH_L && bid < nbA) {
+        // child block j: rows eta3 (nx), eta4 (nu), eta5, eta6 -> one SOC of dim nx+nu+2.
+        // Everything the block reads is staged into LDS by LDS-DMA first (one round trip):
+        // the parents' x, u rows of z+ and p, the children's tau, the four dual ranges and
+        // the child records {anc, iSQ, iSR}.
+        const int G = nx + nu + 2;
+        const int per = blockDim.x / G;
+        const int j0 = 1 + bid * per, j1 = min(p.n, j0 + per), J = j1 - j0;
+        const Rec br = p.dblk[bid];
+        const int a0 = br.x, na = br.y - br.x + 1;
+        ldsd* sb = (ldsd*)s_stage;
+        int o = 0;
+        auto region = [&](int count) { const int r0 = o; o += rup(count, 2) + 2; return r0; };
+        const int oXz = region(na * nx), oXp = region(na * nx), oUz = region(na * nu), oUp = region(na * nu);
+        const int oTz = region(J), oTp = region(J), oD3 = region(J * nx), oD4 = region(J * nu), oD5 = region(J),
+                  oD6 = region(J), oCR = region(2 * J);
+        const int hXz = dma_any(sb + oXz, zp + p.X0 + (size_t)a0 * nx, na * nx * 8);
+        const int hXp = dma_any(sb + oXp, pz + p.X0 + (size_t)a0 * nx, na * nx * 8);
+        const int hUz = dma_any(sb + oUz, zp + p.U0 + (size_t)a0 * nu, na * nu * 8);
+        const int hUp = dma_any(sb + oUp, pz + p.U0 + (size_t)a0 * nu, na * nu * 8);
+        const int hTz = dma_any(sb + oTz, zp + p.T0 + j0, J * 8);
+        const int hTp = dma_any(sb + oTp, pz + p.T0 + j0, J * 8);
+        const int hD3 = dma_any(sb + oD3, d + e3(p, j0), J * nx * 8);
+        const int hD4 = dma_any(sb + oD4, d + e4(p, j0), J * nu * 8);
+        const int hD5 = dma_any(sb + oD5, d + p.E5 + j0, J * 8);
+        const int hD6 = dma_any(sb + oD6, d + p.E6 + j0, J * 8);
+        dma_any(sb + oCR, (const glbd*)(p.crec + j0), J * 16);
+        const int nQ = p.nSQ * nx * nx, nR = p.nSR * nu * nu;
+        const bool mlds = nQ + nR + 4 <= kStageMat;  // weight tables staged too
+        const int oSQ = kStageDual, oSR = oSQ + rup(nQ, 2);
+        if (mlds) {
+            dma_any(sb + oSQ, p.SQ, nQ * 8);
+            dma_any(sb + oSR, p.SR, nR * 8);
+        }
+        dma_wait();
+        lds_sync();
+        const ldsd* Xz = sb + oXz + hXz; const ldsd* Xp = sb + oXp + hXp;
+        const ldsd* Uz = sb + oUz + hUz; const ldsd* Up = sb + oUp + hUp;
+        const ldsd* Tz = sb + oTz + hTz; const ldsd* Tp = sb + oTp + hTp;
+        const ldsd* D3 = sb + oD3 + hD3; const ldsd* D4 = sb + oD4 + hD4;
+        const ldsd* D5 = sb + oD5 + hD5; const ldsd* D6 = sb + oD6 + hD6;
+        const ldsrec* CR = (const ldsrec*)(sb + oCR);
+        const int gl = threadIdx.x / G, r = threadIdx.x - gl * G, base = gl * G;
+        const int jj = gl, j = j0 + gl;
+        const bool live = gl < per && j < j1;
+        double v = 0.0, bb = 0.0, dv = 0.0;
+        int e = -1;
+        if (live) {
+            const Rec cr = CR[jj];
+            const int ai = cr.x - a0;
+            double av = 0.0;
+            if (r < nx) {
+                e = e3(p, j) + r;
+                dv = D3[jj * nx + r];
+                if (mlds) dot_zp<NXc>(sb + oSQ + (size_t)cr.y * nx * nx + r, nx, Xz + ai * nx, Xp + ai * nx, nx, av, bb);
+                else dot_zp<NXc>(p.SQ + (size_t)cr.y * nx * nx + r, nx, Xz + ai * nx, Xp + ai * nx, nx, av, bb);
+            } else if (r < nx + nu) {
+                const int rr = r - nx;
+                e = e4(p, j) + rr;
+                dv = D4[jj * nu + rr];
+                if (mlds) dot_zp<NUc>(sb + oSR + (size_t)cr.z * nu * nu + rr, nu, Uz + ai * nu, Up + ai * nu, nu, av, bb);
+                else dot_zp<NUc>(p.SR + (size_t)cr.z * nu * nu + rr, nu, Uz + ai * nu, Up + ai * nu, nu, av, bb);
+            } else {
+                const bool five = r == nx + nu;
+                e = (five ? p.E5 : p.E6) + j;
+                dv = five ? D5[jj] : D6[jj];
+                const double zt = Tz[jj], pt = Tp[jj];
+                av = 0.5 * (2.0 * zt - pt);
+                bb = 0.5 * (zt - pt);
+            }
+            v = (dv + alpha * av) / alpha;
+            if (r == nx + nu) v += -0.5;
+            if (r == nx + nu + 1) v += 0.5;
+        }
+        // ||f||, f = rows 0..G-2, t = row G-1
+        s_x[threadIdx.x] = (live && r < G - 1) ? v * v : 0.0;
+        if (live && r == G - 1) s_x[threadIdx.x] = v;
+        __syncthreads();
+        if (live) {
+            double ss = 0.0;
+            for (int q = 0; q < G - 1; ++q) ss += s_x[base + q];
+            const double nf = sqrt(ss), t = s_x[base + G - 1];
+            const double pv = soc_apply(v, r == G - 1, nf, t);
+            const double ep = alpha * (v - pv);
+            eo[e] = ep;
+            const double x2 = (dv - ep) / alpha + bb;
+            xi2[e] = x2;
+            m2 = fmax(m2, fabs(x2));
+            m5 = fmax(m5, fabs(ep - dv));
+        }
+    } else if (bid < nbA) {  // standalone prox_g* (no L): direct global reads
         // child block j: rows eta3 (nx), eta4 (nu), eta5, eta6 -> one SOC of dim nx+nu+2
         const int G = nx + nu + 2;
-        GroupIdx g = group_index(G, 1, p.n);
+        GroupIdx g = group_index(G, 1, p.n, bid);
         const int j = g.node, r = g.r, base = g.gl * G;
         double v = 0.0, bb = 0.0;
         int e = -1;
@@ -746,12 +862,12 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
             const double nf = sqrt(ss), t = s_x[base + G - 1];
             finish(e, v, soc_apply(v, r == G - 1, nf, t), bb);
         }
-    } else if ((int)blockIdx.x < nbA + nbB) {
+    } else if (bid < nbA + nbB) {
         // nonleaf i: eta1 (2c+1), eta2, eta7 (nx+nu)
         const int G = 2 * p.cmax + 2 + nx + nu;
-        const int bid = blockIdx.x - nbA;
+        const int lb = bid - nbA;
         const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-        const int i = bid * per + gl;
+        const int i = lb * per + gl;
         if (gl < per && i < p.m) {
             const int c = p.nch[i], cs = p.ch_start[i];
             const int yo = p.yrel[i];
@@ -808,9 +924,9 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
     } else {
         // leaf l: eta11 (nx), eta12, eta13 -> SOC of dim nx+2 ; eta14 (nx) box
         const int G = 2 * nx + 2;
-        const int bid = blockIdx.x - nbA - nbB;
+        const int lb = bid - nbA - nbB;
         const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-        const int l = p.m + bid * per + gl;
+        const int l = p.m + lb * per + gl;
         const bool live = gl < per && l < p.n;
         const int base = gl * G;
         double v = 0.0, bb = 0.0;
@@ -866,11 +982,13 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
         }
     }
     if (WITH_L) {
-        double* prow = part + (size_t)blockIdx.x * 6;
+        double* prow = part + (size_t)bid * 6;
         block_max_store(m2, prow + 2, s_red[0]);
         block_max_store(m5, prow + 5, s_red[1]);
     }
 }
+
+#include "raocp_cp.hip"
 
 // ---- element-wise dual sub-steps of prox_g* (cache.py:329-347, 392-393)
 __global__ void k_div(double* __restrict__ x, double a, int n) {

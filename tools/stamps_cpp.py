@@ -1,0 +1,13 @@
+"""Diagnostics: block 0 timeline of k_cpp (RAOCP_STAMP_KERNEL=p)."""
+import sys, os
+os.environ["RAOCP_STAMP_KERNEL"] = "p"
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raocp-toolbox_amd"))
+import numpy as np
+import raocp.core as core
+from raocp.problems import build_problem, recipe_config
+r = recipe_config(2)
+tree, prob = build_problem(r)
+cache = core.Cache(prob)
+for rep in range(5):
+    st = cache.native.debug_dyn_stamps(64).astype(np.int64)
+print("k_cpp block 0 stamps (ns from start):", [(k, int((st[k] - st[0]) * 10)) for k in range(16) if st[k]])
