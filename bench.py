@@ -10,11 +10,14 @@ the stopping test) on the BASELINE configs[1] tree (i.i.d. binary, N = 12:
 resident in HBM. The loop runs entirely on the device (graph-replayed, on-device
 stopping test); tol = 0 so exactly K iterations run.
 
-Multi-GPU (N > 1, one process per GPU launched by torch.distributed.run): every
-rank solves its own tree instance (an MPC-style batch of independent problems:
-same tree, its own x0), no collective on the data path; the value is the total
-CP iterations/s of the job (weak scaling). Subtree sharding of ONE tree across
-GPUs is SURVEY.md 8(e) and is tracked in DESIGN.md.
+Multi-GPU (N > 1, one process per GPU launched by torch.distributed.run):
+  --mode replicas (default): every rank solves its own tree instance (an MPC-style
+      batch of independent problems: same tree, its own x0), no collective on the data
+      path; value = total CP iterations/s of the job (weak scaling).
+  --mode shard: ONE tree, its subtrees below the replicated top sharded across the
+      ranks; per iteration an RCCL all-gather of the roots' q rows, one
+      of the roots' eta2/xi2 entries and an all-reduce of the residual maxima; value =
+      CP iterations/s of that one tree (strong scaling).
 
 The JSON line also carries
   roofline: the L-sweep kernel (k_ell, operators.py:19-53) timed with HIP events
@@ -79,6 +82,74 @@ def cpu_baseline(recipe, budget_s=12.0):
                       f"elementwise work single-threaded, BLAS up to {blas_threads} threads"}
 
 
+class SocketGroup:
+    """Minimal host rendezvous for --mode shard (rank 0 serves; MASTER_ADDR, MASTER_PORT+1).
+    torch is not imported in shard mode: its wheel bundles a second ROCm runtime, and the
+    RCCL that libraocp_hip.so binds cannot initialise in a process that imported it."""
+
+    def __init__(self, rank, world):
+        import socket
+        import struct
+        self.rank, self.world, self._struct = rank, world, struct
+        addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+        port = int(os.environ.get("MASTER_PORT", "29500")) + 1
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind((addr, port))
+            srv.listen(world)
+            self.peers = [None] * world
+            for _ in range(world - 1):
+                conn, _ = srv.accept()
+                r = struct.unpack("!i", self._recv(conn, 4))[0]
+                self.peers[r] = conn
+            srv.close()
+        else:
+            t0 = time.time()
+            while True:
+                try:
+                    self.conn = socket.create_connection((addr, port), timeout=60)
+                    break
+                except OSError:
+                    if time.time() - t0 > 120:
+                        raise
+                    time.sleep(0.2)
+            self.conn.sendall(struct.pack("!i", rank))
+
+    @staticmethod
+    def _recv(conn, n):
+        buf = b""
+        while len(buf) < n:
+            chunk = conn.recv(n - len(buf))
+            if not chunk:
+                raise ConnectionError("peer closed")
+            buf += chunk
+        return buf
+
+    def bcast(self, data):
+        if self.rank == 0:
+            for c in self.peers[1:]:
+                c.sendall(self._struct.pack("!i", len(data)) + data)
+            return data
+        n = self._struct.unpack("!i", self._recv(self.conn, 4))[0]
+        return self._recv(self.conn, n)
+
+    def max(self, v):
+        st = self._struct
+        if self.rank == 0:
+            m = v
+            for c in self.peers[1:]:
+                m = max(m, st.unpack("!d", self._recv(c, 8))[0])
+            for c in self.peers[1:]:
+                c.sendall(st.pack("!d", m))
+            return m
+        self.conn.sendall(st.pack("!d", v))
+        return st.unpack("!d", self._recv(self.conn, 8))[0]
+
+    def barrier(self):
+        self.max(0.0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -88,6 +159,9 @@ def main():
     ap.add_argument("--op-reps", type=int, default=2000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--mode", choices=["replicas", "shard"], default="replicas",
+                    help="N > 1: independent tree per GPU (replicas, weak scaling) or ONE tree sharded by "
+                         "subtree across the GPUs with RCCL exchanges (shard, strong scaling)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -96,20 +170,30 @@ def main():
     import raocp.core as core
     from raocp.core._native import load_library
     load_library()  # bind /opt/rocm's HIP runtime before torch (gloo only, no torch.cuda) is imported
-    if world > 1:
+    group = None
+    if world > 1 and args.mode == "replicas":
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    elif world > 1:
+        group = SocketGroup(rank, world)
 
     from raocp.problems import build_problem, recipe_config
 
     recipe = recipe_config(args.config, seed=0)
-    if world > 1:  # each rank: its own instance (same tree/dynamics, own initial state)
+    shard = world > 1 and args.mode == "shard"
+    if world > 1 and not shard:  # replicas: each rank its own instance (same tree/dynamics, own initial state)
         recipe["x0"] = np.random.default_rng(1000 + rank).standard_normal(recipe["x0"].size)
     tree, prob = build_problem(recipe)
     cache = core.Cache(prob)
     nat = cache.native
     lam = nat.step_size()
     alpha = 0.999 / lam
+    if shard:
+        # one tree, subtrees sharded across the ranks; RCCL communicator from a uid broadcast
+        from raocp.core._native import comm_unique_id
+        nat.shard(rank, world)
+        uid = group.bcast(comm_unique_id() if rank == 0 else b"")
+        nat.comm_init(uid, rank, world)
 
     # warm-up (W untimed iterations; also captures the CP graph)
     if args.warmup > 0:
@@ -118,6 +202,8 @@ def main():
     def barrier():
         if dist is not None:
             dist.barrier()
+        if group is not None:
+            group.barrier()
 
     # The timed region is bracketed by barrier + device synchronize. The synchronize is
     # hipDeviceSynchronize through libraocp_hip.so: torch's wheel bundles its own
@@ -136,7 +222,9 @@ def main():
         t = torch.tensor([wall], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t[0])
-    its = world * args.steps / wall
+    if group is not None:
+        wall = group.max(wall)
+    its = (1 if shard else world) * args.steps / wall
 
     # L-sweep roofline: k_ell timed with HIP events on the context's stream
     bP, bD = algorithmic_bytes(cache)
@@ -146,20 +234,20 @@ def main():
     gbs_lt = (bP + bD) / (ms_lt * 1e-3) / 1e9
 
     if rank != 0:
-        if dist is not None:
-            dist.barrier()
+        barrier()
         return
     out = {
         "metric": "Chambolle–Pock iterations/sec + L-sweep HBM GB/s, 10k-node tree nₓ=20",
         "value": its, "unit": "it/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": 1e3 * wall / args.steps, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "scaling": "strong" if shard else "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": f"BASELINE configs[1]: i.i.d. binary scenario tree, N=12, {cache.packed.n} nodes, "
                                f"nx={cache.packed.nx}, nu={cache.packed.nu}, AVaR 0.9, boxes +-1 "
                                f"(SURVEY.md 8(d) config {args.config})",
                    "nodes": cache.packed.n, "nx": cache.packed.nx, "nu": cache.packed.nu,
                    "alpha": alpha, "tol": 0.0,
-                   "parallelism": f"replicas{world}: one independent tree instance per GPU" if world > 1 else "1 GPU"},
+                   "parallelism": (f"shard{world}: one tree, subtrees sharded across GPUs, RCCL exchanges" if shard else
+                                   f"replicas{world}: one independent tree instance per GPU") if world > 1 else "1 GPU"},
         "device_ms_per_step": dev_ms / args.steps,
         "roofline": {"bound": "hbm", "kernel": "k_ell (L sweep)", "achieved": gbs_l, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": gbs_l / HBM_PEAK_GBS, "traffic": None,
@@ -170,8 +258,7 @@ def main():
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(recipe, args.cpu_seconds)
     print(json.dumps(out))
-    if dist is not None:
-        dist.barrier()
+    barrier()
 
 
 if __name__ == "__main__":

@@ -160,6 +160,23 @@ int raocp_op_bench(raocp_ctx* ctx, int op, int reps, float* ms_per_launch);
 /* Diagnostics: one dynamics projection with in-kernel s_memrealtime stamps (100 MHz). */
 int raocp_debug_dyn_stamps(raocp_ctx* ctx, unsigned long long* stamps, int cap);
 
+/* Subtree sharding across GPUs (north_star "scenarios shard naturally
+ * by subtree"). Shard `rank` of `nranks` owns a contiguous block of the subtrees rooted
+ * at the boundary stage of the replicated top of the tree; the CP iteration then runs on
+ * the owned nodes only, with three exchanges per iteration (q rows of the roots, the
+ * roots' eta2 / xi2 entries, and an all-reduce of the residual maxima).
+ * raocp_shard_setup restricts this context to its shard; raocp_comm_init binds an RCCL
+ * communicator (one process per GPU; the 128-byte id comes from raocp_comm_unique_id on
+ * one rank); raocp_cp_run / raocp_cp_bench then run the sharded iteration.
+ * raocp_group_cp_run runs the shards of one process (tests: shards sharing a device),
+ * exchanging through device copies. raocp_shard_owned: owned id range per stage. */
+int raocp_shard_setup(raocp_ctx* ctx, int nranks, int rank);
+int raocp_shard_owned(raocp_ctx* ctx, int32_t* stage_lo, int32_t* stage_hi, int cap);
+int raocp_comm_unique_id(unsigned char* id128);
+int raocp_comm_init(raocp_ctx* ctx, const unsigned char* id128, int nranks, int rank);
+int raocp_group_cp_run(raocp_ctx** ctxs, int nranks, const double* x0, int max_iters, double tol, double alpha,
+                       int* status, int* iters, double* err_hist, double* delta_hist);
+
 #ifdef __cplusplus
 }
 #endif

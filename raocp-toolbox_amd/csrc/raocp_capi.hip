@@ -6,6 +6,9 @@
 #include "raocp_kernels.hip"
 #include "../../include/raocp_hip.h"
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -95,6 +98,22 @@ struct raocp_ctx {
     int cp_FB = 1, cp_LB = 1, cp_nbF = 0, cp_nbL = 0;
     size_t lds_cpd = 0, lds_cpp = 0;
     int cp_rows = 0;             // residual partial rows the CP iteration writes
+    // host copies the CP tables are (re)built from (build_cp_blocks)
+    std::vector<int> h_yrel, h_chs, h_nch, h_pos7, h_pos14;
+    // subtree sharding (raocp_shard_setup): R shards own contiguous blocks of the
+    // subtrees rooted at the top's boundary stage sh_S; the top is replicated
+    int sh_R = 1, sh_r = 0, sh_S = 0;
+    std::vector<int> own_lo, own_hi;                // per stage: owned id range
+    std::vector<std::pair<int, int>> tier_own;      // per tier: {first subtree, count}
+    int x_max = 0;                                  // largest slice of stage sh_S
+    int own_first = 0, own_cnt = 0;                 // this shard's slice
+    double *x2_send = nullptr, *x2_recv = nullptr;  // q rows of the roots
+    double *x1_send = nullptr, *x1_recv = nullptr;  // (eta+, xi2) eta2 entries of the roots
+    const int* d_slc = nullptr;                     // [2R] {first id, count} per shard
+    double* red8 = nullptr;                         // this shard's maxima, then all-reduced
+    void* comm = nullptr;                           // ncclComm_t when the transport is RCCL
+    bool eager = false;                             // iterations launched without a graph
+    int n_sq = 0, n_sr = 0, n_sp = 0, nbn = 1, nbl = 1;
     const int* ph = nullptr;     // dual placeholder offsets
     int n_ph = 0;
     bool has_x0 = false;
@@ -219,8 +238,10 @@ struct EllTOp {
 void launch_ell_t(raocp_ctx* c, const double* eta, double* z) { dispatch(c->nx, c->nu, EllTOp{}, c, eta, z); }
 
 struct DynOp {
+    // part: 0 whole projection; 1 the tiers' backward sweeps only; 2 the top and the
+    // tiers' forward sweeps (a shard exchanges the roots' q rows in between)
     template <int NX, int NU>
-    void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl) {
+    void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part) {
         const int s = c->cut;
         const int B = c->dyn_block;
         // diagnostics: each launch stamps into its own 64-slot region
@@ -230,16 +251,26 @@ struct DynOp {
             if (c->dev.stamps) dv.stamps = c->dev.stamps + 64 * slot++;
             return dv;
         };
+        const bool sharded = c->sh_S > 0;
+        auto tier_arg = [&](int k) {  // a shard launches only the subtrees it owns
+            raocp::TierArg ta = c->tiers[k].ta;
+            ta.boff = sharded ? c->tier_own[k].first : 0;
+            return ta;
+        };
+        auto tier_blocks = [&](int k) { return sharded ? c->tier_own[k].second : c->tiers[k].nsub; };
         if (s > 0) {
             // tiers below the top, deepest first (backward), the top, then the tiers (forward)
-            for (int k = (int)c->tiers.size() - 1; k >= 0; --k) {
-                const auto& tp = c->tiers[k];
-                const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1];
-                auto kb = raocp::k_dyn_bottom_back<NX, NU>;
-                allow_lds(kb, tp.lds_b);
-                kb<<<tp.nsub, B, tp.lds_b, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->d, tp.s0, tp.s1, tp.maxch, c0, c1,
-                                                        tp.lv, tp.ta);
-            }
+            if (part != 2)
+                for (int k = (int)c->tiers.size() - 1; k >= 0; --k) {
+                    const auto& tp = c->tiers[k];
+                    const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1];
+                    auto kb = raocp::k_dyn_bottom_back<NX, NU>;
+                    allow_lds(kb, tp.lds_b);
+                    if (tier_blocks(k) > 0)
+                        kb<<<tier_blocks(k), B, tp.lds_b, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->d, tp.s0, tp.s1,
+                                                                      tp.maxch, c0, c1, tp.lv, tier_arg(k));
+                }
+            if (part == 1) return;
             {
                 const int c1 = c->cls_ptr[s], p1 = c->pair_ptr[c1];
                 auto kt = c->f_lds_top ? raocp::k_dyn_top<NX, NU, true> : raocp::k_dyn_top<NX, NU, false>;
@@ -247,15 +278,18 @@ struct DynOp {
                 const int T = c->stage_ptr[s], nb = c->stage_ptr[s + 1] - T;
                 kt<<<1, B, c->lds_top, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->x0, s, c->maxch_top, c1, p1, T, nb);
             }
-            for (const auto& tp : c->tiers) {
+            for (int k = 0; k < (int)c->tiers.size(); ++k) {
+                const auto& tp = c->tiers[k];
                 const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1], p0 = c->pair_ptr[c0], p1 = c->pair_ptr[c1];
                 auto kf = tp.fl ? raocp::k_dyn_bottom_fwd<NX, NU, true> : raocp::k_dyn_bottom_fwd<NX, NU, false>;
                 allow_lds(kf, tp.lds_f);
-                kf<<<tp.nsub, B, tp.lds_f, c->stream>>>(dev_for(), bf, ctl, zsel, c->d, tp.s0, tp.s1, c0, c1, p0, p1, tp.lv,
-                                                        tp.ta);
+                if (tier_blocks(k) > 0)
+                    kf<<<tier_blocks(k), B, tp.lds_f, c->stream>>>(dev_for(), bf, ctl, zsel, c->d, tp.s0, tp.s1, c0, c1,
+                                                                  p0, p1, tp.lv, tier_arg(k));
             }
             return;
         }
+        if (part == 2) return;  // the per-stage path runs whole in part 1 / 0
         // per-stage path on padded global rows
         const int R = c->nu + c->nx;
         raocp::k_dyn_gather<NX, NU><<<std::max(1, std::min(1024, cdiv(c->n * c->KP, kBlock))), kBlock, 0, c->stream>>>(
@@ -279,8 +313,8 @@ struct DynOp {
     }
 };
 // dynamics projection on z = Z[(k + zsel) % 3] (k from ctl when ctl != null, else 0)
-void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl) {
-    dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl);
+void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part = 0) {
+    dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl, part);
 }
 
 // role: 0 all blocks; 1 nonleaf blocks only; 2 leaf blocks only (op_bench timing)
@@ -341,7 +375,7 @@ struct CpdOp {
         auto k = raocp::k_cpd<NX, NU>;
         allow_lds(k, c->lds_cpd);
         k<<<c->cp_nbF + c->cp_nbL, kBlock, c->lds_cpd, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2, c->redpart,
-                                                                     c->cp_nbF, c->cp_FB, c->cp_LB);
+                                                                     c->cp_nbF);
     }
 };
 struct CppOp {
@@ -350,15 +384,106 @@ struct CppOp {
         auto k = raocp::k_cpp<NX, NU>;
         allow_lds(k, c->lds_cpp);
         k<<<c->cp_nbF + c->cp_nbL, kBlock, c->lds_cpp, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2, c->redpart,
-                                                                     c->cp_nbF, c->cp_FB, c->cp_LB);
+                                                                     c->cp_nbF);
     }
 };
 void launch_cpd(raocp_ctx* c) { dispatch(c->nx, c->nu, CpdOp{}, c); }
 void launch_cpp(raocp_ctx* c) { dispatch(c->nx, c->nu, CppOp{}, c); }
 
+// ---- RCCL, loaded on demand (dlopen) so single-GPU users never load it
+struct Rccl {
+    void* h = nullptr;
+    ncclResult_t (*get_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+    const char* (*err)(ncclResult_t) = nullptr;
+};
+Rccl g_rccl;
+int rccl_load() {
+    if (g_rccl.h) return RAOCP_OK;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return fail(RAOCP_ERR_HIP, std::string("cannot load librccl: ") + dlerror());
+    g_rccl.get_id = (decltype(g_rccl.get_id))dlsym(h, "ncclGetUniqueId");
+    g_rccl.init_rank = (decltype(g_rccl.init_rank))dlsym(h, "ncclCommInitRank");
+    g_rccl.all_gather = (decltype(g_rccl.all_gather))dlsym(h, "ncclAllGather");
+    g_rccl.all_reduce = (decltype(g_rccl.all_reduce))dlsym(h, "ncclAllReduce");
+    g_rccl.destroy = (decltype(g_rccl.destroy))dlsym(h, "ncclCommDestroy");
+    g_rccl.err = (decltype(g_rccl.err))dlsym(h, "ncclGetErrorString");
+    if (!g_rccl.get_id || !g_rccl.init_rank || !g_rccl.all_gather || !g_rccl.all_reduce || !g_rccl.destroy)
+        return fail(RAOCP_ERR_HIP, "librccl lacks the collectives used here");
+    g_rccl.h = h;
+    return RAOCP_OK;
+}
+
+// The three exchanges of a sharded iteration:
+//   X2  after the tiers' backward sweeps: q rows of the boundary roots (all-gather);
+//   X1  after k_cpd: eta+ and xi2 of the roots' eta2 (all-gather), read by the
+//       replicated top families of k_cpp;
+//   X3  after k_cpp: the six residual maxima (+ the NaN-in-box flag), all-reduce max.
+// pack/unpack run on every shard; the collective itself is RCCL, or, for shards that
+// share a process (raocp_group_cp_run), host-driven copies between the phases.
+void shard_pack_x2(raocp_ctx* c) {
+    if (c->own_cnt)
+        (void)hipMemcpyAsync(c->x2_send, c->q + (size_t)c->own_first * c->KP, (size_t)c->own_cnt * c->KP * sizeof(double),
+                             hipMemcpyDeviceToDevice, c->stream);
+}
+void shard_unpack_x2(raocp_ctx* c) {
+    const int tot = c->sh_R * c->x_max * c->KP;
+    raocp::k_scatter_rows<<<std::max(1, std::min(256, cdiv(tot, kBlock))), kBlock, 0, c->stream>>>(
+        c->x2_recv, c->q, c->d_slc, c->sh_R, c->x_max, c->KP);
+}
+void shard_pack_x1(raocp_ctx* c) {
+    if (c->own_cnt)
+        raocp::k_pack2<<<std::max(1, cdiv(c->own_cnt, kBlock)), kBlock, 0, c->stream>>>(
+            c->x1_send, c->bufs.e1 + c->dev.E2 + c->own_first, c->XI2 + c->dev.E2 + c->own_first, c->own_cnt);
+}
+void shard_unpack_x1(raocp_ctx* c) {
+    raocp::k_unpack2<<<std::max(1, cdiv(c->sh_R * c->x_max, kBlock)), kBlock, 0, c->stream>>>(
+        c->x1_recv, c->bufs.e1 + c->dev.E2, c->XI2 + c->dev.E2, c->d_slc, c->sh_R, c->x_max);
+}
+int rccl_check(ncclResult_t r, const char* what) {
+    if (r != ncclSuccess)
+        return fail(RAOCP_ERR_HIP, std::string(what) + ": " + (g_rccl.err ? g_rccl.err(r) : "rccl error"));
+    return RAOCP_OK;
+}
+
+// one CP iteration of a shard whose transport is RCCL (graph-capturable)
+int enqueue_shard_iteration(raocp_ctx* c) {
+    ncclComm_t comm = (ncclComm_t)c->comm;
+    int rc;
+    launch_dynamics(c, c->bufs, 1, c->ctl, 1);
+    shard_pack_x2(c);
+    if ((rc = rccl_check(g_rccl.all_gather(c->x2_send, c->x2_recv, (size_t)c->x_max * c->KP, ncclFloat64, comm, c->stream),
+                         "ncclAllGather(q)")))
+        return rc;
+    shard_unpack_x2(c);
+    launch_dynamics(c, c->bufs, 1, c->ctl, 2);
+    launch_cpd(c);
+    shard_pack_x1(c);
+    if ((rc = rccl_check(g_rccl.all_gather(c->x1_send, c->x1_recv, (size_t)2 * c->x_max, ncclFloat64, comm, c->stream),
+                         "ncclAllGather(eta2)")))
+        return rc;
+    shard_unpack_x1(c);
+    launch_cpp(c);
+    raocp::k_cp_reduce<<<1, kBlock, 0, c->stream>>>(c->ctl, c->redpart, c->cp_rows, c->red8);
+    if ((rc = rccl_check(g_rccl.all_reduce(c->red8, c->red8, 8, ncclFloat64, ncclMax, comm, c->stream),
+                         "ncclAllReduce(max)")))
+        return rc;
+    raocp::k_cp_check_red<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->red8);
+    return RAOCP_OK;
+}
+
 void enqueue_cp_iteration(raocp_ctx* c, int it) {
     const raocp::Bufs keep = c->bufs;
     c->bufs = rotated(c, it);
+    if (c->comm) {
+        (void)enqueue_shard_iteration(c);
+        c->bufs = keep;
+        return;
+    }
     launch_dynamics(c, c->bufs, 1, c->ctl);
     launch_cpd(c);
     launch_cpp(c);
@@ -414,6 +539,7 @@ int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double al
 }
 
 int ensure_graph(raocp_ctx* c, int iters) {
+    if (c->eager) return RAOCP_OK;
     if (c->graph && c->graph_iters == iters) return RAOCP_OK;
     if (c->graph) {
         (void)hipGraphExecDestroy(c->graph);
@@ -422,14 +548,132 @@ int ensure_graph(raocp_ctx* c, int iters) {
     hipGraph_t g = nullptr;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     for (int it = 0; it < iters; ++it) enqueue_cp_iteration(c, it);
-    HIPCHK(hipStreamEndCapture(c->stream, &g));
-    hipError_t e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
-    (void)hipGraphDestroy(g);
-    if (e != hipSuccess) return fail(RAOCP_ERR_HIP, std::string("hipGraphInstantiate: ") + hipGetErrorString(e));
+    hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (e == hipSuccess) {
+        e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+    }
+    if (e != hipSuccess) {
+        if (!c->comm) return fail(RAOCP_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+        // an RCCL shard whose collectives cannot be captured: launch iterations eagerly
+        (void)hipGetLastError();
+        c->graph = nullptr;
+        c->eager = true;
+        if (getenv("RAOCP_VERBOSE")) fprintf(stderr, "[raocp] RCCL graph capture failed (%s): eager launches\n", hipGetErrorString(e));
+        return RAOCP_OK;
+    }
     c->graph_iters = iters;
     return RAOCP_OK;
 }
 
+// launch one batch of `iters` CP iterations (the captured graph, or eagerly)
+int launch_batch(raocp_ctx* c, int iters) {
+    if (c->eager) {
+        for (int it = 0; it < iters; ++it) enqueue_cp_iteration(c, it);
+        HIPCHK(hipGetLastError());
+        return RAOCP_OK;
+    }
+    HIPCHK(hipGraphLaunch(c->graph, c->stream));
+    return RAOCP_OK;
+}
+
+
+// ---- node-block CP tables (raocp_cp.hip) for given owned parent / leaf id ranges ----
+struct CpFam { int cb, ce, y0, y1, e7a, e7b; };
+CpFam cp_fam(const raocp_ctx* c, int i0, int i1) {
+    CpFam f;
+    f.cb = c->h_chs[i0];
+    f.ce = c->h_chs[i1 - 1] + c->h_nch[i1 - 1];
+    f.y0 = c->h_yrel[i0];
+    f.y1 = c->h_yrel[i1 - 1] + 2 * c->h_nch[i1 - 1] + 1;
+    f.e7a = c->h_pos7[i0];
+    f.e7b = c->h_pos7[i1];
+    return f;
+}
+
+// LDS doubles of one block (k_cpd, k_cpp), mirroring the Stg regions of raocp_cp.hip
+std::pair<long, long> cp_block_need(const raocp_ctx* c, bool family, int a0, int a1) {
+    const long nx = c->nx, nu = c->nu;
+    auto dbl = [](long cnt) { return (cnt + 1) / 2 * 2 + 2; };
+    auto recs = [](long cnt) { return 2 * cnt + 2; };
+    auto ints = [](long cnt) { return (cnt * 4 + 22) / 8 / 2 * 2 + 4; };
+    const long nQ = (long)c->n_sq * nx * nx, nR = (long)c->n_sr * nu * nu, nP = (long)c->n_sp * nx * nx;
+    const long nBx = (long)c->nbn * (nx + nu), nBlx = (long)c->nbl * nx;
+    if (family) {
+        const long P = a1 - a0;
+        const CpFam f = cp_fam(c, a0, a1);
+        const long C = f.ce - f.cb, Y = f.y1 - f.y0, E7n = f.e7b - f.e7a;
+        const long nd = 2 * dbl(P * nx) + 2 * dbl(P * nu) + 2 * dbl(Y) + 2 * dbl(P) + 2 * dbl(C) + dbl(C) + dbl(Y) +
+                        dbl(P) + dbl(E7n) + dbl(C * nx) + dbl(C * nu) + 2 * dbl(C) + recs(P) + recs(C) + ints(P) +
+                        dbl(nQ) + dbl(nR) + 2 * dbl(nBx);
+        const long npp = 3 * (dbl(Y) + dbl(P) + dbl(C * nx) + dbl(C * nu) + 2 * dbl(C) + dbl(E7n) + 3 * dbl(C)) +
+                         2 * dbl(P * nx) + 2 * dbl(P * nu) + 2 * dbl(Y) + 2 * dbl(C) + 2 * dbl(C) + dbl(C) + dbl(P) +
+                         recs(P) + recs(C) + dbl(nQ) + dbl(nR);
+        return {nd, npp};
+    }
+    const long Lc = a1 - a0;
+    const long E14n = c->h_pos14[a1 - c->m] - c->h_pos14[a0 - c->m];
+    const long nd = 2 * dbl(Lc * nx) + 2 * dbl(Lc) + dbl(Lc * nx) + 2 * dbl(Lc) + dbl(E14n) + recs(Lc) + dbl(nP) +
+                    2 * dbl(nBlx);
+    const long npp = 3 * (dbl(Lc * nx) + dbl(E14n)) + 2 * dbl(Lc * nx) + recs(Lc) + dbl(nP);
+    return {nd, npp};
+}
+
+long cp_need(const raocp_ctx* c, const std::vector<std::pair<int, int>>& pr_, const std::vector<std::pair<int, int>>& lr_,
+             int FB, int LB) {
+    long w = 0;
+    for (const auto& r : pr_)
+        for (int i0 = r.first; i0 < r.second; i0 += FB) {
+            const auto nd = cp_block_need(c, true, i0, std::min(r.second, i0 + FB));
+            w = std::max(w, std::max(nd.first, nd.second));
+        }
+    for (const auto& r : lr_)
+        for (int l0 = r.first; l0 < r.second; l0 += LB) {
+            const auto nd = cp_block_need(c, false, l0, std::min(r.second, l0 + LB));
+            w = std::max(w, std::max(nd.first, nd.second));
+        }
+    return w;
+}
+
+// (re)build the CP block table for the owned parent ranges and leaf ranges
+int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& pranges,
+                    const std::vector<std::pair<int, int>>& lranges) {
+    std::vector<raocp::Rec> fam, leaf;
+    long need_d = 0, need_p = 0;
+    for (const auto& r : pranges)
+        for (int i0 = r.first; i0 < r.second; i0 += c->cp_FB) {
+            const int i1 = std::min(r.second, i0 + c->cp_FB);
+            const CpFam f = cp_fam(c, i0, i1);
+            fam.push_back(raocp::Rec{f.cb, f.ce, f.y0, f.y1});
+            fam.push_back(raocp::Rec{f.e7a, f.e7b, i0, i1});
+            const auto nd = cp_block_need(c, true, i0, i1);
+            need_d = std::max(need_d, nd.first);
+            need_p = std::max(need_p, nd.second);
+        }
+    for (const auto& r : lranges)
+        for (int l0 = r.first; l0 < r.second; l0 += c->cp_LB) {
+            const int l1 = std::min(r.second, l0 + c->cp_LB);
+            leaf.push_back(raocp::Rec{c->h_pos14[l0 - c->m], c->h_pos14[l1 - c->m], l0, l1});
+            const auto nd = cp_block_need(c, false, l0, l1);
+            need_d = std::max(need_d, nd.first);
+            need_p = std::max(need_p, nd.second);
+        }
+    if (std::max(need_d, need_p) * 8 > 150 * 1024)
+        return fail(RAOCP_ERR_ARG, "CP node block does not fit LDS (nx, nu or branching too large)");
+    std::vector<raocp::Rec> tab = fam;
+    tab.insert(tab.end(), leaf.begin(), leaf.end());
+    if (tab.empty()) tab.push_back(raocp::Rec{0, 0, 0, 0});
+    const raocp::Rec* dtab = nullptr;
+    int rc = c->upload_vec(&dtab, tab);
+    if (rc) return rc;
+    c->dev.cpd_tab = dtab;
+    c->cp_nbF = (int)fam.size() / 2;
+    c->cp_nbL = (int)leaf.size();
+    c->lds_cpd = (size_t)need_d * 8;
+    c->lds_cpp = (size_t)need_p * 8;
+    c->cp_rows = c->cp_nbF + c->cp_nbL;
+    return RAOCP_OK;
+}
 }  // namespace
 
 extern "C" {
@@ -871,7 +1115,10 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
 
     // ---- node-block CP kernels (raocp_cp.hip): records, block tables, block sizes
     {
-        std::vector<int> pos7(m + 1), pos14(n - m + 1);
+        std::vector<int>& pos7 = c->h_pos7;
+        std::vector<int>& pos14 = c->h_pos14;
+        pos7.assign(m + 1, 0);
+        pos14.assign(n - m + 1, 0);
         {
             int o = D.E7;
             for (int i = 0; i < m; ++i) { pos7[i] = o; o += e7off[i] >= 0 ? nx + nu : 1; }
@@ -880,86 +1127,29 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             for (int l = m; l < n; ++l) { pos14[l - m] = o; o += e14off[l - m] >= 0 ? nx : 1; }
             pos14[n - m] = o;
         }
+        c->h_yrel = yrel;
+        c->h_chs.assign(t->ch_start, t->ch_start + m);
+        c->h_nch.assign(t->nch, t->nch + m);
+        c->n_sq = pr->n_sq;
+        c->n_sr = pr->n_sr;
+        c->n_sp = pr->n_sp;
+        c->nbn = nbn;
+        c->nbl = nbl;
         std::vector<raocp::Rec> frec(m), lrec(n - m);
         for (int i = 0; i < m; ++i) frec[i] = raocp::Rec{yrel[i], t->nch[i], t->ch_start[i], e7off[i]};
         for (int l = m; l < n; ++l) lrec[l - m] = raocp::Rec{pr->i_sp[l], pr->i_box_l[l] >= 0 ? pr->i_box_l[l] : 0, e14off[l - m], 0};
         D.nBnl = nbn;
         D.nBl = nbl;
-        auto dbl = [](long cnt) { return (cnt + 1) / 2 * 2 + 2; };
-        auto recs = [](long cnt) { return 2 * cnt + 2; };
-        auto ints = [](long cnt) { return (cnt * 4 + 22) / 8 / 2 * 2 + 4; };
-        const long nQ = (long)pr->n_sq * nx * nx, nR = (long)pr->n_sr * nu * nu, nP = (long)pr->n_sp * nx * nx;
-        const long nBx = (long)nbn * (nx + nu), nBlx = (long)nbl * nx;
-        struct Fam { int cb, ce, y0, y1, e7a, e7b; };
-        auto fam = [&](int i0, int i1) {
-            Fam f;
-            f.cb = t->ch_start[i0];
-            f.ce = t->ch_start[i1 - 1] + t->nch[i1 - 1];
-            f.y0 = yrel[i0];
-            f.y1 = yrel[i1 - 1] + 2 * t->nch[i1 - 1] + 1;
-            f.e7a = pos7[i0];
-            f.e7b = pos7[i1];
-            return f;
-        };
-        auto fam_need = [&](int FB_) {  // max LDS doubles of a family block, k_cpd and k_cpp
-            long a = 0, b = 0;
-            for (int i0 = 0; i0 < m; i0 += FB_) {
-                const int i1 = std::min(m, i0 + FB_), P = i1 - i0;
-                const Fam f = fam(i0, i1);
-                const long C = f.ce - f.cb, Y = f.y1 - f.y0, E7n = f.e7b - f.e7a;
-                const long nd = 2 * dbl(P * nx) + 2 * dbl(P * nu) + 2 * dbl(Y) + 2 * dbl(P) + 2 * dbl(C) + dbl(C) +
-                                dbl(Y) + dbl(P) + dbl(E7n) + dbl(C * nx) + dbl(C * nu) + 2 * dbl(C) + recs(P) +
-                                recs(C) + ints(P) + dbl(nQ) + dbl(nR) + 2 * dbl(nBx);
-                const long npp = 3 * (dbl(Y) + dbl(P) + dbl(C * nx) + dbl(C * nu) + 2 * dbl(C) + dbl(E7n) + 3 * dbl(C)) +
-                                 2 * dbl(P * nx) + 2 * dbl(P * nu) + 2 * dbl(Y) + 2 * dbl(C) + 2 * dbl(C) + dbl(C) +
-                                 dbl(P) + recs(P) + recs(C) + dbl(nQ) + dbl(nR);
-                a = std::max(a, nd);
-                b = std::max(b, npp);
-            }
-            return std::make_pair(a, b);
-        };
-        auto leaf_need = [&](int LB_) {
-            long a = 0, b = 0;
-            for (int l0 = m; l0 < n; l0 += LB_) {
-                const int l1 = std::min(n, l0 + LB_), Lc = l1 - l0;
-                const long E14n = pos14[l1 - m] - pos14[l0 - m];
-                const long nd = 2 * dbl((long)Lc * nx) + 2 * dbl(Lc) + dbl((long)Lc * nx) + 2 * dbl(Lc) + dbl(E14n) +
-                                recs(Lc) + dbl(nP) + 2 * dbl(nBlx);
-                const long npp = 3 * (dbl((long)Lc * nx) + dbl(E14n)) + 2 * dbl((long)Lc * nx) + recs(Lc) + dbl(nP);
-                a = std::max(a, nd);
-                b = std::max(b, npp);
-            }
-            return std::make_pair(a, b);
-        };
+        if ((rc = c->upload_vec(&D.frec, frec)) || (rc = c->upload_vec(&D.lrec, lrec))) return bail(rc);
+        // block sizes: about 256 family and 256 leaf blocks, within the LDS budget
         const long kCpLds = 64 * 1024 / 8;  // doubles: keeps >= 2 blocks per CU
         int FB = std::max(1, (m + 255) / 256), LB = std::max(1, (n - m + 255) / 256);
-        while (FB > 1 && std::max(fam_need(FB).first, fam_need(FB).second) > kCpLds) FB = FB * 3 / 4;
-        while (LB > 1 && std::max(leaf_need(LB).first, leaf_need(LB).second) > kCpLds) LB = LB * 3 / 4;
-        const auto fn = fam_need(FB), ln = leaf_need(LB);
-        const long need_d = std::max(fn.first, ln.first), need_p = std::max(fn.second, ln.second);
-        if (std::max(need_d, need_p) * 8 > 150 * 1024)
-            return bail(fail(RAOCP_ERR_ARG, "CP node block does not fit LDS (nx, nu or branching too large)"));
-        std::vector<raocp::Rec> tab;
-        int nbF = 0, nbL = 0;
-        for (int i0 = 0; i0 < m; i0 += FB, ++nbF) {
-            const Fam f = fam(i0, std::min(m, i0 + FB));
-            tab.push_back(raocp::Rec{f.cb, f.ce, f.y0, f.y1});
-            tab.push_back(raocp::Rec{f.e7a, f.e7b, 0, 0});
-        }
-        for (int l0 = m; l0 < n; l0 += LB, ++nbL) {
-            const int l1 = std::min(n, l0 + LB);
-            tab.push_back(raocp::Rec{pos14[l0 - m], pos14[l1 - m], 0, 0});
-        }
+        const std::vector<std::pair<int, int>> allp{{0, m}}, alll{{m, n}};
+        while (FB > 1 && cp_need(c, allp, {}, FB, LB) > kCpLds) FB = FB * 3 / 4;
+        while (LB > 1 && cp_need(c, {}, alll, FB, LB) > kCpLds) LB = LB * 3 / 4;
         c->cp_FB = FB;
         c->cp_LB = LB;
-        c->cp_nbF = nbF;
-        c->cp_nbL = nbL;
-        c->lds_cpd = (size_t)need_d * 8;
-        c->lds_cpp = (size_t)need_p * 8;
-        c->cp_rows = nbF + nbL;
-        if ((rc = c->upload_vec(&D.frec, frec)) || (rc = c->upload_vec(&D.lrec, lrec)) ||
-            (rc = c->upload_vec(&D.cpd_tab, tab)))
-            return bail(rc);
+        if ((rc = build_cp_blocks(c, allp, alll))) return bail(rc);
     }
 
     // ---- iterate and work buffers
@@ -1009,6 +1199,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
 void raocp_ctx_destroy(raocp_ctx* c) {
     if (!c) return;
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->comm && g_rccl.destroy) (void)g_rccl.destroy((ncclComm_t)c->comm);
     if (c->graph) (void)hipGraphExecDestroy(c->graph);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
@@ -1294,7 +1485,7 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     const int batch = kGraphBatch;
     if ((rc = ensure_graph(c, batch))) return rc;
     for (;;) {
-        HIPCHK(hipGraphLaunch(c->graph, c->stream));
+        if ((rc = launch_batch(c, batch))) return rc;
         HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
         if (c->h_ctl->done) break;
@@ -1327,7 +1518,8 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventRecord(e0, c->stream));
-    for (int done = 0; done < iters; done += batch) HIPCHK(hipGraphLaunch(c->graph, c->stream));
+    for (int done = 0; done < iters; done += batch)
+        if ((rc = launch_batch(c, batch))) return rc;
     HIPCHK(hipEventRecord(e1, c->stream));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
@@ -1364,6 +1556,194 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
     c->dev = saved;
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipMemcpy(out, st, cap * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return RAOCP_OK;
+}
+
+
+// ---- subtree sharding ---------------------------------------------------------------
+int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
+    if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(RAOCP_ERR_ARG, "bad shard arguments");
+    // one shard is the unsharded solve, unless forced (tests run the exchange path with R = 1)
+    if (nranks == 1 && !getenv("RAOCP_SHARD_FORCE")) return RAOCP_OK;
+    const int S = c->cut, N = c->N;
+    if (S <= 0 || S >= N || c->tiers.empty())
+        return fail(RAOCP_ERR_ARG, "tree too small to shard (the dynamics plan has no tier below the top)");
+    const int nb = c->stage_ptr[S + 1] - c->stage_ptr[S];
+    if (nb < nranks) return fail(RAOCP_ERR_ARG, "fewer subtrees at the cut stage than shards");
+    c->sh_R = nranks;
+    c->sh_r = rank;
+    c->sh_S = S;
+    std::vector<int> slc(2 * nranks);
+    int xmax = 0;
+    for (int r = 0; r < nranks; ++r) {
+        const int lo = c->stage_ptr[S] + (int)((long)r * nb / nranks), hi = c->stage_ptr[S] + (int)((long)(r + 1) * nb / nranks);
+        slc[2 * r] = lo;
+        slc[2 * r + 1] = hi - lo;
+        xmax = std::max(xmax, hi - lo);
+    }
+    c->x_max = xmax;
+    c->own_first = slc[2 * rank];
+    c->own_cnt = slc[2 * rank + 1];
+    // owned id range per stage: the whole stage above the cut, descendants below
+    c->own_lo.assign(N + 1, 0);
+    c->own_hi.assign(N + 1, 0);
+    for (int t = 0; t < S; ++t) {
+        c->own_lo[t] = c->stage_ptr[t];
+        c->own_hi[t] = c->stage_ptr[t + 1];
+    }
+    int lo = c->own_first, hi = c->own_first + c->own_cnt;
+    for (int t = S; t <= N; ++t) {
+        c->own_lo[t] = lo;
+        c->own_hi[t] = hi;
+        if (t < N && hi > lo) {
+            const int nlo = c->h_chs[lo], nhi = c->h_chs[hi - 1] + c->h_nch[hi - 1];
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    c->tier_own.clear();
+    for (const auto& tp : c->tiers)
+        c->tier_own.push_back({c->own_lo[tp.s0] - c->stage_ptr[tp.s0], c->own_hi[tp.s0] - c->own_lo[tp.s0]});
+    // CP blocks: the replicated top families plus the owned ones, the owned leaves
+    std::vector<std::pair<int, int>> pr_;
+    pr_.push_back({0, c->stage_ptr[S]});
+    for (int t = S; t < N; ++t)
+        if (c->own_hi[t] > c->own_lo[t]) pr_.push_back({c->own_lo[t], c->own_hi[t]});
+    std::vector<std::pair<int, int>> lr_{{c->own_lo[N], c->own_hi[N]}};
+    int rc;
+    if ((rc = build_cp_blocks(c, pr_, lr_))) return rc;
+    if ((rc = c->alloc(&c->x2_send, (size_t)xmax * c->KP)) || (rc = c->alloc(&c->x2_recv, (size_t)nranks * xmax * c->KP)) ||
+        (rc = c->alloc(&c->x1_send, (size_t)2 * xmax)) || (rc = c->alloc(&c->x1_recv, (size_t)2 * nranks * xmax)) ||
+        (rc = c->alloc(&c->red8, 8)) || (rc = c->upload_vec(&c->d_slc, slc)))
+        return rc;
+    if (c->graph) {
+        (void)hipGraphExecDestroy(c->graph);
+        c->graph = nullptr;
+        c->graph_iters = 0;
+    }
+    return RAOCP_OK;
+}
+
+int raocp_shard_owned(raocp_ctx* c, int32_t* lo, int32_t* hi, int cap) {
+    if (!c || !lo || !hi) return fail(RAOCP_ERR_ARG, "null argument");
+    for (int t = 0; t <= c->N && t < cap; ++t) {
+        lo[t] = c->sh_S > 0 ? c->own_lo[t] : c->stage_ptr[t];
+        hi[t] = c->sh_S > 0 ? c->own_hi[t] : c->stage_ptr[t + 1];
+    }
+    return RAOCP_OK;
+}
+
+int raocp_comm_unique_id(unsigned char* out128) {
+    if (!out128) return fail(RAOCP_ERR_ARG, "null argument");
+    int rc;
+    if ((rc = rccl_load())) return rc;
+    ncclUniqueId id;
+    if ((rc = rccl_check(g_rccl.get_id(&id), "ncclGetUniqueId"))) return rc;
+    memcpy(out128, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return RAOCP_OK;
+}
+
+int raocp_comm_init(raocp_ctx* c, const unsigned char* id128, int nranks, int rank) {
+    if (!c || !id128) return fail(RAOCP_ERR_ARG, "null argument");
+    if (c->sh_R != nranks || c->sh_r != rank) return fail(RAOCP_ERR_STATE, "call raocp_shard_setup with the same ranks first");
+    int rc;
+    if ((rc = rccl_load())) return rc;
+    HIPCHK(hipSetDevice(c->device));
+    ncclUniqueId id;
+    memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t comm = nullptr;
+    if ((rc = rccl_check(g_rccl.init_rank(&comm, nranks, id, rank), "ncclCommInitRank"))) return rc;
+    c->comm = comm;
+    if (c->graph) {
+        (void)hipGraphExecDestroy(c->graph);
+        c->graph = nullptr;
+        c->graph_iters = 0;
+    }
+    return RAOCP_OK;
+}
+
+// Shards that share one process and one device (tests, and a host-driven transport):
+// the CP loop runs eagerly, the exchanges are device copies between the shards' buffers.
+int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, double tol, double alpha, int* status,
+                       int* iters, double* err_hist, double* delta_hist) {
+    if (!cs || R < 1 || !x0) return fail(RAOCP_ERR_ARG, "null argument");
+    for (int r = 0; r < R; ++r)
+        if (!cs[r] || cs[r]->sh_R != R || cs[r]->sh_r != r) return fail(RAOCP_ERR_STATE, "shards not set up for this group");
+    int rc;
+    for (int r = 0; r < R; ++r) {
+        raocp_ctx* c = cs[r];
+        HIPCHK(hipSetDevice(c->device));
+        if ((rc = ensure_hist(c, (size_t)max_iters + 1))) return rc;
+        if ((rc = raocp_set_initial_state(c, x0))) return rc;
+        if ((rc = cp_init(c, x0, max_iters, tol, alpha))) return rc;
+    }
+    auto sync_all = [&]() -> int {
+        for (int r = 0; r < R; ++r) HIPCHK(hipStreamSynchronize(cs[r]->stream));
+        return RAOCP_OK;
+    };
+    std::vector<double> red(8 * R);
+    for (int k = 0;; ++k) {
+        for (int r = 0; r < R; ++r) {
+            raocp_ctx* c = cs[r];
+            c->bufs = rotated(c, k % 6);
+            launch_dynamics(c, c->bufs, 1, c->ctl, 1);
+            shard_pack_x2(c);
+        }
+        if ((rc = sync_all())) return rc;
+        for (int r = 0; r < R; ++r) {
+            raocp_ctx* c = cs[r];
+            for (int q = 0; q < R; ++q)
+                HIPCHK(hipMemcpyAsync(c->x2_recv + (size_t)q * c->x_max * c->KP, cs[q]->x2_send,
+                                      (size_t)c->x_max * c->KP * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+            shard_unpack_x2(c);
+            launch_dynamics(c, c->bufs, 1, c->ctl, 2);
+            launch_cpd(c);
+            shard_pack_x1(c);
+        }
+        if ((rc = sync_all())) return rc;
+        for (int r = 0; r < R; ++r) {
+            raocp_ctx* c = cs[r];
+            for (int q = 0; q < R; ++q)
+                HIPCHK(hipMemcpyAsync(c->x1_recv + (size_t)2 * q * c->x_max, cs[q]->x1_send, (size_t)2 * c->x_max * sizeof(double),
+                                      hipMemcpyDeviceToDevice, c->stream));
+            shard_unpack_x1(c);
+            launch_cpp(c);
+            raocp::k_cp_reduce<<<1, kBlock, 0, c->stream>>>(c->ctl, c->redpart, c->cp_rows, c->red8);
+            HIPCHK(hipMemcpyAsync(red.data() + 8 * r, c->red8, 8 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+        }
+        if ((rc = sync_all())) return rc;
+        double g[8];
+        for (int q = 0; q < 8; ++q) {
+            g[q] = red[q];
+            for (int r = 1; r < R; ++r) g[q] = std::max(g[q], red[8 * r + q]);
+        }
+        for (int r = 0; r < R; ++r) {
+            raocp_ctx* c = cs[r];
+            HIPCHK(hipMemcpyAsync(c->red8, g, 8 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+            raocp::k_cp_check_red<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->red8);
+            HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+        }
+        if ((rc = sync_all())) return rc;
+        HIPCHK(hipGetLastError());
+        if (cs[0]->h_ctl->done) break;
+    }
+    for (int r = 0; r < R; ++r) cs[r]->bufs = raocp::Bufs{cs[r]->Z[0], cs[r]->Z[1], cs[r]->Z[2], cs[r]->E[0], cs[r]->E[1]};
+    raocp_ctx* c = cs[0];
+    const int fk = c->h_ctl->final_k;
+    std::vector<double> h((size_t)(fk + 1) * 6);
+    HIPCHK(hipMemcpy(h.data(), c->hist, h.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int k = 0; k <= fk; ++k)
+        for (int q = 0; q < 3; ++q) {
+            if (err_hist) err_hist[k * 3 + q] = h[(size_t)k * 6 + q];
+            if (delta_hist) delta_hist[k * 3 + q] = h[(size_t)k * 6 + 3 + q];
+        }
+    for (int r = 0; r < R; ++r) {
+        cs[r]->cur_z = cs[r]->Z[(fk + 1) % 3];
+        cs[r]->cur_e = cs[r]->E[(fk + 1) % 2];
+    }
+    if (iters) *iters = fk + 1;
+    if (status) *status = fk < max_iters ? 0 : 1;
+    if (c->h_ctl->flags & 1) return fail(RAOCP_ERR_NAN_IN_BOX, "Rectangle constraint - 'nan' value cannot be constrained");
     return RAOCP_OK;
 }
 

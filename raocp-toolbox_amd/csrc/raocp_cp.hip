@@ -46,7 +46,8 @@ struct Stg {
     }
 };
 
-// block tables (host): family block {cb, ce, y0, y1}, {e7a, e7b, 0, 0}; leaf block {e14a, e14b, 0, 0}
+// block tables (host): family block {cb, ce, y0, y1}, {e7a, e7b, i0, i1}; leaf block {e14a, e14b, l0, l1}.
+// The table, not the block index, says which nodes a block owns (a shard launches only its blocks).
 typedef __attribute__((address_space(4))) const Rec crec4;  // scalar (constant) loads
 
 // ==============================================================================
@@ -54,7 +55,7 @@ typedef __attribute__((address_space(4))) const Rec crec4;  // scalar (constant)
 // ==============================================================================
 template <int NXc, int NUc>
 __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bufs bf, double* __restrict__ xi2_,
-                                                double* __restrict__ part, int nbF, int FB, int LB) {
+                                                double* __restrict__ part, int nbF) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ double s_x[kBlock];
     __shared__ double s_red[2][kBlock / 64];
@@ -78,8 +79,8 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
         m5 = fmax(m5, fabs(ep - dv));
     };
     if (bid < nbF) {
-        const int i0 = bid * FB, i1 = min(p.m, i0 + FB), P = i1 - i0;
         const Rec t0 = ((crec4*)p.cpd_tab)[2 * bid], t1 = ((crec4*)p.cpd_tab)[2 * bid + 1];
+        const int i0 = t1.z, i1 = t1.w, P = i1 - i0;
         const int cb = t0.x, ce = t0.y, C = ce - cb, y0 = t0.z, Y = t0.w - t0.z, e7a = t1.x, E7n = t1.y - t1.x;
         // stage
         const ldsd* Xz = st.dbl(zp + p.X0 + (size_t)i0 * nx, P * nx);
@@ -224,8 +225,8 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
     } else {
         // leaves [l0, l1): eta11 (nx), eta12, eta13 -> SOC of dim nx+2 ; eta14 (nx) box
         const int lb = bid - nbF;
-        const int l0 = p.m + lb * LB, l1 = min(p.n, l0 + LB), Lc = l1 - l0;
         const Rec t0 = ((crec4*)p.cpd_tab)[2 * nbF + lb];
+        const int l0 = t0.z, l1 = t0.w, Lc = l1 - l0;
         const int e14a = t0.x, E14n = t0.y - t0.x;
         const ldsd* Xz = st.dbl(zp + p.X0 + (size_t)l0 * nx, Lc * nx);
         const ldsd* Xp = st.dbl(pz + p.X0 + (size_t)l0 * nx, Lc * nx);
@@ -318,7 +319,7 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
 // ==============================================================================
 template <int NXc, int NUc>
 __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bufs bf, const double* __restrict__ xi2_,
-                                                double* __restrict__ part, int nbF, int FB, int LB) {
+                                                double* __restrict__ part, int nbF) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ double s_x[kBlock];
     __shared__ double s_red[4][kBlock / 64];
@@ -344,8 +345,8 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
         m0 = fmax(m0, fabs(x0v)); m1 = fmax(m1, fabs(x1)); m3 = fmax(m3, fabs(dl0)); m4 = fmax(m4, fabs(dl1));
     };
     if (bid < nbF) {
-        const int i0 = bid * FB, i1 = min(p.m, i0 + FB), P = i1 - i0;
         const Rec t0 = ((crec4*)p.cpd_tab)[2 * bid], t1 = ((crec4*)p.cpd_tab)[2 * bid + 1];
+        const int i0 = t1.z, i1 = t1.w, P = i1 - i0;
         const int cb = t0.x, ce = t0.y, C = ce - cb, y0 = t0.z, Y = t0.w - t0.z, e7a = t1.x, E7n = t1.y - t1.x;
         // a family may straddle a stage boundary: leaf and nonleaf children are told apart per child
         // stage: three duals (A = eta+, P = d_prev, X = xi2) over the family's ranges
@@ -530,8 +531,8 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
     } else {
         // leaves: x = sqrtPf eta11 + eta14
         const int lb = bid - nbF;
-        const int l0 = p.m + lb * LB, l1 = min(p.n, l0 + LB), Lc = l1 - l0;
         const Rec t0 = ((crec4*)p.cpd_tab)[2 * nbF + lb];
+        const int l0 = t0.z, l1 = t0.w, Lc = l1 - l0;
         const int e14a = t0.x, E14n = t0.y - t0.x;
         const glbd* dsrc[3] = {dA, dP, xg};
         const ldsd *D11[3], *D14[3];

@@ -486,6 +486,7 @@ __device__ __forceinline__ void rows_in(bool dmaok, ldsd* dst, int w, const doub
 // (every subtree the same shape, ids consecutive), else from the host table
 struct TierArg {
     int regular;
+    int boff;  // first subtree of this launch (a shard launches only the subtrees it owns)
     int lo0[kMaxLevels + 1];
     int cnt[kMaxLevels + 1];
 };
@@ -496,11 +497,11 @@ __device__ __forceinline__ void tier_levels(Prologue& pl, const TierArg& ta, con
     if (ta.regular) {
         int off = 0;
         for (int k = 0; k < l; ++k) off += ta.cnt[k];
-        pl.lo[l] = ta.lo0[l] + blockIdx.x * ta.cnt[l];
+        pl.lo[l] = ta.lo0[l] + (blockIdx.x + ta.boff) * ta.cnt[l];
         pl.hi[l] = pl.lo[l] + ta.cnt[l];
         pl.off[l] = off;
     } else {
-        const Rec r = sub_lv[(size_t)blockIdx.x * (L + 1) + l];
+        const Rec r = sub_lv[(size_t)(blockIdx.x + ta.boff) * (L + 1) + l];
         pl.lo[l] = r.x;
         pl.hi[l] = r.y;
         pl.off[l] = r.z;

@@ -1031,6 +1031,69 @@ __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, con
     }
 }
 
+
+// ---- subtree sharding (raocp_capi.hip, raocp_shard_setup): exchange packing and the
+// residual reduction split around the all-reduce
+// recv holds R slices of maxc rows of w doubles; slice r goes to dst rows lo_r .. lo_r + cnt_r
+__global__ void k_scatter_rows(const double* __restrict__ recv, double* __restrict__ dst, const int* __restrict__ slc,
+                               int R, int maxc, int w) {
+    const int tot = R * maxc * w;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
+        const int r = e / (maxc * w), rem = e - r * maxc * w, i = rem / w, k = rem - i * w;
+        if (i < slc[2 * r + 1]) dst[(size_t)(slc[2 * r] + i) * w + k] = recv[e];
+    }
+}
+// pack (a[i], b[i]) pairs of the owned slice; unpack every rank's pairs into a, b
+__global__ void k_pack2(double* __restrict__ send, const double* __restrict__ a, const double* __restrict__ b, int cnt) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
+        send[2 * i] = a[i];
+        send[2 * i + 1] = b[i];
+    }
+}
+__global__ void k_unpack2(const double* __restrict__ recv, double* __restrict__ a, double* __restrict__ b,
+                          const int* __restrict__ slc, int R, int maxc) {
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < R * maxc; e += gridDim.x * blockDim.x) {
+        const int r = e / maxc, i = e - r * maxc;
+        if (i < slc[2 * r + 1]) {
+            a[slc[2 * r] + i] = recv[2 * e];
+            b[slc[2 * r] + i] = recv[2 * e + 1];
+        }
+    }
+}
+// local part of k_cp_check: this shard's six maxima -> red6 (then all-reduced with max)
+__global__ void __launch_bounds__(kBlock) k_cp_reduce(const Ctl* ctl, const double* __restrict__ part, int rows,
+                                                      double* red6) {
+    __shared__ double s_m[6][kBlock];
+    if (ctl->done) return;
+    double m[6] = {0, 0, 0, 0, 0, 0};
+    for (int r = threadIdx.x; r < rows; r += blockDim.x)
+        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = fmax(m[q], part[(size_t)r * 6 + q]);
+    _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = m[q];
+    __syncthreads();
+    for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w)
+            _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = fmax(s_m[q][threadIdx.x], s_m[q][threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) red6[threadIdx.x] = s_m[threadIdx.x][0];
+    if (threadIdx.x == 6) red6[6] = (ctl->flags & 1) ? 1.0 : 0.0;  // NaN-in-box flag, all-reduced too
+    if (threadIdx.x == 7) red6[7] = 0.0;
+}
+// history + stopping test on the all-reduced maxima (same decision on every shard)
+__global__ void k_cp_check_red(Ctl* ctl, double* hist, const double* __restrict__ red6) {
+    if (threadIdx.x != 0 || ctl->done) return;
+    const int k = ctl->k;
+    for (int q = 0; q < 6; ++q) hist[(size_t)k * 6 + q] = red6[q];
+    const double err = fmax(fmax(red6[0], red6[1]), red6[2]);
+    if (red6[6] > 0.0) ctl->flags |= 1;
+    if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
+        ctl->done = 1;
+        ctl->final_k = k;
+    } else {
+        ctl->k = k + 1;
+    }
+}
+
 // ---- vector helpers for Lanczos (step size)
 __global__ void k_dot_partial(const double* __restrict__ a, const double* __restrict__ b, int n, double* part) {
     __shared__ double s[kBlock / 64];

@@ -10,7 +10,8 @@ import os
 
 import numpy as np
 
-__all__ = ["load_library", "NativeContext", "RaocpError", "LIB_PATH", "EXPORTED_SYMBOLS"]
+__all__ = ["load_library", "NativeContext", "RaocpError", "LIB_PATH", "EXPORTED_SYMBOLS", "comm_unique_id",
+           "group_cp_run"]
 
 LIB_PATH = os.environ.get("RAOCP_HIP_LIB", os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                            "libraocp_hip.so"))
@@ -25,6 +26,7 @@ EXPORTED_SYMBOLS = [
     "raocp_step_size", "raocp_cp_run", "raocp_cp_bench", "raocp_op_bench",
     "raocp_dual_scale", "raocp_dual_add_halves", "raocp_dual_project", "raocp_dual_moreau",
     "raocp_device_synchronize", "raocp_debug_dyn_stamps",
+    "raocp_shard_setup", "raocp_shard_owned", "raocp_comm_unique_id", "raocp_comm_init", "raocp_group_cp_run",
 ]
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -95,6 +97,12 @@ def load_library():
         "raocp_dual_moreau": (c_int, [vp, c_double, vp]),
         "raocp_device_synchronize": (c_int, [c_int]),
         "raocp_debug_dyn_stamps": (c_int, [vp, vp, c_int]),
+        "raocp_shard_setup": (c_int, [vp, c_int, c_int]),
+        "raocp_shard_owned": (c_int, [vp, vp, vp, c_int]),
+        "raocp_comm_unique_id": (c_int, [vp]),
+        "raocp_comm_init": (c_int, [vp, vp, c_int, c_int]),
+        "raocp_group_cp_run": (c_int, [vp, c_int, vp, c_int, c_double, c_double, ctypes.POINTER(c_int),
+                                       ctypes.POINTER(c_int), vp, vp]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)
@@ -121,6 +129,34 @@ def device_synchronize(device=None):
     rc = lib.raocp_device_synchronize(_default_device() if device is None else int(device))
     if rc != 0:
         raise RaocpError(lib.raocp_last_error().decode(errors="replace"))
+
+
+def comm_unique_id():
+    """128-byte RCCL unique id (call on one rank, share with the others)."""
+    lib = load_library()
+    out = np.zeros(128, dtype=np.uint8)
+    rc = lib.raocp_comm_unique_id(_ptr(out))
+    if rc != 0:
+        raise RaocpError(lib.raocp_last_error().decode(errors="replace"))
+    return out.tobytes()
+
+
+def group_cp_run(contexts, x0, max_iters, tol, alpha):
+    """CP loop over the shards of one process (contexts[r].shard(r, R) done), exchanging
+    through device copies. Returns (status, error_cache, delta_error_cache) like cp_run."""
+    lib = load_library()
+    R = len(contexts)
+    arr = (ctypes.c_void_p * R)(*[c._h for c in contexts])
+    x0 = np.ascontiguousarray(np.asarray(x0, dtype=np.float64).reshape(-1))
+    err = np.zeros((max_iters + 1, 3))
+    derr = np.zeros((max_iters + 1, 3))
+    status, iters = ctypes.c_int(), ctypes.c_int()
+    rc = lib.raocp_group_cp_run(ctypes.cast(arr, ctypes.c_void_p), R, _ptr(x0), int(max_iters), float(tol), float(alpha),
+                                ctypes.byref(status), ctypes.byref(iters), _ptr(err), _ptr(derr))
+    if rc != 0:
+        raise RaocpError(lib.raocp_last_error().decode(errors="replace"))
+    k = iters.value
+    return status.value, err[:k].copy(), derr[:k].copy()
 
 
 class NativeContext:
@@ -278,6 +314,25 @@ class NativeContext:
         out = np.zeros(cap, dtype=np.uint64)
         self._check(self._lib.raocp_debug_dyn_stamps(self._h, _ptr(out), int(cap)))
         return out
+
+    # ---- subtree sharding (include/raocp_hip.h)
+    def shard(self, rank, nranks):
+        """Restrict this context to shard `rank` of `nranks` (owned subtrees + replicated top)."""
+        self._check(self._lib.raocp_shard_setup(self._h, int(nranks), int(rank)))
+        self.rank, self.nranks = int(rank), int(nranks)
+
+    def shard_owned(self):
+        """Owned node-id range [lo, hi) per stage 0..N."""
+        N = int(self._packed.N)
+        lo = np.zeros(N + 1, dtype=np.int32)
+        hi = np.zeros(N + 1, dtype=np.int32)
+        self._check(self._lib.raocp_shard_owned(self._h, _ptr(lo), _ptr(hi), N + 1))
+        return lo, hi
+
+    def comm_init(self, uid, rank, nranks):
+        """Bind an RCCL communicator (uid: 128 bytes from comm_unique_id() on one rank)."""
+        buf = np.frombuffer(bytes(uid), dtype=np.uint8).copy()
+        self._check(self._lib.raocp_comm_init(self._h, _ptr(buf), int(nranks), int(rank)))
 
     def op_bench(self, op, reps):
         ms = ctypes.c_float()

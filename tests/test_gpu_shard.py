@@ -1,0 +1,99 @@
+"""GPU: subtree sharding — R shards of one tree, each owning a block of
+the subtrees below the replicated top, exchanging the roots' q rows, the roots' eta2 /
+xi2 entries and the residual maxima each iteration. Here the shards share the one
+device of the test box and exchange through device copies (raocp_group_cp_run); the
+multi-GPU transport is RCCL with the same packing (bench.py --shard).
+
+Parity: the residual histories and the owned parts of the final iterate equal those of
+the unsharded solve (the per-node arithmetic is identical; only max reductions are
+regrouped, which is exact), and match the oracle within the north_star tolerance.
+"""
+import numpy as np
+import pytest
+
+import raocp.core as core
+from raocp.core._native import group_cp_run
+from raocp.problems import build_problem, recipe_config
+
+pytestmark = pytest.mark.gpu
+
+
+def _cache(cfg):
+    r = recipe_config(cfg, seed=0)
+    tree, prob = build_problem(r)
+    return r, tree, prob
+
+
+@pytest.fixture(scope="module")
+def c2():
+    return _cache(2)
+
+
+def _owned_x_slices(ctx):
+    lo, hi = ctx.shard_owned()
+    return [(int(a), int(b)) for a, b in zip(lo, hi)]
+
+
+@pytest.mark.parametrize("R", [2, 4, 8])
+def test_sharded_solve_matches_unsharded(c2, R):
+    r, tree, prob = c2
+    base = core.Cache(prob)
+    lam = base.native.step_size()
+    alpha = 0.999 / lam
+    iters = 40
+    st0, err0, derr0 = base.native.cp_run(r["x0"], iters, 0.0, alpha)
+    z0 = base.get_primal_flat()
+    shards = [core.Cache(prob) for _ in range(R)]
+    for k, s in enumerate(shards):
+        s.native.shard(k, R)
+    st, err, derr = group_cp_run([s.native for s in shards], r["x0"], iters, 0.0, alpha)
+    assert st == st0 and err.shape == err0.shape
+    assert np.array_equal(err, err0)
+    assert np.array_equal(derr, derr0)
+    nx = base.packed.nx
+    covered = np.zeros(tree.num_nodes, dtype=bool)
+    for s in shards:
+        z = s.get_primal_flat()
+        for (a, b) in _owned_x_slices(s.native):
+            if b > a:
+                np.testing.assert_array_equal(z[a * nx:b * nx], z0[a * nx:b * nx])
+                covered[a:b] = True
+    assert covered.all()
+
+
+def test_sharded_stopping_and_status(c2):
+    """The stopping test sees the all-reduced residuals: every shard stops together at
+    the same iteration as the unsharded solve (tolerance reached before max_iters)."""
+    r, tree, prob = c2
+    base = core.Cache(prob)
+    alpha = 0.999 / base.native.step_size()
+    st0, err0, _ = base.native.cp_run(r["x0"], 400, 5e-2, alpha)
+    shards = [core.Cache(prob) for _ in range(2)]
+    for k, s in enumerate(shards):
+        s.native.shard(k, 2)
+    st, err, _ = group_cp_run([s.native for s in shards], r["x0"], 400, 5e-2, alpha)
+    assert (st, err.shape) == (st0, err0.shape)
+    assert np.array_equal(err, err0)
+
+
+def test_shard_setup_rejects_small_trees():
+    r, tree, prob = _cache(1)
+    c = core.Cache(prob)
+    with pytest.raises(Exception):
+        c.native.shard(0, 2)
+
+
+def test_rccl_transport_single_rank():
+    """The RCCL exchange path (all-gathers + all-reduce inside the captured graph) with one
+    forced shard reproduces the unsharded solve bit for bit. Own process: torch must not
+    be loaded next to the RCCL the library binds (bench.py SocketGroup)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("RAOCP_SHARD_FORCE", None)
+    res = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_single_rank.py")], capture_output=True,
+                         text=True, timeout=300, env=env)
+    assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
+    assert "bit-identical" in res.stdout
