@@ -21,8 +21,10 @@ Multi-GPU (N > 1, one process per GPU launched by torch.distributed.run):
 
 The JSON line also carries
   roofline: the L-sweep kernel (k_ell, operators.py:19-53) timed with HIP events
-            on its own stream, algorithmic bytes = 8 (|P| + |D|) per launch
-            (SURVEY.md 8(d)), against the 8 TB/s HBM3E peak;
+            on its own stream over a graph of back-to-back launches, algorithmic bytes =
+            8 (|P| + |D|) per launch, against the 8 TB/s HBM3E peak
+            (cache-resident at this size);
+  l_sweep_hbm: the same kernels at config 4 (104.6 MB per launch, the HBM regime);
   cpu_baseline: the oracle (vectorised NumPy restatement, oracle/raocp_oracle.py)
             timed on this host on a bounded sample of the same workload.
 """
@@ -51,6 +53,21 @@ def algorithmic_bytes(cache):
     l_box = int((pk.i_box_l[m:] >= 0).sum())
     D = (2 * (n - 1) + m) + m + (n - 1) * (nx + nu + 2) + nl_box * (nx + nu) + nl * (nx + 2) + l_box * nx
     return 8 * P, 8 * D
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/<round>/traffic.json, written by tools/traffic.py from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this bench), or None."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")), reverse=True):
+        try:
+            k = json.load(open(f))["kernels"].get(kernel)
+        except Exception:
+            continue
+        if k:
+            return k["traffic_bytes"], os.path.relpath(f, ROOT)
+    return None, None
 
 
 def cpu_baseline(recipe, budget_s=12.0):
@@ -159,6 +176,7 @@ def main():
     ap.add_argument("--op-reps", type=int, default=2000)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-hbm", action="store_true", help="skip the config-4 L / L^T measurement")
     ap.add_argument("--mode", choices=["replicas", "shard"], default="replicas",
                     help="N > 1: independent tree per GPU (replicas, weak scaling) or ONE tree sharded by "
                          "subtree across the GPUs with RCCL exchanges (shard, strong scaling)")
@@ -236,6 +254,21 @@ def main():
     if rank != 0:
         barrier()
         return
+    traffic, traffic_src = pmc_traffic("k_ell")
+    # HBM regime: the same L / L^T kernels at config 4 (88,573 nodes,
+    # nx = 32, nu = 12: 104.6 MB per application, past L2)
+    hbm = None
+    if not args.no_hbm:
+        r4 = recipe_config(4, seed=0)
+        c4 = core.Cache(build_problem(r4)[1])
+        b4P, b4D = algorithmic_bytes(c4)
+        m4l, m4t = c4.native.op_bench(0, 200), c4.native.op_bench(1, 200)
+        hbm = {"config": "SURVEY.md 8(d) config 4: 88,573 nodes, nx=32, nu=12", "bytes_per_launch": b4P + b4D,
+               "L": {"us_per_launch": m4l * 1e3, "achieved": (b4P + b4D) / (m4l * 1e-3) / 1e9,
+                     "frac": (b4P + b4D) / (m4l * 1e-3) / 1e9 / HBM_PEAK_GBS},
+               "L_transpose": {"us_per_launch": m4t * 1e3, "achieved": (b4P + b4D) / (m4t * 1e-3) / 1e9,
+                               "frac": (b4P + b4D) / (m4t * 1e-3) / 1e9 / HBM_PEAK_GBS},
+               "unit": "GB/s", "peak": HBM_PEAK_GBS}
     out = {
         "metric": "Chambolle–Pock iterations/sec + L-sweep HBM GB/s, 10k-node tree nₓ=20",
         "value": its, "unit": "it/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -250,10 +283,11 @@ def main():
                                    f"replicas{world}: one independent tree instance per GPU") if world > 1 else "1 GPU"},
         "device_ms_per_step": dev_ms / args.steps,
         "roofline": {"bound": "hbm", "kernel": "k_ell (L sweep)", "achieved": gbs_l, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": gbs_l / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": gbs_l / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "bytes_per_launch": bP + bD, "us_per_launch": ms_l * 1e3,
                      "note": "working set L2/MALL-resident at this size (SURVEY.md 8(d))"},
         "l_transpose": {"kernel": "k_ell_t", "achieved": gbs_lt, "unit": "GB/s", "us_per_launch": ms_lt * 1e3},
+        "l_sweep_hbm": hbm,
     }
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(recipe, args.cpu_seconds)

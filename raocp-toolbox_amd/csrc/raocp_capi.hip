@@ -96,6 +96,8 @@ struct raocp_ctx {
     int dyn_block = 1024;
     // node-block CP kernels (raocp_cp.hip): family / leaf block sizes, grid, LDS bytes
     int cp_FB = 1, cp_LB = 1, cp_nbF = 0, cp_nbL = 0;
+    int ell_nb = 0, ell_threads = 512;  // L / L^T blocks (raocp_ell.hip), threads, LDS bytes
+    size_t ell_lds = 0, ellt_lds = 0;
     size_t lds_cpd = 0, lds_cpp = 0;
     int cp_rows = 0;             // residual partial rows the CP iteration writes
     // host copies the CP tables are (re)built from (build_cp_blocks)
@@ -217,11 +219,9 @@ void allow_lds(K kernel, size_t bytes) {
 struct EllOp {
     template <int NX, int NU>
     void run(raocp_ctx* c, const double* z, double* eta) {
-        const Launch a = groups(c->nx + c->nu + 2, c->n - 1);
-        const Launch b = groups(2 * c->cmax + 2 + c->nx + c->nu, c->m);
-        const Launch l = groups(2 * c->nx + 2, c->n - c->m);
-        const int grid = a.blocks + b.blocks + l.blocks;
-        if (grid) raocp::k_ell<NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, z, eta, a.blocks, b.blocks);
+        auto k = raocp::k_ell<NX, NU>;
+        allow_lds(k, c->ell_lds);
+        if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ell_lds, c->stream>>>(c->dev, z, eta);
     }
 };
 void launch_ell(raocp_ctx* c, const double* z, double* eta) { dispatch(c->nx, c->nu, EllOp{}, c, z, eta); }
@@ -229,10 +229,9 @@ void launch_ell(raocp_ctx* c, const double* z, double* eta) { dispatch(c->nx, c-
 struct EllTOp {
     template <int NX, int NU>
     void run(raocp_ctx* c, const double* eta, double* z) {
-        const Launch a = groups(c->nx + c->nu + 2 * c->cmax + 2 + c->cmax, c->m);
-        const Launch l = groups(c->nx + 1, c->n - c->m);
-        const int grid = a.blocks + l.blocks;
-        if (grid) raocp::k_ell_t<NX, NU><<<grid, kBlock, 0, c->stream>>>(c->dev, eta, z, a.blocks);
+        auto k = raocp::k_ell_t<NX, NU>;
+        allow_lds(k, c->ellt_lds);
+        if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ellt_lds, c->stream>>>(c->dev, eta, z);
     }
 };
 void launch_ell_t(raocp_ctx* c, const double* eta, double* z) { dispatch(c->nx, c->nu, EllTOp{}, c, eta, z); }
@@ -801,6 +800,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     if ((rc = c->upload_vec(&D.SQ, to_colmajor(pr->sqrt_q, pr->n_sq, nx, nx))) ||
         (rc = c->upload_vec(&D.SR, to_colmajor(pr->sqrt_r, pr->n_sr, nu, nu))) ||
         (rc = c->upload_vec(&D.SP, to_colmajor(pr->sqrt_pf, pr->n_sp, nx, nx))) ||
+        (rc = c->upload(&D.SQr, pr->sqrt_q, (size_t)pr->n_sq * nx * nx)) ||
+        (rc = c->upload(&D.SRr, pr->sqrt_r, (size_t)pr->n_sr * nu * nu)) ||
+        (rc = c->upload(&D.SPr, pr->sqrt_pf, (size_t)pr->n_sp * nx * nx)) ||
         (rc = c->upload(&D.iSQ, pr->i_sq, n)) || (rc = c->upload(&D.iSR, pr->i_sr, n)) ||
         (rc = c->upload(&D.iSP, pr->i_sp, n)) || (rc = c->upload(&D.alpha_r, pr->alpha_r, m)) ||
         ((D.nSQ = pr->n_sq), (D.nSR = pr->n_sr), (D.nSP = pr->n_sp), false) ||
@@ -1152,6 +1154,70 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         if ((rc = build_cp_blocks(c, allp, alll))) return bail(rc);
     }
 
+    // ---- L / L^T node-range blocks (raocp_ell.hip): nonleaf and leaf ranges split evenly
+    // over B blocks; B from the node count (env RAOCP_ELL_NODES overrides the nodes per
+    // block), raised until every block's LDS stage fits 64 KB
+    {
+        // measured (tools/ell_try.sh): 512-thread blocks while the grid is one block per CU,
+        // 256-thread blocks of 64 nodes once there are several per CU
+        int per = 64;
+        if (const char* e = getenv("RAOCP_ELL_NODES")) per = std::max(1, atoi(e));
+        int thr = (n + per - 1) / per > 512 ? 256 : 512;
+        if (const char* e = getenv("RAOCP_ELL_THREADS")) thr = std::min(512, std::max(64, atoi(e) / 64 * 64));
+        c->ell_threads = thr;
+        const int Bmax = std::max(1, std::max(m, n - m));
+        int B = std::max(1, std::min(std::max(256, (n + per - 1) / per), Bmax));
+        std::vector<raocp::Rec> tab;
+        long need_l = 0, need_t = 0;
+        // LDS doubles of one gathered range (raocp_ell.hip Gather): 16-B chunks, +1 for a
+        // range that starts 8 B into its first chunk
+        auto dbl = [](long cnt) { return 2 * ((cnt * 8 + 15) / 16 + 1); };
+        auto rec = [](long cnt) { return 2 * cnt + 2; };
+        for (;;) {
+            tab.assign((size_t)B * raocp::kEllRecs, raocp::Rec{0, 0, 0, 0});
+            need_l = need_t = 0;
+            for (int b = 0; b < B; ++b) {
+                raocp::Rec* T = tab.data() + (size_t)b * raocp::kEllRecs;
+                const int i0 = (int)((int64_t)b * m / B), i1 = (int)((int64_t)(b + 1) * m / B);
+                const int l0 = m + (int)((int64_t)b * (n - m) / B), l1 = m + (int)((int64_t)(b + 1) * (n - m) / B);
+                int c0 = 0, c1 = 0, y0 = 0, y1 = 0;
+                if (i1 > i0) {
+                    c0 = t->ch_start[i0];
+                    c1 = t->ch_start[i1 - 1] + t->nch[i1 - 1];
+                    y0 = yrel[i0];
+                    y1 = yrel[i1 - 1] + 2 * t->nch[i1 - 1] + 1;
+                }
+                const int e7a = c->h_pos7[i0], e7b = c->h_pos7[i1];
+                const int e14a = c->h_pos14[l0 - m], e14b = c->h_pos14[l1 - m];
+                T[0] = raocp::Rec{i0, i1, c0, c1};
+                T[1] = raocp::Rec{l0, l1, y0, y1};
+                T[2] = raocp::Rec{e7a, e7b, e14a, e14b};
+                // the block's table index of each product family, -1 when its nodes differ
+                auto uni = [](const int* idx, int a, int b) {
+                    if (b <= a) return -1;
+                    for (int q = a + 1; q < b; ++q)
+                        if (idx[q] != idx[a]) return -1;
+                    return idx[a];
+                };
+                T[3] = raocp::Rec{uni(pr->i_sq, c0, c1), uni(pr->i_sr, c0, c1), uni(pr->i_sp, l0, l1), 0};
+                const long np = i1 - i0, nc = c1 - c0, nl = l1 - l0, Y = y1 - y0;
+                need_l = std::max(need_l, dbl(np * nx) + dbl(np * nu) + dbl(Y) + dbl(np) + 2 * dbl(nc) + rec(np) +
+                                              rec(nc) + dbl(nl * nx) + dbl(nl) + rec(nl));
+                need_t = std::max(need_t, dbl(nc * nx) + dbl(nc * nu) + dbl(e7b - e7a) + dbl(Y) + dbl(np) +
+                                              3 * dbl(nc) + rec(np) + rec(nc) + dbl(nl * nx) + dbl(e14b - e14a) +
+                                              2 * dbl(nl) + rec(nl) + nc * (nx + nu) + nl * nx);
+            }
+            if (std::max(need_l, need_t) * 8 <= 64 * 1024 || B >= Bmax) break;
+            B = std::min(Bmax, B * 2);
+        }
+        if (std::max(need_l, need_t) * 8 > 64 * 1024)
+            return bail(fail(RAOCP_ERR_ARG, "L block does not fit LDS (node dimension too large)"));
+        if ((rc = c->upload_vec(&D.ell_tab, tab))) return bail(rc);
+        c->ell_nb = B;
+        c->ell_lds = need_l * 8;
+        c->ellt_lds = need_t * 8;
+    }
+
     // ---- iterate and work buffers
     for (int b = 0; b < 3; ++b)
         if ((rc = c->alloc(&c->Z[b], c->P))) return bail(rc);
@@ -1189,6 +1255,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         hipMemset(c->d, 0, (size_t)m * nu * sizeof(double)) != hipSuccess)
         return bail(fail(RAOCP_ERR_HIP, "memset"));
     c->bufs = raocp::Bufs{c->Z[0], c->Z[1], c->Z[2], c->E[0], c->E[1]};
+    // RAOCP_EAGER=1: CP iterations launched one kernel at a time instead of the captured
+    // graph (for rocprofv3 --kernel-trace --stats, which crashes replaying this graph)
+    if (const char* e = getenv("RAOCP_EAGER")) c->eager = atoi(e) != 0;
     c->cur_z = c->Z[0];
     c->cur_e = c->E[0];
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
@@ -1293,6 +1362,10 @@ int raocp_project_on_dynamics(raocp_ctx* c) {
         int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
         if (rc2) return rc2;
         launch_cpp(c);
+    } else if (which && which[0] == 'l') {  // k_ell on the staging buffers
+        launch_ell(c, c->tmpP, c->tmpD);
+    } else if (which && which[0] == 't') {  // k_ell_t
+        launch_ell_t(c, c->tmpD, c->tmpP);
     } else {
         launch_dynamics(c, solo, 0, nullptr);
     }
@@ -1550,6 +1623,10 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
         int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
         if (rc2) return rc2;
         launch_cpp(c);
+    } else if (which && which[0] == 'l') {  // k_ell on the staging buffers
+        launch_ell(c, c->tmpP, c->tmpD);
+    } else if (which && which[0] == 't') {  // k_ell_t
+        launch_ell_t(c, c->tmpD, c->tmpP);
     } else {
         launch_dynamics(c, solo, 0, nullptr);
     }
@@ -1781,17 +1858,32 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
         }
     };
     for (int i = 0; i < 3; ++i) run();  // warm-up
+    // the reps launches replay as one graph (as in the CP loop), so the time is the
+    // kernels' back to back, not the host's launch rate; RAOCP_EAGER=1 launches them
+    // one by one (rocprofv3 kernel tracing)
+    hipGraphExec_t gx = nullptr;
+    if (!c->eager) {
+        hipGraph_t g = nullptr;
+        HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+        for (int i = 0; i < reps; ++i) run();
+        HIPCHK(hipStreamEndCapture(c->stream, &g));
+        HIPCHK(hipGraphInstantiate(&gx, g, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(g);
+        HIPCHK(hipGraphLaunch(gx, c->stream));  // warm-up replay
+    }
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipEventRecord(e0, c->stream));
-    for (int i = 0; i < reps; ++i) run();
+    if (gx) HIPCHK(hipGraphLaunch(gx, c->stream));
+    else for (int i = 0; i < reps; ++i) run();
     HIPCHK(hipEventRecord(e1, c->stream));
     HIPCHK(hipEventSynchronize(e1));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    if (gx) (void)hipGraphExecDestroy(gx);
     HIPCHK(hipGetLastError());
     *ms_per_launch = ms / reps;
     return RAOCP_OK;

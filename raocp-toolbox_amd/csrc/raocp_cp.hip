@@ -19,36 +19,8 @@
 // Arithmetic (operation order included) is that of k_cp_dual / k_cp_primal, which the
 // GPU parity tests pin against the reference.
 
-// sequential LDS regions filled by LDS-DMA; a region may start 8 B into its first chunk
-struct Stg {
-    ldsd* base;
-    int o;  // next free offset (doubles), kept even
-    template <class PT>
-    __device__ __forceinline__ const ldsd* dbl(PT src, int count) {  // count doubles
-        ldsd* dst = base + o;
-        const int sh = dma_any(dst, src, count * 8);
-        o += rup(count, 2) + 2;
-        return dst + sh;
-    }
-    __device__ __forceinline__ const ldsrec* rec(const Rec* src, int count) {  // 16-B records
-        ldsd* dst = base + o;
-        dma_any(dst, (const glbd*)src, count * 16);
-        o += 2 * count + 2;
-        return (const ldsrec*)dst;
-    }
-    __device__ __forceinline__ const __attribute__((address_space(3))) int* ints(const int* src, int count) {
-        ldsd* dst = base + o;
-        const uintptr_t a = (uintptr_t)src;
-        const int shb = (int)(a & 15);
-        dma_any(dst, (const glbd*)(a - shb), count * 4 + shb);
-        o += rup((count * 4 + shb + 7) / 8, 2) + 2;
-        return (const __attribute__((address_space(3))) int*)((__attribute__((address_space(3))) char*)dst + shb);
-    }
-};
-
 // block tables (host): family block {cb, ce, y0, y1}, {e7a, e7b, i0, i1}; leaf block {e14a, e14b, l0, l1}.
 // The table, not the block index, says which nodes a block owns (a shard launches only its blocks).
-typedef __attribute__((address_space(4))) const Rec crec4;  // scalar (constant) loads
 
 // ==============================================================================
 // k_cpd — dual. Roles: blocks [0, nbF) families, [nbF, nbF + nbL) leaves.

@@ -443,13 +443,18 @@ __device__ __forceinline__ void tflush(const Dev& p, const Prologue& pl, int n) 
 // so a prologue costs about one memory round trip. The destination of one wave
 // instruction is linear (base + lane * 16 B), the source is per lane: padded rows are
 // filled chunk by chunk, tail chunks reading a page of zeros (p.zpage).
+// Group g (64 chunks) goes to wave (g + rot) mod nw: callers staging many small regions
+// rotate the start so the issue cost (≈100+ cycles per instruction) is spread over the
+// waves instead of queueing on wave 0. Returns the number of groups.
 template <class SrcF>
-__device__ __forceinline__ void dma_gen(ldsd* dst, int chunks, SrcF src) {
+__device__ __forceinline__ int dma_gen(ldsd* dst, int chunks, SrcF src, int rot = 0) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int c0 = wave * 64; c0 < chunks; c0 += nw * 64) {
+    const int g0 = ((wave - rot) % nw + nw) % nw;
+    for (int c0 = g0 * 64; c0 < chunks; c0 += nw * 64) {
         const int ch = c0 + lane;
         if (ch < chunks) __builtin_amdgcn_global_load_lds((const glbd*)src(ch), dst + 2 * c0, 16, 0, 0);
     }
+    return (chunks + 63) >> 6;
 }
 // contiguous range of n (even) doubles, 16-B aligned at both ends
 __device__ __forceinline__ void dma(ldsd* dst, const double* src, int n) {

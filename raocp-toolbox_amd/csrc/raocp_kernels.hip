@@ -67,6 +67,7 @@ struct Dev {
     const int* e14off;   // [n-m] absolute offset of eta14_l or -1
     // L / L^T weights, column-major: M[k*rows + r] = M_rk
     const double* SQ; const double* SR; const double* SP;
+    const double* SQr; const double* SRr; const double* SPr;  // the same tables row-major
     const int* iSQ; const int* iSR; const int* iSP;
     int nSQ, nSR, nSP;   // table counts
     const double* alpha_r; const double* cond;
@@ -82,6 +83,7 @@ struct Dev {
     const Rec* lrec;       // [n-m] {iSP, iBl, e14off, 0} — CP leaf blocks
     const Rec* cpd_tab;    // per CP block: family {cb, ce, y0, y1}, {e7a, e7b}; leaf {e14a, e14b}
     int nBnl, nBl;         // box table counts
+    const Rec* ell_tab;    // [L / L^T blocks][kEllRecs] node ranges (raocp_ell.hip)
     const Rec* dblk;       // [child blocks of the CP kernels] {first parent, last parent, 0, 0}
     const Rec* ninfo;      // [m] {ch_start, nch, class, stage}
     const Rec* cinfo;      // [n] {kind, pair, anc, 0} (node 0: unused)
@@ -251,154 +253,6 @@ __device__ __forceinline__ GroupIdx group_index(int G, int begin, int end, int b
     return g;
 }
 
-// ==============================================================================
-// L (operators.py:19-53): eta <- L z on active slots only.
-// Three node types in one launch, block-uniform branch on blockIdx.x.
-// ==============================================================================
-template <int NXc, int NUc>
-__global__ void __launch_bounds__(kBlock) k_ell(Dev p, const double* __restrict__ z, double* __restrict__ eta,
-                                                 int nbA, int nbB) {
-    const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
-    if ((int)blockIdx.x < nbA) {
-        // child blocks j = 1..n-1: eta3 = sqrtQ_j x_anc, eta4 = sqrtR_j u_anc, eta5 = eta6 = tau_j/2
-        GroupIdx g = group_index(nx + nu + 2, 1, p.n);
-        if (!g.live) return;
-        const int j = g.node, a = p.anc[j], r = g.r;
-        if (r < nx) {
-            const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
-            const double* x = z + p.X0 + (size_t)a * nx;
-            double acc = 0.0;
-            acc = dotb<NXc>(M + r, nx, x, nx);
-            eta[e3(p, j) + r] = acc;
-        } else if (r < nx + nu) {
-            const int rr = r - nx;
-            const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
-            const double* u = z + p.U0 + (size_t)a * nu;
-            double acc = 0.0;
-            acc = dotb<NUc>(M + rr, nu, u, nu);
-            eta[e4(p, j) + rr] = acc;
-        } else {
-            const double ht = 0.5 * z[p.T0 + j];
-            eta[(r == nx + nu ? p.E5 : p.E6) + j] = ht;
-        }
-        return;
-    }
-    if ((int)blockIdx.x < nbA + nbB) {
-        // nonleaf i: eta1 = y, eta2 = s - b'y, eta7 = [x; u]
-        const int G = 2 * p.cmax + 2 + nx + nu;
-        const int bid = blockIdx.x - nbA;
-        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-        const int i = bid * per + gl;
-        if (gl >= per || i >= p.m) return;
-        const int c = p.nch[i], cs = p.ch_start[i];
-        const double* y = z + p.Y0 + p.yrel[i];
-        if (r < 2 * c + 1) {
-            eta[p.E1 + p.yrel[i] + r] = y[r];
-        } else if (r == 2 * p.cmax + 1) {
-            double by = 0.0;
-            for (int k = 0; k < c; ++k) by = fma(p.cond[cs + k], y[k], by);
-            for (int k = c; k < 2 * c; ++k) by += 0.0 * y[k];
-            by += y[2 * c];
-            eta[p.E2 + i] = z[p.S0 + i] - by;
-        } else if (r >= 2 * p.cmax + 2) {
-            const int rr = r - (2 * p.cmax + 2);
-            const int o7 = p.e7off[i];
-            if (o7 >= 0) eta[o7 + rr] = rr < nx ? z[p.X0 + (size_t)i * nx + rr] : z[p.U0 + (size_t)i * nu + rr - nx];
-        }
-        return;
-    }
-    {
-        // leaf l: eta11 = sqrtPf x, eta12 = eta13 = s/2, eta14 = x
-        const int G = 2 * nx + 2;
-        const int bid = blockIdx.x - nbA - nbB;
-        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-        const int l = p.m + bid * per + gl;
-        if (gl >= per || l >= p.n) return;
-        const double* x = z + p.X0 + (size_t)l * nx;
-        if (r < nx) {
-            const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
-            double acc = 0.0;
-            acc = dotb<NXc>(M + r, nx, x, nx);
-            eta[e11(p, l) + r] = acc;
-        } else if (r < nx + 2) {
-            eta[(r == nx ? p.E12 : p.E13) + l] = 0.5 * z[p.S0 + l];
-        } else {
-            const int o14 = p.e14off[l - p.m];
-            if (o14 >= 0) eta[o14 + r - nx - 2] = x[r - nx - 2];
-        }
-    }
-}
-
-// ==============================================================================
-// L^T (operators.py:55-94): z <- L^T eta on every slot except tau_0.
-// ==============================================================================
-template <int NXc, int NUc>
-__global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restrict__ eta, double* __restrict__ z,
-                                                   int nbA) {
-    const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
-    if ((int)blockIdx.x < nbA) {
-        // nonleaf i: x, u (child sums), y = eta1 - b eta2, s = eta2, tau of the children
-        const int G = nx + nu + (2 * p.cmax + 1) + 1 + p.cmax;
-        GroupIdx g = group_index(G, 0, p.m);
-        if (!g.live) return;
-        const int i = g.node, r = g.r, c = p.nch[i], cs = p.ch_start[i];
-        const int o7 = p.e7off[i];
-        if (r < nx) {
-            double acc = o7 >= 0 ? eta[o7 + r] : 0.0;
-            for (int q = 0; q < c; ++q) {
-                const int j = cs + q;
-                const double* M = p.SQ + (size_t)p.iSQ[j] * nx * nx;
-                const double* e = eta + e3(p, j);
-                acc += dotb<NXc>(M + r, nx, e, nx);
-            }
-            z[p.X0 + (size_t)i * nx + r] = acc;
-        } else if (r < nx + nu) {
-            const int rr = r - nx;
-            double acc = o7 >= 0 ? eta[o7 + nx + rr] : 0.0;
-            for (int q = 0; q < c; ++q) {
-                const int j = cs + q;
-                const double* M = p.SR + (size_t)p.iSR[j] * nu * nu;
-                const double* e = eta + e4(p, j);
-                acc += dotb<NUc>(M + rr, nu, e, nu);
-            }
-            z[p.U0 + (size_t)i * nu + rr] = acc;
-        } else if (r < nx + nu + 2 * p.cmax + 1) {
-            const int k = r - nx - nu;
-            if (k < 2 * c + 1) {
-                const double b = k < c ? p.cond[cs + k] : (k < 2 * c ? 0.0 : 1.0);
-                z[p.Y0 + p.yrel[i] + k] = eta[p.E1 + p.yrel[i] + k] - b * eta[p.E2 + i];
-            }
-        } else if (r == nx + nu + 2 * p.cmax + 1) {
-            z[p.S0 + i] = eta[p.E2 + i];
-        } else {
-            const int q = r - (nx + nu + 2 * p.cmax + 2);
-            if (q < c) {
-                const int j = cs + q;
-                z[p.T0 + j] = 0.5 * (eta[p.E5 + j] + eta[p.E6 + j]);
-            }
-        }
-        return;
-    }
-    {
-        // leaf l: x = sqrtPf eta11 + eta14, s = (eta12 + eta13)/2
-        const int bid = blockIdx.x - nbA;
-        const int G = nx + 1;
-        const int per = blockDim.x / G, gl = threadIdx.x / G, r = threadIdx.x - gl * G;
-        const int l = p.m + bid * per + gl;
-        if (gl >= per || l >= p.n) return;
-        if (r < nx) {
-            const double* M = p.SP + (size_t)p.iSP[l] * nx * nx;
-            const double* e = eta + e11(p, l);
-            double acc = dotb<NXc>(M + r, nx, e, nx);
-            const int o14 = p.e14off[l - p.m];
-            if (o14 >= 0) acc += eta[o14 + r];
-            z[p.X0 + (size_t)l * nx + r] = acc;
-        } else {
-            z[p.S0 + l] = 0.5 * (eta[p.E12 + l] + eta[p.E13 + l]);
-        }
-    }
-}
-
 #include "raocp_dyn.hip"
 
 // ---- LDS-DMA staging for the CP kernels (see raocp_dyn.hip: dma_gen) ----------------
@@ -406,14 +260,17 @@ __global__ void __launch_bounds__(kBlock) k_ell_t(Dev p, const double* __restric
 // chunks start at the 16-B boundary below src; returns the shift in doubles (0 or 1) at
 // which the data starts in dst. Sources have >= 16 B of slack after their end.
 template <class PT>
-__device__ __forceinline__ int dma_any(ldsd* dst, PT src, int nbytes) {
+__device__ __forceinline__ int dma_any(ldsd* dst, PT src, int nbytes, int* rot = nullptr) {
     const uintptr_t a = (uintptr_t)src;
     const int sh = (int)(a & 15);
     const char* s0 = (const char*)(a - sh);
     const int chunks = (sh + nbytes + 15) >> 4;
-    dma_gen(dst, chunks, [=](int ch) { return (const double*)(s0 + 16 * ch); });
+    const int g = dma_gen(dst, chunks, [=](int ch) { return (const double*)(s0 + 16 * ch); }, rot ? *rot : 0);
+    if (rot) *rot += g;
     return sh >> 3;
 }
+
+#include "raocp_ell.hip"
 
 // ==============================================================================
 // AVaR kernel projection of (y_i, tau_children, s_children) (cache.py:290-317),

@@ -28,12 +28,15 @@ __all__ = ["PackedProblem", "pack_problem"]
 
 
 class _Table:
-    """Deduplicating matrix table keyed by object identity."""
+    """Deduplicating matrix table keyed by object identity (and, with by_value, by the
+    matrix's bytes: per-mode cost objects holding equal weights share one entry, so the
+    L / L^T kernels see one table row where the modes' weights coincide)."""
 
-    def __init__(self, shape, strict=True):
+    def __init__(self, shape, strict=True, by_value=False):
         self.shape = shape
         self.mats = []
         self._ids = {}
+        self._vals = {} if by_value else None
         self.strict = strict
         self.mismatch = None
 
@@ -49,8 +52,15 @@ class _Table:
                 # reference's own tests build such problems (tests/test_cache.py:35-54)
                 self.mismatch = self.mismatch or msg
                 arr = np.full(self.shape, np.nan)
-            self._ids[key] = len(self.mats)
-            self.mats.append(np.ascontiguousarray(arr))
+            arr = np.ascontiguousarray(arr)
+            vkey = arr.tobytes() if self._vals is not None and not np.isnan(arr).any() else None
+            if vkey is not None and vkey in self._vals:
+                self._ids[key] = self._vals[vkey]
+            else:
+                self._ids[key] = len(self.mats)
+                self.mats.append(arr)
+                if vkey is not None:
+                    self._vals[vkey] = self._ids[key]
         return self._ids[key]
 
     def array(self):
@@ -97,7 +107,8 @@ def pack_problem(spec):
         rank[ch_start[i]:ch_start[i] + nch[i]] = np.arange(nch[i])
 
     # ---- L / L^T weights
-    t_sq, t_sr, t_sp = _Table((nx, nx), False), _Table((nu, nu), False), _Table((nx, nx), False)
+    t_sq, t_sr, t_sp = (_Table((nx, nx), False, True), _Table((nu, nu), False, True),
+                        _Table((nx, nx), False, True))
     i_sq = np.zeros(n, dtype=np.int64)
     i_sr = np.zeros(n, dtype=np.int64)
     i_sp = np.zeros(n, dtype=np.int64)

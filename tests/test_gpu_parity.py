@@ -226,3 +226,26 @@ def test_c2_cp_trace_vs_oracle(c2):
     assert trace_rel_err(derr, derr_o) <= 1e-8
     assert rel_err(cache.get_primal_flat(), z_o) <= 1e-10
     assert rel_err(cache.get_dual_flat(), e_o) <= 1e-10
+
+
+@pytest.mark.parametrize("cfg", [3, 4, "4-modes"])
+def test_large_operators_vs_oracle(cfg):
+    """L and L^T at the HBM-sized configs (87k / 88k nodes,
+    nx = 20 / 32): many node-range blocks, multi-pass row loops, adjoint identity.
+    "4-modes": config 4 with a different cost per mode, so consecutive children use
+    different weight tables (the register rows reload)."""
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(4 if cfg == "4-modes" else cfg)
+    if cfg == "4-modes":
+        r["Q"] = np.array([(1.0 + k) * q for k, q in enumerate(r["Q"])])
+        r["R"] = np.array([(2.0 + k) * q for k, q in enumerate(r["R"])])
+    tree, prob = build_problem(r)
+    cache, orc = core.Cache(prob), OracleProblem(prob)
+    rng = np.random.default_rng(5)
+    zz = rng.standard_normal(cache.primal_size)
+    ee = rng.standard_normal(cache.dual_size)
+    lz, lte = cache.native.ell(zz), cache.native.ell_t(ee)
+    assert rel_err(lz, orc.ell(zz)) <= 1e-12
+    assert rel_err(lte, orc.ell_t(ee)) <= 1e-12
+    a, b = zz @ lte, lz @ ee
+    assert abs(a - b) <= 1e-10 * max(abs(a), 1.0)
