@@ -254,7 +254,7 @@ def main():
     if rank != 0:
         barrier()
         return
-    traffic, traffic_src = pmc_traffic("k_ell")
+    traffic, traffic_src = pmc_traffic(f"k_ell<{cache.packed.nx}, {cache.packed.nu}>")
     # HBM regime: the same L / L^T kernels at config 4 (88,573 nodes,
     # nx = 32, nu = 12: 104.6 MB per application, past L2)
     hbm = None

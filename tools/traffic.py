@@ -16,8 +16,8 @@ tag = sys.argv[1]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob("gpurun_out/pmc2_*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"].split("(")[0].replace("void raocp::", "").replace("raocp::", "")
-        name = name.split("<")[0]
+        # keep the template arguments: k_ell<20, 8> (config 2) and k_ell<32, 12> (config 4)
+        name = r["Kernel_Name"].split("(")[0].replace("void raocp::", "").replace("raocp::", "").strip()
         if r["Counter_Name"] in ("FETCH_SIZE", "WRITE_SIZE"):
             acc[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
 out = {}
