@@ -151,8 +151,16 @@ int raocp_step_size(raocp_ctx* ctx, double* lambda_max, int max_it, double rtol)
 int raocp_cp_run(raocp_ctx* ctx, const double* x0, int max_iters, double tol, double alpha,
                  int* status, int* iters, double* err_hist, double* delta_hist);
 
+/* Which CP driver raocp_cp_run / raocp_cp_bench use on this context: the persistent
+ * engine (ONE launch per solve; *cut = its cut stage s > 0, *workgroups = 1 + #stage-s
+ * subtrees) or the graph-replayed multi-kernel iteration (*cut = 0). The engine is
+ * opt-in (RAOCP_MEGA=1 at context creation) and planned when the tree fits it;
+ * RAOCP_MEGA_CUT=s forces a cut stage. */
+int raocp_engine_info(raocp_ctx* ctx, int* cut, int* workgroups);
+
 /* Benchmark helpers (bench.py): run exactly `iters` CP iterations (tol = 0) on the
- * device, graph-replayed, without host syncs inside; returns device ms. */
+ * device (one persistent launch, or graph-replayed), without host syncs inside;
+ * returns device ms. */
 int raocp_cp_bench(raocp_ctx* ctx, const double* x0, int iters, double alpha, float* ms);
 /* Time `reps` back-to-back launches of L (op=0) or L^T (op=1) on device-resident
  * vectors with HIP events on the context's stream; returns average ms per launch. */

@@ -120,6 +120,11 @@ struct raocp_ctx {
     int n_ph = 0;
     bool has_x0 = false;
     std::vector<double> h_x0;
+    // persistent CP engine (raocp_mega.hip): one launch per solve when the plan fits
+    bool mega_ok = false;
+    int mega_s = 0, mega_nwg = 0;
+    size_t mega_lds = 0;
+    raocp::MegaArg mega{};
     // captured CP iterations
     hipGraphExec_t graph = nullptr;
     int graph_iters = 0;
@@ -673,6 +678,201 @@ int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& prange
     c->cp_rows = c->cp_nbF + c->cp_nbL;
     return RAOCP_OK;
 }
+
+// ---- persistent CP engine plan (raocp_mega.hip). Cut stage s: workgroup 0 = stages
+// 0..s-1 (level s = the roots, q / x exchanged), workgroup 1+k = the subtree of the k-th
+// stage-s node, levels 0..N-s. The plan exists when every workgroup's LDS fits and the grid
+// (1 + #roots workgroups, one per CU) is co-resident. Opt-in: RAOCP_MEGA=1 (default off);
+// RAOCP_MEGA_CUT=s forces a cut.
+int mega_plan(raocp_ctx* c, const raocp_tree_desc* t) {
+    using raocp::kMegaLev;
+    using raocp::Rec;
+    c->mega_ok = false;
+    // opt-in (RAOCP_MEGA=1): on MI355X the graph-replayed launches are still faster
+    // (persistent engine)
+    const char* on = getenv("RAOCP_MEGA");
+    if (!on || atoi(on) == 0) return RAOCP_OK;
+    const int N = c->N, nx = c->nx, nu = c->nu;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
+        cus = 256;
+    const size_t lds_cap = 160 * 1024 - 4096;  // dynamic LDS budget (static arrays + slack)
+    int forced = -1;
+    if (const char* e = getenv("RAOCP_MEGA_CUT")) forced = atoi(e);
+    struct Cand {
+        int s = 0;
+        long cost = 0;
+        size_t lds = 0;
+        int maxch = 0, stage_cap = 0;
+        std::vector<Rec> lv;
+        std::vector<int> wl;
+    };
+    Cand best;
+    bool have = false;
+    for (int s = 1; s < N; ++s) {
+        if (forced > 0 && s != forced) continue;
+        const int nsub = c->stage_ptr[s + 1] - c->stage_ptr[s];
+        const int L = N - s;
+        if (s > kMegaLev || L > kMegaLev || nsub + 1 > cus) continue;
+        Cand cd;
+        cd.s = s;
+        const int nwg = 1 + nsub;
+        cd.lv.assign((size_t)nwg * (kMegaLev + 1), Rec{0, 0, 0, 0});
+        cd.wl.assign(nwg, 0);
+        int maxch = 1;
+        long top_nodes = c->stage_ptr[s], sub_max = 0;
+        // top
+        for (int l = 0; l <= s; ++l) {
+            const int lo = c->stage_ptr[l], hi = c->stage_ptr[l + 1];
+            cd.lv[l] = Rec{lo, hi, lo, 0};
+            if (l >= 1) maxch = std::max(maxch, hi - lo);
+        }
+        cd.wl[0] = s;
+        // subtrees
+        bool ok = true;
+        for (int k = 0; k < nsub && ok; ++k) {
+            Rec* lv = cd.lv.data() + (size_t)(1 + k) * (kMegaLev + 1);
+            int lo = c->stage_ptr[s] + k, hi = lo + 1, off = 0;
+            for (int l = 0; l <= L; ++l) {
+                lv[l] = Rec{lo, hi, off, 0};
+                off += hi - lo;
+                if (l >= 1) maxch = std::max(maxch, hi - lo);
+                if (l < L) {
+                    if (lo >= c->m) { ok = false; break; }
+                    const int nlo = t->ch_start[lo], nhi = t->ch_start[hi - 1] + t->nch[hi - 1];
+                    lo = nlo;
+                    hi = nhi;
+                }
+            }
+            sub_max = std::max<long>(sub_max, off);
+            cd.wl[1 + k] = L;
+        }
+        if (!ok) continue;
+        cd.maxch = maxch;
+        // LDS: the stage gets what the largest workgroup leaves of the budget; it must hold
+        // the operands of any single level of the dual / primal phases (raocp_mega.hip)
+        const int ncl_top = c->cls_ptr[s], ncl_sub = c->cls_ptr[N] - c->cls_ptr[s];
+        const int nmat = c->n_sq * nx * nx + c->n_sr * nu * nu + c->n_sp * nx * nx;
+        const long budget = (long)(lds_cap / 8);
+        long cap = budget, need1 = 0;
+        auto rup2 = [](long v) { return (v + 1) / 2 * 2; };
+        auto level_need = [&](const Rec* lv, int nl, bool leaves) {
+            long mx = 0;
+            for (int l = 0; l < nl; ++l) {
+                const long cp = lv[l].y - lv[l].x, cc = lv[l + 1].y - lv[l + 1].x;
+                mx = std::max(mx, 2 * (rup2(cp * nx) + 4) + 2 * (rup2(cp * nu) + 4) + 2 * cp + 4 + 2 * cc + 4);
+                mx = std::max(mx, 3 * (rup2(cc * nx) + 4) + 3 * (rup2(cc * nu) + 4) + 2 * cc + 4 + 2 * cp + 4);
+            }
+            if (leaves) {
+                const long cl = lv[nl].y - lv[nl].x;
+                mx = std::max(mx, 3 * (rup2(cl * nx) + 4) + 2 * cl + 4);
+            }
+            return mx;
+        };
+        {
+            const raocp::MegaLds m0(c->nkind, ncl_top, c->stage_ptr[s + 1], c->stage_ptr[s], maxch, nsub, nx, nu, nmat, 0);
+            cap = std::min<long>(cap, budget - (m0.total - (m0.oNL - m0.oXQ)));
+            need1 = std::max(need1, level_need(cd.lv.data(), s, false));
+        }
+        for (int k = 0; k < nsub; ++k) {
+            const Rec* lv = cd.lv.data() + (size_t)(1 + k) * (kMegaLev + 1);
+            const int nall = lv[L].z + (lv[L].y - lv[L].x), nnl = lv[L].z;
+            const raocp::MegaLds m1(c->nkind, ncl_sub, nall, nnl, maxch, 0, nx, nu, nmat, 0);
+            cap = std::min<long>(cap, budget - (m1.total - (m1.oNL - m1.oXQ)));
+            need1 = std::max(need1, level_need(lv, L, true));
+        }
+        if (cap < need1) continue;
+        cap = cap / 2 * 2;
+        size_t lds = 0;
+        {
+            const raocp::MegaLds m0(c->nkind, ncl_top, c->stage_ptr[s + 1], c->stage_ptr[s], maxch, nsub, nx, nu, nmat,
+                                    (int)cap);
+            lds = std::max(lds, (size_t)m0.total * 8);
+        }
+        for (int k = 0; k < nsub; ++k) {
+            const Rec* lv = cd.lv.data() + (size_t)(1 + k) * (kMegaLev + 1);
+            const int nall = lv[L].z + (lv[L].y - lv[L].x), nnl = lv[L].z;
+            const raocp::MegaLds m1(c->nkind, ncl_sub, nall, nnl, maxch, 0, nx, nu, nmat, (int)cap);
+            lds = std::max(lds, (size_t)m1.total * 8);
+        }
+        if (lds > lds_cap) continue;
+        cd.lds = lds;
+        cd.stage_cap = (int)cap;
+        // cost: the larger of the top and a subtree (phases) plus the levels of both sweeps
+        cd.cost = std::max(top_nodes, sub_max) * 4 + 2 * (long)N;
+        if (!have || cd.cost < best.cost || (cd.cost == best.cost && cd.s > best.s)) {
+            best = cd;
+            have = true;
+        }
+    }
+    if (!have) return RAOCP_OK;
+    const int s = best.s, nsub = c->stage_ptr[s + 1] - c->stage_ptr[s], nwg = 1 + nsub;
+    raocp::MegaArg& a = c->mega;
+    int rc;
+    const raocp::Rec* dlv = nullptr;
+    const int* dwl = nullptr;
+    if ((rc = c->upload_vec(&dlv, best.lv)) || (rc = c->upload_vec(&dwl, best.wl))) return rc;
+    a.lv = dlv;
+    a.wl = dwl;
+    a.ups = c->KP + 16;
+    a.dns = raocp::rup(nx + 1, 2) + 2;
+    if ((rc = c->alloc(&a.up, (size_t)nsub * a.ups)) || (rc = c->alloc(&a.dn, (size_t)nsub * a.dns)) ||
+        (rc = c->alloc(&a.up_flag, (size_t)nsub + 64)) || (rc = c->alloc(&a.dn_flag, 64)))
+        return rc;
+    a.s = s;
+    a.nsub = nsub;
+    a.c_top1 = c->cls_ptr[s];
+    a.c_sub0 = c->cls_ptr[s];
+    a.c_sub1 = c->cls_ptr[N];
+    a.maxch = best.maxch;
+    a.stage_cap = best.stage_cap;
+    a.timeout = 20000000;  // 0.2 s per wait (100 MHz)
+    c->mega_s = s;
+    c->mega_nwg = nwg;
+    c->mega_lds = best.lds;
+    c->mega_ok = true;
+    if (getenv("RAOCP_VERBOSE"))
+        fprintf(stderr, "[raocp] persistent CP engine: cut stage %d, %d workgroups, LDS %zu B\n", s, nwg, best.lds);
+    return RAOCP_OK;
+}
+
+struct MegaOp {
+    template <int NX, int NU>
+    void run(raocp_ctx* c, hipError_t* err) {
+        auto k = raocp::k_mega<NX, NU>;
+        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->mega_lds);
+        if (e == hipSuccess) {
+            void* args[] = {(void*)&c->dev, (void*)&c->mega};
+            e = hipLaunchCooperativeKernel((const void*)k, dim3(c->mega_nwg), dim3(raocp::kMegaThreads), args,
+                                           (unsigned)c->mega_lds, c->stream);
+        }
+        *err = e;
+    }
+};
+
+// one persistent launch: iterations 0 .. (stop) after cp_init (buffers reset, first half step)
+int mega_launch(raocp_ctx* c, int max_iters, double tol, double alpha, unsigned long long* stamps = nullptr) {
+    raocp::MegaArg& a = c->mega;
+    for (int b = 0; b < 3; ++b) a.Z[b] = c->Z[b];
+    for (int b = 0; b < 2; ++b) a.E[b] = c->E[b];
+    a.xi2 = c->XI2;
+    a.x0 = c->x0;
+    a.hist = c->hist;
+    a.ctl = c->ctl;
+    a.alpha = alpha;
+    a.tol = tol;
+    a.max_iters = max_iters;
+    a.stamps = stamps;
+    HIPCHK(hipMemsetAsync(a.up_flag, 0, (size_t)(a.nsub + 64) * sizeof(unsigned), c->stream));
+    HIPCHK(hipMemsetAsync(a.dn_flag, 0, 64 * sizeof(unsigned), c->stream));
+    hipError_t e = hipSuccess;
+    dispatch(c->nx, c->nu, MegaOp{}, c, &e);
+    if (e != hipSuccess) return fail(RAOCP_ERR_HIP, std::string("persistent CP launch: ") + hipGetErrorString(e));
+    return RAOCP_OK;
+}
+
+bool mega_on(const raocp_ctx* c) { return c->mega_ok && !c->comm && c->sh_R == 1; }
+
 }  // namespace
 
 extern "C" {
@@ -1261,6 +1461,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     c->cur_z = c->Z[0];
     c->cur_e = c->E[0];
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
+    if ((rc = mega_plan(c, t))) return bail(rc);
     *out = c;
     return RAOCP_OK;
 }
@@ -1555,13 +1756,21 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     if ((rc = ensure_hist(c, (size_t)max_iters + 1))) return rc;
     if ((rc = raocp_set_initial_state(c, x0))) return rc;
     if ((rc = cp_init(c, x0, max_iters, tol, alpha))) return rc;
-    const int batch = kGraphBatch;
-    if ((rc = ensure_graph(c, batch))) return rc;
-    for (;;) {
-        if ((rc = launch_batch(c, batch))) return rc;
+    if (mega_on(c)) {
+        if ((rc = mega_launch(c, max_iters, tol, alpha))) return rc;
         HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
-        if (c->h_ctl->done) break;
+        if (c->h_ctl->flags & 2) return fail(RAOCP_ERR_HIP, "persistent CP engine: hand-off timed out");
+        if (!c->h_ctl->done) return fail(RAOCP_ERR_STATE, "persistent CP engine ended without a stopping decision");
+    } else {
+        const int batch = kGraphBatch;
+        if ((rc = ensure_graph(c, batch))) return rc;
+        for (;;) {
+            if ((rc = launch_batch(c, batch))) return rc;
+            HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (c->h_ctl->done) break;
+        }
     }
     const int fk = c->h_ctl->final_k;
     std::vector<double> h((size_t)(fk + 1) * 6);
@@ -1579,26 +1788,40 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     return RAOCP_OK;
 }
 
+int raocp_engine_info(raocp_ctx* c, int* cut, int* workgroups) {
+    if (!c) return fail(RAOCP_ERR_ARG, "null argument");
+    const bool on = mega_on(c);
+    if (cut) *cut = on ? c->mega_s : 0;
+    if (workgroups) *workgroups = on ? c->mega_nwg : 0;
+    return RAOCP_OK;
+}
+
 int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, float* ms) {
     if (!c || !x0 || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
     int rc;
     if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
     const int batch = kGraphBatch;
-    if ((rc = ensure_graph(c, batch))) return rc;
+    const bool mg = mega_on(c);
+    if (!mg && (rc = ensure_graph(c, batch))) return rc;
     if ((rc = cp_init(c, x0, iters - 1, 0.0, alpha))) return rc;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventRecord(e0, c->stream));
-    for (int done = 0; done < iters; done += batch)
-        if ((rc = launch_batch(c, batch))) return rc;
+    if (mg) {
+        if ((rc = mega_launch(c, iters - 1, 0.0, alpha))) return rc;
+    } else {
+        for (int done = 0; done < iters; done += batch)
+            if ((rc = launch_batch(c, batch))) return rc;
+    }
     HIPCHK(hipEventRecord(e1, c->stream));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     HIPCHK(hipMemcpy(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
+    if (c->h_ctl->flags & 2) return fail(RAOCP_ERR_HIP, "persistent CP engine: hand-off timed out");
     if (c->h_ctl->final_k != iters - 1) return fail(RAOCP_ERR_STATE, "bench did not run the requested iterations");
     c->cur_z = c->Z[iters % 3];
     c->cur_e = c->E[iters % 2];
@@ -1623,6 +1846,19 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
         int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
         if (rc2) return rc2;
         launch_cpp(c);
+    } else if (which && which[0] == 'm' && mega_on(c)) {
+        // persistent engine: 8 iterations; stamps of workgroup 0 (top) then 1 (a subtree), 64 each
+        std::vector<double> x0(c->nx, 0.0);
+        c->dev = saved;
+        if (cap < 128) return fail(RAOCP_ERR_ARG, "engine stamps need cap >= 128");
+        int rc2 = cp_init(c, x0.data(), 7, 0.0, 0.3);
+        if (rc2) return rc2;
+        unsigned long long* all = nullptr;
+        if ((rc2 = c->alloc(&all, (size_t)c->mega_nwg * 64))) return rc2;
+        HIPCHK(hipMemset(all, 0, (size_t)c->mega_nwg * 64 * sizeof(unsigned long long)));
+        if ((rc2 = mega_launch(c, 7, 0.0, 0.3, all))) return rc2;
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipMemcpy(st, all, 128 * sizeof(unsigned long long), hipMemcpyDeviceToDevice));
     } else if (which && which[0] == 'l') {  // k_ell on the staging buffers
         launch_ell(c, c->tmpP, c->tmpD);
     } else if (which && which[0] == 't') {  // k_ell_t

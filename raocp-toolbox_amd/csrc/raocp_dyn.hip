@@ -628,7 +628,7 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     glbd* z = dyn_z(bf, zsel, ctl);
     lds_sync();
     tstamp(p, pl, 1);
-    const int nall = pl.off[L] + (pl.hi[L] - pl.lo[L]), nnl = pl.off[L];
+    const int nnl = pl.off[L];
     const int root = pl.lo[0];
     ldsd* XD = smem + oXD;
     ldsd* NLd = XD + (size_t)nnl * g.KF;

@@ -1,0 +1,8 @@
+# L / L^T: parity (operators) then stamps and op timings at configs 2 and 4
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/parity.log 2>&1 || { tail -30 gpurun_out/parity.log; exit 1; }
+tail -2 gpurun_out/parity.log
+timeout -k 10 120 python tools/stamps_ell.py > gpurun_out/d_ell.txt 2>&1 || { tail -5 gpurun_out/d_ell.txt; exit 1; }
+cat gpurun_out/d_ell.txt
+timeout -k 10 200 python bench.py --steps 500 --warmup 50 --no-cpu --op-reps 500 > gpurun_out/b.json 2> gpurun_out/b.err || { tail -5 gpurun_out/b.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/b.json')); r=d['roofline']; h=d['l_sweep_hbm']; print('it/s', round(d['value'],1), '| c2 L', round(r['us_per_launch'],2), 'us', round(r['frac'],3), '| c2 LT', round(d['l_transpose']['us_per_launch'],2), '| c4 L', round(h['L']['us_per_launch'],2), round(h['L']['frac'],3), '| c4 LT', round(h['L_transpose']['us_per_launch'],2), round(h['L_transpose']['frac'],3))"
