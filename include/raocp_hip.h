@@ -155,8 +155,10 @@ int raocp_cp_run(raocp_ctx* ctx, const double* x0, int max_iters, double tol, do
  * engine (ONE launch per solve; *cut = its cut stage s > 0, *workgroups = 1 + #stage-s
  * subtrees) or the graph-replayed multi-kernel iteration (*cut = 0). The engine is
  * opt-in (RAOCP_MEGA=1 at context creation) and planned when the tree fits it;
- * RAOCP_MEGA_CUT=s forces a cut stage. */
-int raocp_engine_info(raocp_ctx* ctx, int* cut, int* workgroups);
+ * RAOCP_MEGA_CUT=s forces a cut stage. *dyn_cut > 0: inside the graph-replayed
+ * iteration each dynamics projection is ONE launch of the dynamics-only engine cut at
+ * that stage (RAOCP_DYN_ENGINE=1, RAOCP_DYN_ENGINE_CUT=s) instead of one launch per tier. */
+int raocp_engine_info(raocp_ctx* ctx, int* cut, int* workgroups, int* dyn_cut);
 
 /* Benchmark helpers (bench.py): run exactly `iters` CP iterations (tol = 0) on the
  * device (one persistent launch, or graph-replayed), without host syncs inside;

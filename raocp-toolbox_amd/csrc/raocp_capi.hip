@@ -125,6 +125,19 @@ struct raocp_ctx {
     int mega_s = 0, mega_nwg = 0;
     size_t mega_lds = 0;
     raocp::MegaArg mega{};
+    // L / L^T as streaming wave tasks (raocp_ells.hip), opt-in RAOCP_ELL_STREAM=1: on MI355X
+    // the node-range block kernels (raocp_ell.hip) are faster at configs 2 and 4
+    bool ells_on = false;
+    raocp::EllsPlan ells_l{}, ells_t{};
+    int ells_lb = 0, ells_tb = 0;
+    unsigned* ticket = nullptr;  // k_cpp blocks done (fused stopping test)
+    bool no_fuse_check = true;   // RAOCP_FUSE_CHECK=1: the stopping test inside k_cpp's last block
+                                 // (measured slower than its own launch: DESIGN.md)
+    // dynamics-only engine (one launch per projection inside the CP graph)
+    bool dyn_ok = false;
+    int dyn_s = 0, dyn_nwg = 0;
+    size_t dyn_lds = 0;
+    raocp::MegaArg dyn{};
     // captured CP iterations
     hipGraphExec_t graph = nullptr;
     int graph_iters = 0;
@@ -224,6 +237,10 @@ void allow_lds(K kernel, size_t bytes) {
 struct EllOp {
     template <int NX, int NU>
     void run(raocp_ctx* c, const double* z, double* eta) {
+        if (c->ells_on) {  // streaming wave tasks (raocp_ells.hip)
+            raocp::k_ells<NX, NU><<<c->ells_lb, 256, 0, c->stream>>>(c->dev, c->ells_l, z, eta);
+            return;
+        }
         auto k = raocp::k_ell<NX, NU>;
         allow_lds(k, c->ell_lds);
         if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ell_lds, c->stream>>>(c->dev, z, eta);
@@ -234,6 +251,10 @@ void launch_ell(raocp_ctx* c, const double* z, double* eta) { dispatch(c->nx, c-
 struct EllTOp {
     template <int NX, int NU>
     void run(raocp_ctx* c, const double* eta, double* z) {
+        if (c->ells_on) {
+            raocp::k_ellts<NX, NU><<<c->ells_tb, 256, 0, c->stream>>>(c->dev, c->ells_t, eta, z);
+            return;
+        }
         auto k = raocp::k_ell_t<NX, NU>;
         allow_lds(k, c->ellt_lds);
         if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ellt_lds, c->stream>>>(c->dev, eta, z);
@@ -246,6 +267,18 @@ struct DynOp {
     // tiers' forward sweeps (a shard exchanges the roots' q rows in between)
     template <int NX, int NU>
     void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part) {
+        if (c->dyn_ok && part == 0 && ctl && c->sh_R == 1 && !c->comm && !c->dev.stamps) {
+            raocp::MegaArg a = c->dyn;
+            const int w3 = zsel % 3;
+            a.Z[0] = a.Z[1] = a.Z[2] = w3 == 0 ? bf.z0 : (w3 == 1 ? bf.z1 : bf.z2);  // projects Z[1] only
+            a.x0 = c->x0;
+            a.ctl = c->ctl;
+            a.stamps = nullptr;
+            auto k = raocp::k_mega<NX, NU, true>;
+            allow_lds(k, c->dyn_lds);
+            k<<<c->dyn_nwg, raocp::kMegaDynThreads, c->dyn_lds, c->stream>>>(c->dev, a, ctl);
+            return;
+        }
         const int s = c->cut;
         const int B = c->dyn_block;
         // diagnostics: each launch stamps into its own 64-slot region
@@ -383,16 +416,19 @@ struct CpdOp {
     }
 };
 struct CppOp {
+    // fuse: the stopping test rides on the launch's last block (the CP iteration only)
     template <int NX, int NU>
-    void run(raocp_ctx* c) {
+    void run(raocp_ctx* c, bool fuse) {
         auto k = raocp::k_cpp<NX, NU>;
         allow_lds(k, c->lds_cpp);
         k<<<c->cp_nbF + c->cp_nbL, kBlock, c->lds_cpp, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2, c->redpart,
-                                                                     c->cp_nbF);
+                                                                     c->cp_nbF, c->hist, fuse ? c->ticket : nullptr);
     }
 };
 void launch_cpd(raocp_ctx* c) { dispatch(c->nx, c->nu, CpdOp{}, c); }
-void launch_cpp(raocp_ctx* c) { dispatch(c->nx, c->nu, CppOp{}, c); }
+void launch_cpp(raocp_ctx* c, bool fuse = false) { dispatch(c->nx, c->nu, CppOp{}, c, fuse); }
+// RAOCP_FUSE_CHECK=1: the unsharded CP iteration runs its stopping test inside k_cpp
+bool fuse_check(const raocp_ctx* c) { return !c->comm && c->sh_R == 1 && !c->no_fuse_check; }
 
 // ---- RCCL, loaded on demand (dlopen) so single-GPU users never load it
 struct Rccl {
@@ -490,9 +526,10 @@ void enqueue_cp_iteration(raocp_ctx* c, int it) {
     }
     launch_dynamics(c, c->bufs, 1, c->ctl);
     launch_cpd(c);
-    launch_cpp(c);
+    const bool fuse = fuse_check(c);
+    launch_cpp(c, fuse);
     c->bufs = keep;
-    raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
+    if (!fuse) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
 }
 
 
@@ -684,21 +721,26 @@ int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& prange
 // stage-s node, levels 0..N-s. The plan exists when every workgroup's LDS fits and the grid
 // (1 + #roots workgroups, one per CU) is co-resident. Opt-in: RAOCP_MEGA=1 (default off);
 // RAOCP_MEGA_CUT=s forces a cut.
-int mega_plan(raocp_ctx* c, const raocp_tree_desc* t) {
+struct EnginePlan {
+    bool ok = false;
+    int s = 0, nwg = 0;
+    size_t lds = 0;
+    raocp::MegaArg a{};
+};
+
+// dyn: the dynamics-only engine (no phase stage, no L tables, 1024 threads)
+int engine_plan(raocp_ctx* c, const raocp_tree_desc* t, bool dyn, EnginePlan* out) {
     using raocp::kMegaLev;
     using raocp::Rec;
-    c->mega_ok = false;
-    // opt-in (RAOCP_MEGA=1): on MI355X the graph-replayed launches are still faster
-    // (DESIGN.md, persistent engine)
-    const char* on = getenv("RAOCP_MEGA");
-    if (!on || atoi(on) == 0) return RAOCP_OK;
+    out->ok = false;
     const int N = c->N, nx = c->nx, nu = c->nu;
+    const int nthreads = dyn ? raocp::kMegaDynThreads : raocp::kMegaThreads;
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
         cus = 256;
     const size_t lds_cap = 160 * 1024 - 4096;  // dynamic LDS budget (static arrays + slack)
     int forced = -1;
-    if (const char* e = getenv("RAOCP_MEGA_CUT")) forced = atoi(e);
+    if (const char* e = getenv(dyn ? "RAOCP_DYN_ENGINE_CUT" : "RAOCP_MEGA_CUT")) forced = atoi(e);
     struct Cand {
         int s = 0;
         long cost = 0;
@@ -752,7 +794,7 @@ int mega_plan(raocp_ctx* c, const raocp_tree_desc* t) {
         // LDS: the stage gets what the largest workgroup leaves of the budget; it must hold
         // the operands of any single level of the dual / primal phases (raocp_mega.hip)
         const int ncl_top = c->cls_ptr[s], ncl_sub = c->cls_ptr[N] - c->cls_ptr[s];
-        const int nmat = c->n_sq * nx * nx + c->n_sr * nu * nu + c->n_sp * nx * nx;
+        const int nmat = dyn ? 0 : c->n_sq * nx * nx + c->n_sr * nu * nu + c->n_sp * nx * nx;
         const long budget = (long)(lds_cap / 8);
         long cap = budget, need1 = 0;
         auto rup2 = [](long v) { return (v + 1) / 2 * 2; };
@@ -770,36 +812,49 @@ int mega_plan(raocp_ctx* c, const raocp_tree_desc* t) {
             return mx;
         };
         {
-            const raocp::MegaLds m0(c->nkind, ncl_top, c->stage_ptr[s + 1], c->stage_ptr[s], maxch, nsub, nx, nu, nmat, 0);
+            const raocp::MegaLds m0(c->nkind, ncl_top, c->stage_ptr[s + 1], c->stage_ptr[s], maxch, nsub, nx, nu, nmat, 0,
+                                    nthreads);
             cap = std::min<long>(cap, budget - (m0.total - (m0.oNL - m0.oXQ)));
             need1 = std::max(need1, level_need(cd.lv.data(), s, false));
         }
         for (int k = 0; k < nsub; ++k) {
             const Rec* lv = cd.lv.data() + (size_t)(1 + k) * (kMegaLev + 1);
             const int nall = lv[L].z + (lv[L].y - lv[L].x), nnl = lv[L].z;
-            const raocp::MegaLds m1(c->nkind, ncl_sub, nall, nnl, maxch, 0, nx, nu, nmat, 0);
+            const raocp::MegaLds m1(c->nkind, ncl_sub, nall, nnl, maxch, 0, nx, nu, nmat, 0, nthreads);
             cap = std::min<long>(cap, budget - (m1.total - (m1.oNL - m1.oXQ)));
             need1 = std::max(need1, level_need(lv, L, true));
         }
-        if (cap < need1) continue;
+        if (dyn) cap = 0;
+        else if (cap < need1) continue;
         cap = cap / 2 * 2;
         size_t lds = 0;
         {
             const raocp::MegaLds m0(c->nkind, ncl_top, c->stage_ptr[s + 1], c->stage_ptr[s], maxch, nsub, nx, nu, nmat,
-                                    (int)cap);
+                                    (int)cap, nthreads);
             lds = std::max(lds, (size_t)m0.total * 8);
         }
         for (int k = 0; k < nsub; ++k) {
             const Rec* lv = cd.lv.data() + (size_t)(1 + k) * (kMegaLev + 1);
             const int nall = lv[L].z + (lv[L].y - lv[L].x), nnl = lv[L].z;
-            const raocp::MegaLds m1(c->nkind, ncl_sub, nall, nnl, maxch, 0, nx, nu, nmat, (int)cap);
+            const raocp::MegaLds m1(c->nkind, ncl_sub, nall, nnl, maxch, 0, nx, nu, nmat, (int)cap, nthreads);
             lds = std::max(lds, (size_t)m1.total * 8);
         }
         if (lds > lds_cap) continue;
         cd.lds = lds;
         cd.stage_cap = (int)cap;
-        // cost: the larger of the top and a subtree (phases) plus the levels of both sweeps
-        cd.cost = std::max(top_nodes, sub_max) * 4 + 2 * (long)N;
+        // cost: full engine: the larger of the top and a subtree (phases) plus the levels of
+        // both sweeps; dynamics only: the passes of every level step on the critical path
+        // (top levels, then the widest subtree's), a pass being one row per lane
+        if (dyn) {
+            long passes = 0;
+            const int R = nx + nu;
+            for (int l = 0; l <= s; ++l) passes += 1 + (long)(c->stage_ptr[l + 1] - c->stage_ptr[l]) * R / nthreads;
+            const Rec* lv1 = cd.lv.data() + (size_t)(kMegaLev + 1);
+            for (int l = 0; l <= L; ++l) passes += 1 + (long)(lv1[l].y - lv1[l].x) * R / nthreads;
+            cd.cost = passes;
+        } else {
+            cd.cost = std::max(top_nodes, sub_max) * 4 + 2 * (long)N;
+        }
         if (!have || cd.cost < best.cost || (cd.cost == best.cost && cd.s > best.s)) {
             best = cd;
             have = true;
@@ -807,7 +862,7 @@ int mega_plan(raocp_ctx* c, const raocp_tree_desc* t) {
     }
     if (!have) return RAOCP_OK;
     const int s = best.s, nsub = c->stage_ptr[s + 1] - c->stage_ptr[s], nwg = 1 + nsub;
-    raocp::MegaArg& a = c->mega;
+    raocp::MegaArg& a = out->a;
     int rc;
     const raocp::Rec* dlv = nullptr;
     const int* dwl = nullptr;
@@ -827,22 +882,57 @@ int mega_plan(raocp_ctx* c, const raocp_tree_desc* t) {
     a.maxch = best.maxch;
     a.stage_cap = best.stage_cap;
     a.timeout = 20000000;  // 0.2 s per wait (100 MHz)
-    c->mega_s = s;
-    c->mega_nwg = nwg;
-    c->mega_lds = best.lds;
-    c->mega_ok = true;
+    if ((rc = c->alloc(&a.epoch, 64))) return rc;
+    if (hipMemset(a.up_flag, 0, (size_t)(nsub + 64) * sizeof(unsigned)) != hipSuccess ||
+        hipMemset(a.dn_flag, 0, 64 * sizeof(unsigned)) != hipSuccess || hipMemset(a.epoch, 0, 64 * sizeof(unsigned)) != hipSuccess)
+        return fail(RAOCP_ERR_HIP, "memset");
+    out->s = s;
+    out->nwg = nwg;
+    out->lds = best.lds;
+    out->ok = true;
     if (getenv("RAOCP_VERBOSE"))
-        fprintf(stderr, "[raocp] persistent CP engine: cut stage %d, %d workgroups, LDS %zu B\n", s, nwg, best.lds);
+        fprintf(stderr, "[raocp] %s engine: cut stage %d, %d workgroups, LDS %zu B\n", dyn ? "dynamics" : "persistent CP", s,
+                nwg, best.lds);
+    return RAOCP_OK;
+}
+
+int mega_plan(raocp_ctx* c, const raocp_tree_desc* t) {
+    int rc;
+    c->mega_ok = c->dyn_ok = false;
+    // full engine: opt-in (RAOCP_MEGA=1); on MI355X the graph-replayed launches are faster
+    // (DESIGN.md, persistent engine)
+    const char* on = getenv("RAOCP_MEGA");
+    if (on && atoi(on) != 0) {
+        EnginePlan e;
+        if ((rc = engine_plan(c, t, false, &e))) return rc;
+        c->mega_ok = e.ok;
+        c->mega_s = e.s;
+        c->mega_nwg = e.nwg;
+        c->mega_lds = e.lds;
+        c->mega = e.a;
+    }
+    // dynamics-only engine inside the CP graph: RAOCP_DYN_ENGINE=1
+    const char* dn = getenv("RAOCP_DYN_ENGINE");
+    if (dn && atoi(dn) != 0) {
+        EnginePlan e;
+        if ((rc = engine_plan(c, t, true, &e))) return rc;
+        c->dyn_ok = e.ok;
+        c->dyn_s = e.s;
+        c->dyn_nwg = e.nwg;
+        c->dyn_lds = e.lds;
+        c->dyn = e.a;
+    }
     return RAOCP_OK;
 }
 
 struct MegaOp {
     template <int NX, int NU>
     void run(raocp_ctx* c, hipError_t* err) {
-        auto k = raocp::k_mega<NX, NU>;
+        auto k = raocp::k_mega<NX, NU, false>;
         hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->mega_lds);
+        const Ctl* none = nullptr;
         if (e == hipSuccess) {
-            void* args[] = {(void*)&c->dev, (void*)&c->mega};
+            void* args[] = {(void*)&c->dev, (void*)&c->mega, (void*)&none};
             e = hipLaunchCooperativeKernel((const void*)k, dim3(c->mega_nwg), dim3(raocp::kMegaThreads), args,
                                            (unsigned)c->mega_lds, c->stream);
         }
@@ -1462,6 +1552,21 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     c->cur_e = c->E[0];
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
     if ((rc = mega_plan(c, t))) return bail(rc);
+    {
+        const int rtx = cdiv(nx, 16), rtu = cdiv(nu, 16), tc = cdiv(n - 1, 16), tl = cdiv(n - m, 16), tp = cdiv(m, 16);
+        const int per = 64 * raocp::kEllsE;
+        const long ny = c->dev.T0 - c->dev.Y0;
+        const long totl = ny + m + (n - 1) + (long)m * (nx + nu) + (n - m) + (long)(n - m) * nx;
+        const long tott = (long)m + (n - 1) + (n - m);
+        c->ells_l = raocp::EllsPlan{tc * rtx, tc * rtu, tl * rtx, rtx, rtu, (int)((totl + per - 1) / per)};
+        c->ells_t = raocp::EllsPlan{tp * rtx, tp * rtu, tl * rtx, rtx, rtu, (int)((tott + per - 1) / per)};
+        c->ells_lb = cdiv(c->ells_l.nQ + c->ells_l.nR + c->ells_l.nP + c->ells_l.ncopy, 4);
+        c->ells_tb = cdiv(c->ells_t.nQ + c->ells_t.nR + c->ells_t.nP + c->ells_t.ncopy, 4);
+        if (const char* e = getenv("RAOCP_ELL_STREAM")) c->ells_on = atoi(e) != 0;
+    }
+    if ((rc = c->alloc(&c->ticket, 64))) return bail(rc);
+    if (hipMemset(c->ticket, 0, 64 * sizeof(unsigned)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
+    if (const char* e = getenv("RAOCP_FUSE_CHECK")) c->no_fuse_check = atoi(e) == 0;
     *out = c;
     return RAOCP_OK;
 }
@@ -1788,11 +1893,12 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     return RAOCP_OK;
 }
 
-int raocp_engine_info(raocp_ctx* c, int* cut, int* workgroups) {
+int raocp_engine_info(raocp_ctx* c, int* cut, int* workgroups, int* dyn_cut) {
     if (!c) return fail(RAOCP_ERR_ARG, "null argument");
     const bool on = mega_on(c);
     if (cut) *cut = on ? c->mega_s : 0;
     if (workgroups) *workgroups = on ? c->mega_nwg : 0;
+    if (dyn_cut) *dyn_cut = (c->dyn_ok && c->sh_R == 1 && !c->comm) ? c->dyn_s : 0;
     return RAOCP_OK;
 }
 

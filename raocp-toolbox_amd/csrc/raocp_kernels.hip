@@ -98,6 +98,20 @@ __device__ __forceinline__ void stamp(const Dev& p, int slot) {
 }
 
 
+// agent-scope relaxed accesses (global_store / global_load ... sc1): write-through stores and
+// L1-bypassing loads for values another workgroup of the same launch reads (MI355X: per-XCD
+// L2s are not coherent with each other)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(1))) unsigned int gu32;
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return __longlong_as_double(
+        (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 __device__ __forceinline__ int e3(const Dev& p, int j) { return p.E3 + 1 + (j - 1) * p.nx; }
 __device__ __forceinline__ int e4(const Dev& p, int j) { return p.E4 + 1 + (j - 1) * p.nu; }
 __device__ __forceinline__ int e11(const Dev& p, int l) { return p.E11 + p.m + (l - p.m) * p.nx; }
@@ -271,6 +285,7 @@ __device__ __forceinline__ int dma_any(ldsd* dst, PT src, int nbytes, int* rot =
 }
 
 #include "raocp_ell.hip"
+#include "raocp_ells.hip"
 
 // ==============================================================================
 // AVaR kernel projection of (y_i, tau_children, s_children) (cache.py:290-317),

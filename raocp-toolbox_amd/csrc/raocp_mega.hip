@@ -32,7 +32,8 @@
 // (MegaArg::timeout, 100 MHz ticks): a timed-out workgroup sets ctl->flags bit 1 and
 // leaves, so the others time out too and the launch drains.
 
-constexpr int kMegaThreads = 512;
+constexpr int kMegaThreads = 512;   // full engine (dual / primal phases: 256 VGPRs per lane)
+constexpr int kMegaDynThreads = 1024;  // dynamics-only engine
 constexpr int kMegaLev = 16;  // levels per workgroup (the host plans within it)
 
 struct MegaArg {
@@ -55,19 +56,11 @@ struct MegaArg {
     int stage_cap;               // doubles of the LDS stage (aliases the dynamics rows)
     long long timeout;           // per wait, 100 MHz ticks
     unsigned long long* stamps;  // diagnostics: [nwg][64] (nullptr = off)
+    unsigned* epoch;             // dynamics-only engine: launches so far (flag tags grow across launches)
 };
 
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned int gu32;
+typedef __attribute__((address_space(1))) unsigned int glbd32;
 
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double* p) {
-    return __longlong_as_double(
-        (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
 __device__ __forceinline__ unsigned ld_flag(const unsigned* f) {
     return __hip_atomic_load((gu32*)f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -87,7 +80,7 @@ __device__ __forceinline__ void mega_publish(unsigned* flag, unsigned v) {
 struct MegaLds {
     int oW, oRG, oKM, oMAT, oXQ, oU, oDR, oP, oNL, oCH, oSX, oE2, total;
     __host__ __device__ MegaLds(int nkind, int ncls, int nall, int nnl, int maxch, int nb, int nx, int nu, int nmat,
-                                int stage_cap) {
+                                int stage_cap, int nthreads = kMegaThreads) {
         const int KP = rup(nx, 2 * kKS), NUP = rup(nu, 2), PS = NUP + rup(nx, 2);
         const int SKP = tstride(KP), SNU = tstride(NUP), R = nx + nu;
         oW = 0;
@@ -102,7 +95,7 @@ struct MegaLds {
         oNL = oXQ + (dyn > stage_cap ? dyn : stage_cap);
         oCH = oNL + 2 * nnl;
         oSX = oCH + 2 * nall;
-        oE2 = oSX + kMegaThreads;
+        oE2 = oSX + nthreads;
         total = oE2 + 4 * nb;
     }
 };
@@ -229,12 +222,16 @@ __device__ __forceinline__ void mega_fwd_level(const Dev& p, const ldsd* W, cons
     lds_sync();
 }
 
-template <int NXc, int NUc>
-__global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
+// DYN: the dynamics projection only (cache.py:259-288) of the half step a.Z[1], one launch per
+// projection inside the captured CP iteration: the backward / forward sweeps and the two
+// hand-offs, no dual / primal phases; tags continue from *a.epoch.
+template <int NXc, int NUc, bool DYN>
+__global__ void __launch_bounds__(DYN ? kMegaDynThreads : kMegaThreads) k_mega(Dev p, MegaArg a, const Ctl* dctl) {
+    constexpr int NT = DYN ? kMegaDynThreads : kMegaThreads;
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ int s_lo[kMegaLev + 1], s_hi[kMegaLev + 1], s_off[kMegaLev + 1];
     __shared__ int s_L, s_ok, s_stop;
-    __shared__ double s_red[kMegaThreads / 64][8];
+    __shared__ double s_red[NT / 64][8];
     __shared__ double s_sr[2];  // subtree: s_r of z+ and of p
     __shared__ int s_sg[kMegaLev + 1][8];  // LDS offsets of the staged operands, per level
     const int wg = blockIdx.x, tid = threadIdx.x, nthr = blockDim.x;
@@ -251,6 +248,10 @@ __global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
         ++nst;
     };
     stamp_();
+    // the dynamics-only engine inside a captured batch: iterations past the stopping test
+    // do nothing (every workgroup reads the same word, so none waits on another)
+    if (DYN && dctl && dctl->done) return;
+    const unsigned ep = DYN ? *(const glbd32*)a.epoch : 0u;
     if (tid <= kMegaLev) {
         const Rec r = a.lv[(size_t)wg * (kMegaLev + 1) + tid];
         s_lo[tid] = r.x;
@@ -268,7 +269,8 @@ __global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
     const int nall = s_off[L] + (s_hi[L] - s_lo[L]), nnl = s_off[L];
     const int c0 = top ? 0 : a.c_sub0, c1 = top ? a.c_top1 : a.c_sub1;
     const int nQ = p.nSQ * nx * nx, nR = p.nSR * nu * nu, nP = p.nSP * nx * nx;
-    const MegaLds ml(p.nkind, c1 - c0, nall, nnl, a.maxch, top ? a.nsub : 0, nx, nu, nQ + nR + nP, a.stage_cap);
+    const MegaLds ml(p.nkind, c1 - c0, nall, nnl, a.maxch, top ? a.nsub : 0, nx, nu, DYN ? 0 : nQ + nR + nP,
+                     DYN ? 0 : a.stage_cap, NT);
     ldsd* sm = (ldsd*)smem_;
     ldsd* W = sm + ml.oW;
     ldsd* RG = sm + ml.oRG;
@@ -307,10 +309,12 @@ __global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
         for (int e = tid; e < nW; e += nthr) W[e] = gW[e];
         for (int e = tid; e < nRG; e += nthr) RG[e] = gRG[e];
         for (int e = tid; e < nKM; e += nthr) KM[e] = gKM[e];
-        ldsd* MAT = sm + ml.oMAT;
-        for (int e = tid; e < nQ; e += nthr) MAT[e] = ((const glbd*)p.SQ)[e];
-        for (int e = tid; e < nR; e += nthr) MAT[nQ + e] = ((const glbd*)p.SR)[e];
-        for (int e = tid; e < nP; e += nthr) MAT[nQ + nR + e] = ((const glbd*)p.SP)[e];
+        if (!DYN) {
+            ldsd* MAT = sm + ml.oMAT;
+            for (int e = tid; e < nQ; e += nthr) MAT[e] = ((const glbd*)p.SQ)[e];
+            for (int e = tid; e < nR; e += nthr) MAT[nQ + e] = ((const glbd*)p.SR)[e];
+            for (int e = tid; e < nP; e += nthr) MAT[nQ + nR + e] = ((const glbd*)p.SP)[e];
+        }
         ldsrec* NL = (ldsrec*)NLd;
         ldsrec* CH = (ldsrec*)CHd;
         for (int l = 0; l <= L; ++l) {
@@ -349,7 +353,7 @@ __global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
         glbd* Ed = (glbd*)a.E[it % 2];
         glbd* Ee = (glbd*)a.E[(it + 1) % 2];
         glbd* X2 = (glbd*)a.xi2;
-        const unsigned tag = (unsigned)(it + 1);
+        const unsigned tag = ep + (unsigned)(it + 1);
 
         // ================= backward sweep: x, u rows of the half step -> q, d ==================
         if (top) {
@@ -534,6 +538,11 @@ __global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
             }
             mega_publish(a.dn_flag, 2u * tag);
             stamp_();
+            if (DYN) {
+                // every subtree has read the epoch (its UP arrived): the next launch's tags follow
+                if (tid == 0) *(glbd32*)a.epoch = ep + 1u;
+                break;
+            }
         } else {
             // subtree: x, u rows of the half step (leaves too: their q = -x)
             for (int l = 0; l <= L; ++l) {
@@ -614,7 +623,7 @@ __global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
                 XQ[tid] = v;
                 Zc[p.X0 + (size_t)root * nx + tid] = v;
             }
-            if (tid == 64) {
+            if (!DYN && tid == 64) {  // s_r of z+ and p (the dual's eta2_r row)
                 s_sr[1] = it == 0 ? (double)Zp[p.S0 + root] : s_sr[0];
                 s_sr[0] = ld_sc1(drec + nx);
             }
@@ -624,8 +633,10 @@ __global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
                                          rows(XQ, l, g.KP), rows(DR, l, g.NUP), rows(U, l, g.NUP),
                                          rows(XQ, l + 1, g.KP), Zc, true);
             stamp_();
+            if (DYN) break;
         }
 
+        if constexpr (!DYN) {
         // ================= dual: eta+ = prox_{alpha g*}(d + alpha L(2z+ - p)), xi2, delta2 =====
         // Operands read by several lanes (the parents' x, u rows of z+ and p, the child / node
         // records) are staged into LDS by LDS-DMA, a batch of levels at a time (one memory round
@@ -1021,6 +1032,7 @@ __global__ void __launch_bounds__(kMegaThreads) k_mega(Dev p, MegaArg a) {
         }
         __syncthreads();
         stamp_();
+        }  // !DYN
     }
     if (!s_ok && tid == 0) atomicOr(&a.ctl->flags, 2);
 }

@@ -89,7 +89,7 @@ def load_library():
         "raocp_step_size": (c_int, [vp, _f64p, c_int, c_double]),
         "raocp_cp_run": (c_int, [vp, vp, c_int, c_double, c_double, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                  vp, vp]),
-        "raocp_engine_info": (c_int, [vp, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+        "raocp_engine_info": (c_int, [vp, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
         "raocp_cp_bench": (c_int, [vp, vp, c_int, c_double, ctypes.POINTER(ctypes.c_float)]),
         "raocp_op_bench": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_float)]),
         "raocp_dual_scale": (c_int, [vp, c_double]),
@@ -307,9 +307,15 @@ class NativeContext:
     def engine_info(self):
         """(cut stage, workgroups) of the persistent CP engine, or (0, 0) when the context
         runs the graph-replayed multi-kernel iteration."""
-        cut, wg = ctypes.c_int(), ctypes.c_int()
-        self._check(self._lib.raocp_engine_info(self._h, ctypes.byref(cut), ctypes.byref(wg)))
+        cut, wg, dc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._check(self._lib.raocp_engine_info(self._h, ctypes.byref(cut), ctypes.byref(wg), ctypes.byref(dc)))
         return cut.value, wg.value
+
+    def dyn_engine_cut(self):
+        """cut stage of the dynamics-only engine used inside the CP iteration (0: tier launches)"""
+        cut, wg, dc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        self._check(self._lib.raocp_engine_info(self._h, ctypes.byref(cut), ctypes.byref(wg), ctypes.byref(dc)))
+        return dc.value
 
     def engine_cut(self):
         return self.engine_info()[0]

@@ -93,3 +93,35 @@ def test_engine_repeated_runs_are_identical(c2_ref):
     _, e2, _ = cache.native.cp_run(r["x0"], 9, 0.0, alpha)
     assert np.array_equal(e1, e2)
     assert np.array_equal(z1, cache.get_primal_flat())
+
+
+@pytest.mark.parametrize("cut", [0, 6, 7])
+def test_c2_dynamics_engine_vs_oracle(c2_ref, cut):
+    """graph-replayed CP iteration whose dynamics projection is ONE launch of the
+    dynamics-only engine (cut 0: the planner's choice)"""
+    r, prob, alpha, (st_o, err_o, derr_o, z_o, e_o) = c2_ref
+    env = {"RAOCP_DYN_ENGINE": "1"}
+    if cut:
+        env["RAOCP_DYN_ENGINE_CUT"] = cut
+    cache = _with_env(env, lambda: core.Cache(prob))
+    dc = cache.native.dyn_engine_cut()
+    assert dc > 0 and (cut == 0 or dc == cut)
+    for _ in range(2):  # the epoch-tagged flags carry over between solves
+        status, err, derr = cache.native.cp_run(r["x0"], 29, 0.0, alpha)
+        assert status == st_o == 1 and err.shape == (30, 3)
+        assert trace_rel_err(err, err_o) <= 1e-8
+        assert trace_rel_err(derr, derr_o) <= 1e-8
+        assert rel_err(cache.get_primal_flat(), z_o) <= 1e-10
+        assert rel_err(cache.get_dual_flat(), e_o) <= 1e-10
+
+
+def test_dynamics_engine_main_py_trace(golden):
+    z = golden("main_trace")
+    r, tree, prob = problem_from_golden(z, "main")
+    solver = _with_env({"RAOCP_DYN_ENGINE": "1"}, lambda: core.Solver(problem_spec=prob))
+    assert solver.cache.native.dyn_engine_cut() > 0
+    status = solver.chock(initial_state=r["x0"].reshape(-1, 1), max_iters=int(z["main/cp_max_iters"]),
+                          tol=float(z["main/cp_tol"]), step_size=float(z["main/cp_alpha"]))
+    assert status == 0 and solver.error_cache.shape == (937, 3)
+    assert trace_rel_err(solver.error_cache, z["main/cp_error"]) <= 1e-8
+    assert rel_err(solver.cache.get_primal_flat(), z["main/cp_z"]) <= 1e-9

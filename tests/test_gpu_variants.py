@@ -1,0 +1,89 @@
+"""GPU parity of the opt-in kernel variants (measured slower on MI355X than the defaults,
+kept correct): L / L^T as streaming wave-task kernels (raocp_ells.hip, RAOCP_ELL_STREAM=1)
+and the CP stopping test fused into k_cpp's last block (RAOCP_FUSE_CHECK=1).
+
+Tolerances as in test_gpu_parity.py.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import raocp.core as core
+from raocp.problems import build_problem, recipe_config
+from helpers import problem_from_golden, rel_err, trace_rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("name", ["main", "ops2x2", "bin6", "c1n5"])
+def test_streaming_ell_matches_reference(golden, name):
+    z = golden("ops_kat")
+    r, tree, prob = problem_from_golden(z, name)
+    cache = _with_env({"RAOCP_ELL_STREAM": "1"}, lambda: core.Cache(prob))
+    op = core.Operator(cache)
+    lz = op.linop_ell(z[f"{name}/ops_z"].reshape(-1, 1)).reshape(-1)
+    assert rel_err(lz, z[f"{name}/ops_Lz"]) <= 1e-12
+    lte = op.linop_ell_transpose(z[f"{name}/ops_eta"].reshape(-1, 1)).reshape(-1)
+    assert rel_err(lte, z[f"{name}/ops_LTeta"]) <= 1e-12
+
+
+@pytest.mark.parametrize("cfg", [2, 4, "4-modes"])
+def test_streaming_ell_large_vs_oracle(cfg):
+    """config 4 with a different cost per mode: tiles mixing weight tables take the per-lane path"""
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(4 if cfg == "4-modes" else cfg)
+    if cfg == "4-modes":
+        r["Q"] = np.array([(1.0 + k) * q for k, q in enumerate(r["Q"])])
+        r["R"] = np.array([(2.0 + k) * q for k, q in enumerate(r["R"])])
+    tree, prob = build_problem(r)
+    cache = _with_env({"RAOCP_ELL_STREAM": "1"}, lambda: core.Cache(prob))
+    orc = OracleProblem(prob)
+    rng = np.random.default_rng(5)
+    zz = rng.standard_normal(cache.primal_size)
+    ee = rng.standard_normal(cache.dual_size)
+    lz, lte = cache.native.ell(zz), cache.native.ell_t(ee)
+    assert rel_err(lz, orc.ell(zz)) <= 1e-12
+    assert rel_err(lte, orc.ell_t(ee)) <= 1e-12
+    a, b = zz @ lte, lz @ ee
+    assert abs(a - b) <= 1e-10 * max(abs(a), 1.0)
+
+
+def test_fused_stopping_test_c2_vs_oracle():
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    orc = OracleProblem(prob)
+    cache = _with_env({"RAOCP_FUSE_CHECK": "1"}, lambda: core.Cache(prob))
+    alpha = 0.999 / cache.native.step_size()
+    st_o, err_o, derr_o, z_o, e_o, _ = orc.chock(r["x0"], 29, 0.0, alpha=alpha)
+    for _ in range(2):  # the ticket is re-armed by the last block of every launch
+        status, err, derr = cache.native.cp_run(r["x0"], 29, 0.0, alpha)
+        assert status == st_o == 1 and err.shape == (30, 3)
+        assert trace_rel_err(err, err_o) <= 1e-8
+        assert trace_rel_err(derr, derr_o) <= 1e-8
+        assert rel_err(cache.get_primal_flat(), z_o) <= 1e-10
+
+
+def test_fused_stopping_test_main_py(golden):
+    z = golden("main_trace")
+    r, tree, prob = problem_from_golden(z, "main")
+    solver = _with_env({"RAOCP_FUSE_CHECK": "1"}, lambda: core.Solver(problem_spec=prob))
+    status = solver.chock(initial_state=r["x0"].reshape(-1, 1), max_iters=int(z["main/cp_max_iters"]),
+                          tol=float(z["main/cp_tol"]), step_size=float(z["main/cp_alpha"]))
+    assert status == 0 and solver.error_cache.shape == (937, 3)
+    assert trace_rel_err(solver.error_cache, z["main/cp_error"]) <= 1e-8
+    assert rel_err(solver.cache.get_primal_flat(), z["main/cp_z"]) <= 1e-9
