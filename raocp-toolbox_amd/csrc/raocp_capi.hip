@@ -1435,7 +1435,13 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         if ((rc = c->upload_vec(&D.frec, frec)) || (rc = c->upload_vec(&D.lrec, lrec))) return bail(rc);
         // block sizes: about 256 family and 256 leaf blocks, within the LDS budget
         const long kCpLds = 64 * 1024 / 8;  // doubles: keeps >= 2 blocks per CU
-        int FB = std::max(1, (m + 255) / 256), LB = std::max(1, (n - m + 255) / 256);
+        // family blocks of one k_cpp lane chunk (kBlock / (nx + nu + cmax + 1) parents: the
+        // chunks of a block run one after the other; measured +3.7 % it/s at config 2 over
+        // 256 blocks of 16 parents), leaf blocks of ~1/256 of the leaves
+        int FB = std::max(1, std::min((m + 255) / 256, kBlock / (nx + nu + cmax + 1))),
+            LB = std::max(1, (n - m + 255) / 256);
+        if (const char* e = getenv("RAOCP_CP_FB")) FB = std::max(1, atoi(e));  // parents per family block
+        if (const char* e = getenv("RAOCP_CP_LB")) LB = std::max(1, atoi(e));  // leaves per leaf block
         const std::vector<std::pair<int, int>> allp{{0, m}}, alll{{m, n}};
         while (FB > 1 && cp_need(c, allp, {}, FB, LB) > kCpLds) FB = FB * 3 / 4;
         while (LB > 1 && cp_need(c, {}, alll, FB, LB) > kCpLds) LB = LB * 3 / 4;
@@ -1564,6 +1570,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         c->ells_tb = cdiv(c->ells_t.nQ + c->ells_t.nR + c->ells_t.nP + c->ells_t.ncopy, 4);
         if (const char* e = getenv("RAOCP_ELL_STREAM")) c->ells_on = atoi(e) != 0;
     }
+    c->dev.regstage = 0;  // RAOCP_REGSTAGE=1: k_ell's gather by vector loads (measured slower)
+    if (const char* e = getenv("RAOCP_REGSTAGE")) c->dev.regstage = atoi(e) != 0;
     if ((rc = c->alloc(&c->ticket, 64))) return bail(rc);
     if (hipMemset(c->ticket, 0, 64 * sizeof(unsigned)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
     if (const char* e = getenv("RAOCP_FUSE_CHECK")) c->no_fuse_check = atoi(e) == 0;

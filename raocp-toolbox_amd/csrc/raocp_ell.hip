@@ -59,6 +59,33 @@ struct Gather {
             }
         }
     }
+    // the same chunks by vector loads into registers (all of a lane's loads in flight, then
+    // LDS stores): a CU streams ~4x the bytes of its LDS-DMA path (staging)
+    __device__ __forceinline__ void issue_reg() const {
+        const int tid = threadIdx.x, nt = blockDim.x;
+        constexpr int K = 8;
+        for (int b0 = 0; b0 < total; b0 += K * nt) {
+            d2v v[K];
+            _Pragma("unroll") for (int k = 0; k < K; ++k) {
+                const int ch = b0 + k * nt + tid;
+                if (ch < total) {
+                    const char* s = src[0];
+                    int c = cum[0];
+                    _Pragma("unroll") for (int r = 1; r < MAXR; ++r)
+                        if (r < nr && ch >= cum[r]) { s = src[r]; c = cum[r]; }
+                    v[k] = *(const glb2*)(s + 16 * (ch - c));
+                }
+            }
+            _Pragma("unroll") for (int k = 0; k < K; ++k) {
+                const int ch = b0 + k * nt + tid;
+                if (ch < total) *(lds2*)(base + 2 * ch) = v[k];
+            }
+        }
+    }
+    __device__ __forceinline__ void issue(bool reg) const {
+        if (reg) issue_reg();
+        else issue();
+    }
 };
 
 // sequential LDS regions filled by LDS-DMA, one DMA pass per region (CP kernels)
@@ -288,7 +315,7 @@ __global__ void __launch_bounds__(512) k_ell(Dev p, const double* __restrict__ z
     const ldsd* XL = g.dbl(zg + p.X0 + (size_t)l0 * nx, nl * nx);  // leaves' x, s
     const ldsd* SL = g.dbl(zg + p.S0 + l0, nl);
     const ldsrec* LR = g.rec(p.lrec + (l0 - p.m), nl);  // {iSP, iBl, e14off, 0}
-    g.issue();
+    g.issue(p.regstage);
     const Rec t3 = tb[3];
     FamRun<NXc, NUc> fr(Fam{p.SQ, t3.x, nx, c0, nc, X}, Fam{p.SR, t3.y, nu, c0, nc, U}, Fam{p.SP, t3.z, nx, l0, nl, XL});
     fr.prefetch();
@@ -367,7 +394,7 @@ __global__ void __launch_bounds__(512) k_ell_t(Dev p, const double* __restrict__
     const ldsd* D12 = g.dbl(eg + p.E12 + l0, nl);
     const ldsd* D13 = g.dbl(eg + p.E13 + l0, nl);
     const ldsrec* LR = g.rec(p.lrec + (l0 - p.m), nl);  // {iSP, iBl, e14off, 0}
-    g.issue();
+    g.issue(p.regstage);
     // products sqrtQ_j eta3_j, sqrtR_j eta4_j (children), sqrtPf_l eta11_l (leaves) in LDS
     ldsd* PX = (ldsd*)ell_smem + 2 * g.total;
     ldsd* PU = PX + nc * nx;

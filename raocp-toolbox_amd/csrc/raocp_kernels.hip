@@ -90,6 +90,7 @@ struct Dev {
     const int* stage_ptr;  // [N+2] first node id of each stage (BFS numbering)
     int N;                 // last stage
     unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)
+    int regstage;          // staging by vector loads + LDS stores instead of LDS-DMA (RAOCP_REGSTAGE)
 };
 
 // diagnostic timestamp (100 MHz constant clock), thread 0 only, when enabled

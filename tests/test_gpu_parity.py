@@ -249,3 +249,38 @@ def test_large_operators_vs_oracle(cfg):
     assert rel_err(lte, orc.ell_t(ee)) <= 1e-12
     a, b = zz @ lte, lz @ ee
     assert abs(a - b) <= 1e-10 * max(abs(a), 1.0)
+
+
+@pytest.mark.parametrize("cfg", [2, 3])
+def test_projections_full_size_vs_oracle_and_idempotent(cfg):
+    """The dynamics and kernel projections (cache.py:259-317) at the HBM-sized configs:
+    against the oracle, and size-independent properties: a projection applied twice is
+    the projection (idempotence), and its output satisfies x_j = A_j x_i + B_j u_i,
+    x_0 = x0 (feasibility; relative to the state scale)."""
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(cfg)
+    tree, prob = build_problem(r)
+    cache, orc = core.Cache(prob), OracleProblem(prob)
+    nat = cache.native
+    rng = np.random.default_rng(17)
+    zz = rng.standard_normal(cache.primal_size)
+    cache.cache_initial_state(r["x0"])
+    nat.set_primal(zz)
+    nat.project_on_dynamics()
+    z1 = nat.get_primal()
+    assert rel_err(z1, orc.project_on_dynamics(zz, r["x0"])) <= 1e-11
+    nat.project_on_dynamics()
+    assert rel_err(nat.get_primal(), z1) <= 1e-11
+    X = z1[orc.X0:orc.U0].reshape(orc.n, orc.nx)
+    U = z1[orc.U0:orc.Y0].reshape(orc.m, orc.nu)
+    j = np.arange(1, orc.n)
+    par = orc.anc[j]
+    pred = np.stack([orc.A[orc.iA[k]] @ X[par[t]] + orc.B[orc.iB[k]] @ U[par[t]] for t, k in enumerate(j)])
+    assert np.max(np.abs(X[j] - pred)) <= 1e-10 * max(1.0, np.max(np.abs(X)))
+    assert np.array_equal(X[0], np.asarray(r["x0"], dtype=float).reshape(-1))
+    nat.set_primal(zz)
+    nat.project_on_kernel()
+    z2 = nat.get_primal()
+    assert rel_err(z2, orc.project_on_kernel(zz)) <= 1e-12
+    nat.project_on_kernel()
+    assert rel_err(nat.get_primal(), z2) <= 1e-12
