@@ -69,10 +69,12 @@ struct raocp_ctx {
     std::vector<int> pair_ptr;   // first (kind, class) pair of each class (size n_k+1)
     int nkind = 0;
     bool f_lds_top = false;      // F table staged in LDS by k_dyn_top
+    bool fold_top = false;       // k_dyn_top's backward levels in one phase (WT tables)
     struct TierPlan {            // a tier [s0, s1) below the top: one workgroup per subtree
         int s0, s1, nsub, maxch;
         size_t lds_b, lds_f;
         bool fl;                 // F staged in LDS by the forward kernel
+        bool fold;               // one-phase backward levels (WT tables)
         const raocp::Rec* lv;    // level ranges of its subtrees
         raocp::TierArg ta;       // the same, as a kernel argument, when the tier is regular
     };
@@ -301,16 +303,18 @@ struct DynOp {
                 for (int k = (int)c->tiers.size() - 1; k >= 0; --k) {
                     const auto& tp = c->tiers[k];
                     const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1];
-                    auto kb = raocp::k_dyn_bottom_back<NX, NU>;
+                    const int p0 = c->pair_ptr[c0], p1 = c->pair_ptr[c1];
+                    auto kb = tp.fold ? raocp::k_dyn_bottom_back<NX, NU, true> : raocp::k_dyn_bottom_back<NX, NU, false>;
                     allow_lds(kb, tp.lds_b);
                     if (tier_blocks(k) > 0)
                         kb<<<tier_blocks(k), B, tp.lds_b, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->d, tp.s0, tp.s1,
-                                                                      tp.maxch, c0, c1, tp.lv, tier_arg(k));
+                                                                      tp.maxch, c0, c1, p0, p1, tp.lv, tier_arg(k));
                 }
             if (part == 1) return;
             {
                 const int c1 = c->cls_ptr[s], p1 = c->pair_ptr[c1];
-                auto kt = c->f_lds_top ? raocp::k_dyn_top<NX, NU, true> : raocp::k_dyn_top<NX, NU, false>;
+                auto kt = c->f_lds_top ? (c->fold_top ? raocp::k_dyn_top<NX, NU, true, true> : raocp::k_dyn_top<NX, NU, true, false>)
+                                       : (c->fold_top ? raocp::k_dyn_top<NX, NU, false, true> : raocp::k_dyn_top<NX, NU, false, false>);
                 allow_lds(kt, c->lds_top);
                 const int T = c->stage_ptr[s], nb = c->stage_ptr[s + 1] - T;
                 kt<<<1, B, c->lds_top, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->x0, s, c->maxch_top, c1, p1, T, nb);
@@ -1212,8 +1216,25 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 for (int k = 0; k < nu; ++k) F[(q * nx + r) * SKF + nx + k] = Bm(ib, r, k);
             }
         }
+        // one-phase backward levels: WT[pair] = [-Rinv B' ; A' - G B'] of (child kind, parent class)
+        std::vector<double> WT(std::max<size_t>(1, pairs.size()) * R * SKP, 0.0);
+        for (size_t q = 0; q < pairs.size(); ++q) {
+            const int ia = kinds[pairs[q].first].first, ib = kinds[pairs[q].first].second, c_ = pairs[q].second;
+            for (int tr = 0; tr < R; ++tr)
+                for (int k = 0; k < nx; ++k) {
+                    double v = 0.0;
+                    if (tr < nu) {
+                        for (int t2 = 0; t2 < nu; ++t2) v -= Ri(c_, tr, t2) * Bm(ib, k, t2);
+                    } else {
+                        const double* grow = &RG[((size_t)c_ * R + tr) * SNU];
+                        for (int t2 = 0; t2 < nu; ++t2) v -= grow[t2] * Bm(ib, k, t2);
+                        v += A(ia, k, tr - nu);
+                    }
+                    WT[(q * R + tr) * SKP + k] = v;
+                }
+        }
         if ((rc = c->upload_vec(&D.dW, W)) || (rc = c->upload_vec(&D.dRG, RG)) || (rc = c->upload_vec(&D.dKM, KM)) ||
-            (rc = c->upload_vec(&D.dF, F)))
+            (rc = c->upload_vec(&D.dF, F)) || (rc = c->upload_vec(&D.dWT, WT)))
             return bail(rc);
         std::vector<raocp::Rec> ninfo(m), cinfo(n);
         for (int i = 0; i < m; ++i) ninfo[i] = raocp::Rec{t->ch_start[i], t->nch[i], pr->i_k[i], t->stage[i]};
@@ -1259,12 +1280,15 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         auto stage_n = [&](int st) { return c->stage_ptr[st + 1] - c->stage_ptr[st]; };
         auto level_cost = [&](double P, double C) { return 3.0 + (C * R + P * R + P * nu + C * nx) / 384.0; };
         auto recs = [](size_t cnt) { return 2 * cnt; };  // 16-B records in doubles
-        auto top_bytes = [&](int s_, int& maxch, bool fl) {
+        // fold: one-phase backward levels (per-pair WT tables instead of per-kind W, no P rows)
+        bool fold_ok = false;  // measured slower at config 2: opt-in RAOCP_DYN_FOLD=1
+        if (const char* env = getenv("RAOCP_DYN_FOLD")) fold_ok = atoi(env) != 0;
+        auto top_bytes = [&](int s_, int& maxch, bool fl, bool fold) {
             const size_t T = c->stage_ptr[s_], nb = stage_n(s_);
             maxch = 0;
             for (int st = 1; st <= s_; ++st) maxch = std::max(maxch, stage_n(st));
-            const size_t mats = c->nkind * W1 + cp[s_] * (RG1 + KM1) + (fl ? pp[cp[s_]] * F1 : 0);
-            const size_t dbl = mats + T * KP + nb * KP + T * NUP + T * KF + raocp::rup(maxch * PS, 2) +
+            const size_t mats = (fold ? pp[cp[s_]] * W1 : c->nkind * W1) + cp[s_] * (RG1 + KM1) + (fl ? pp[cp[s_]] * F1 : 0);
+            const size_t dbl = mats + T * KP + nb * KP + T * NUP + T * KF + (fold ? 0 : raocp::rup(maxch * PS, 2)) +
                                recs(T + T + nb - 1);
             return 8 * dbl;
         };
@@ -1273,7 +1297,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             int maxch = 0;
             double cost = 0;
             size_t bb = 0, bf = 0;
-            bool fl = true, ok = false;
+            bool fl = true, ok = false, fold = false;
         };
         auto tier = [&](int a, int b) {  // subtrees rooted at stage a, levels a..b-1, boundary b (worst case)
             Tier w;
@@ -1299,6 +1323,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             const size_t st_b = 0, st_f = 0;
             w.bb = 8 * (c->nkind * W1 + ncl * RG1 + w.nall * KP + w.nnl * NUP + raocp::rup(w.maxch * PS, 2) +
                         recs(w.nnl + w.nall - 1) + st_b);
+            const size_t bb_fold = 8 * (npr * W1 + ncl * RG1 + w.nall * KP + w.nnl * NUP + recs(w.nnl + w.nall - 1) + st_b);
+            if (fold_ok && bb_fold <= kLds) {
+                w.fold = true;
+                w.bb = bb_fold;
+                w.cost -= (b - a);  // one barrier phase per backward level instead of two
+            }
             w.bf = 8 * (ncl * KM1 + npr * F1 + w.nnl * KF + recs(w.nnl + w.nall - 1) + st_f);
             if (w.bf > kLds) {
                 w.fl = false;
@@ -1331,23 +1361,26 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         double top_cost = 5.0;
         for (int s_ = 1; s_ <= N && s_ <= raocp::kMaxTopStages; ++s_) {
             top_cost += level_cost(stage_n(s_ - 1), stage_n(s_));
-            int mt = 0;
-            bool fl = true;
-            size_t tb = top_bytes(s_, mt, true);
-            if (tb > kLds) {
-                fl = false;
-                tb = top_bytes(s_, mt, false);
+            bool any = false;
+            for (int v = 0; v < 4; ++v) {  // (F in LDS, fold) = (1,1), (1,0), (0,1), (0,0)
+                const bool fl = v < 2, fold = (v % 2 == 0);
+                if (fold && !fold_ok) continue;
+                int mt = 0;
+                const size_t tb = top_bytes(s_, mt, fl, fold);
+                if (tb > kLds) continue;
+                any = true;
+                if (forced > 0 && s_ != std::min(forced, N)) continue;
+                const double cost = top_cost + (fl ? 0.0 : 2.0 * s_) - (fold ? s_ : 0) + f[s_];
+                if (cost < best) {
+                    best = cost;
+                    best_s = s_;
+                    c->lds_top = tb;
+                    c->maxch_top = mt;
+                    c->f_lds_top = fl;
+                    c->fold_top = fold;
+                }
             }
-            if (tb > kLds) break;
-            if (forced > 0 && s_ != std::min(forced, N)) continue;
-            const double cost = top_cost + (fl ? 0.0 : 2.0 * s_) + f[s_];
-            if (cost < best) {
-                best = cost;
-                best_s = s_;
-                c->lds_top = tb;
-                c->maxch_top = mt;
-                c->f_lds_top = fl;
-            }
+            if (!any) break;
         }
         c->cut = best_s;
         if (const char* env = getenv("RAOCP_DYN_PER_STAGE"))
@@ -1364,6 +1397,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             tp.lds_b = w.bb;
             tp.lds_f = w.bf;
             tp.fl = w.fl;
+            tp.fold = w.fold;
             std::vector<raocp::Rec> lv;  // level ranges {lo, hi, off} of every subtree of the tier
             for (int r = c->stage_ptr[a]; r < c->stage_ptr[a + 1]; ++r) {
                 int lo = r, hi = r + 1, acc = 0;
@@ -1396,11 +1430,11 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             c->tiers.push_back(tp);
         }
         if (getenv("RAOCP_DYN_VERBOSE")) {
-            fprintf(stderr, "[raocp] dynamics plan: top stages [0,%d) lds %zu F%s", c->cut, c->lds_top,
-                    c->f_lds_top ? "(lds)" : "(global)");
+            fprintf(stderr, "[raocp] dynamics plan: top stages [0,%d) lds %zu F%s%s", c->cut, c->lds_top,
+                    c->f_lds_top ? "(lds)" : "(global)", c->fold_top ? " fold" : "");
             for (const auto& tp : c->tiers)
-                fprintf(stderr, " | tier [%d,%d) x%d lds %zu/%zu F%s", tp.s0, tp.s1, tp.nsub, tp.lds_b, tp.lds_f,
-                        tp.fl ? "(lds)" : "(global)");
+                fprintf(stderr, " | tier [%d,%d) x%d lds %zu/%zu F%s%s", tp.s0, tp.s1, tp.nsub, tp.lds_b, tp.lds_f,
+                        tp.fl ? "(lds)" : "(global)", tp.fold ? " fold" : "");
             fprintf(stderr, "\n");
         }
     }
@@ -1570,6 +1604,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         c->ells_tb = cdiv(c->ells_t.nQ + c->ells_t.nR + c->ells_t.nP + c->ells_t.ncopy, 4);
         if (const char* e = getenv("RAOCP_ELL_STREAM")) c->ells_on = atoi(e) != 0;
     }
+    c->dev.dyn_regtab = 0;  // RAOCP_DYN_REGTAB=1: dynamics tables by vector loads instead of LDS-DMA
+    if (const char* e = getenv("RAOCP_DYN_REGTAB")) c->dev.dyn_regtab = atoi(e) != 0;
     c->dev.regstage = 0;  // RAOCP_REGSTAGE=1: k_ell's gather by vector loads (measured slower)
     if (const char* e = getenv("RAOCP_REGSTAGE")) c->dev.regstage = atoi(e) != 0;
     if ((rc = c->alloc(&c->ticket, 64))) return bail(rc);

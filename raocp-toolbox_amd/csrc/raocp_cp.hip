@@ -31,8 +31,8 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ double s_x[kBlock];
     __shared__ double s_red[2][kBlock / 64];
-    const int done = ctl->done;
-    const double alpha = ctl->alpha;
+    int done;      // read once the staging loads are in flight (ctl_done, raocp_dyn.hip)
+    double alpha;
     const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
     const glbd* pz = (const glbd*)bf.z0;   // p
     const glbd* zp = (const glbd*)bf.z1;   // z+
@@ -81,6 +81,8 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
         const ldsd* SR = st.dbl((const glbd*)p.SR, nR);
         const ldsd* BL = st.dbl((const glbd*)p.blo_nl, nBx);
         const ldsd* BH = st.dbl((const glbd*)p.bhi_nl, nBx);
+        done = ctl->done;
+        alpha = ctl->alpha;
         dma_wait();
         lds_sync();
         if (done) return;
@@ -213,6 +215,8 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
         const ldsd* SP = st.dbl((const glbd*)p.SP, nP);
         const ldsd* BL = st.dbl((const glbd*)p.blo_l, nBx);
         const ldsd* BH = st.dbl((const glbd*)p.bhi_l, nBx);
+        done = ctl->done;
+        alpha = ctl->alpha;
         dma_wait();
         lds_sync();
         if (done) return;
@@ -330,8 +334,8 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ double s_x[kBlock];
     __shared__ double s_red[4][kBlock / 64];
-    const int done = ctl->done;
-    const double alpha = ctl->alpha;
+    int done;      // read once the staging loads are in flight (ctl_done, raocp_dyn.hip)
+    double alpha;
     const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
     const glbd* pz = (const glbd*)bf.z0;   // p_prev
     const glbd* zp = (const glbd*)bf.z1;   // z+ (also where the half step starts)
@@ -390,6 +394,8 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
         const ldsd* SQ = st.dbl((const glbd*)p.SQ, nQ);
         const ldsd* SR = st.dbl((const glbd*)p.SR, nR);
         stamp(p, 1);
+        done = ctl->done;
+        alpha = ctl->alpha;
         dma_wait();
         lds_sync();
         stamp(p, 2);
@@ -552,6 +558,8 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
         const ldsrec* LR = st.rec(p.lrec + (l0 - p.m), Lc);
         const int nP = p.nSP * nx * nx;
         const ldsd* SP = st.dbl((const glbd*)p.SP, nP);
+        done = ctl->done;
+        alpha = ctl->alpha;
         dma_wait();
         lds_sync();
         if (done) return;

@@ -84,6 +84,28 @@ __device__ __forceinline__ double dot_slice(PM m, PV v, int kc) {
             s1 = fma(a.y, b.y, s1);
         }
         return s0 + s1;
+    } else if constexpr (KC > 12) {
+        // long slices (KS = 1 on wide levels) in batches of 8 doubles: loading a whole
+        // 24 / 32-element slice of matrix and vector at once needs 2 KC VGPRs, which at 1024
+        // threads (128 VGPRs) spilled the whole kernel to scratch
+        double s0 = 0.0, s1 = 0.0;
+        _Pragma("unroll") for (int k0 = 0; k0 < KC; k0 += 8) {
+            constexpr int B = 4;
+            d2v a[B], b[B];
+            _Pragma("unroll") for (int t = 0; t < B; ++t) {
+                if (k0 + 2 * t < KC) {
+                    a[t] = ld2(m + k0 + 2 * t);
+                    b[t] = ld2(v + k0 + 2 * t);
+                }
+            }
+            _Pragma("unroll") for (int t = 0; t < B; ++t) {
+                if (k0 + 2 * t < KC) {
+                    s0 = fma(a[t].x, b[t].x, s0);
+                    s1 = fma(a[t].y, b[t].y, s1);
+                }
+            }
+        }
+        return s0 + s1;
     } else {
         d2v a[KC / 2], b[KC / 2];
         _Pragma("unroll") for (int t = 0; t < KC / 2; ++t) {
@@ -244,6 +266,58 @@ __device__ __forceinline__ void back_phase_b(const Dev& p, const TB& tb, const I
             }
         }
     }
+}
+
+// ---- backward level in ONE phase (phases A and B folded) ------------------------------
+// With the per-pair table WT_j = [-Rinv B_j' ; A_j' - G B_j'] (host) the level is
+//     out = RG u_i + sign * sum_j WT_j q_j ;  d_i = out[0:nu] ,  q_i = -x_i + out[nu:]
+// (the same algebra as phases A + B, re-associated): every output row is one split-k dot
+// over the node's children and its own u, so a level costs one barrier instead of two and
+// no P rows go through LDS. tb.W = WT (pairs rebased by tb.p0), tb.RG = RG (classes by c0).
+template <int KS, int NXc, int NUc, class TB, class INF, class QI, class XI, class UI, class QO, class DO>
+__device__ __forceinline__ void back_fold_ks(const Dev& p, const TB& tb, const INF& inf, int b, int e, QI qin,
+                                             double sign, XI xin, UI uin, QO qout, DO dout, int tid, int nthr) {
+    const Geo<NXc, NUc> g(p);
+    constexpr int cKC = Geo<NXc, NUc>::cKP / KS;
+    const int KC = g.KP / KS;
+    const int per = g.R * KS;
+    const int slots = nthr / per;
+    const int slot = tid / per, rem = tid - slot * per, t = rem / KS, sl = rem - t * KS;
+    for (int first = b; first < e; first += slots) {
+        const int i = first + slot;
+        if (slot < slots && i < e) {
+            const Rec ni = inf.nonleaf(i);
+            double acc = 0.0;
+            for (int q = 0; q < ni.y; ++q) {
+                const int j = ni.x + q;
+                const Rec cj = inf.child(j);
+                const auto w = tb.W + ((size_t)(cj.y - tb.p0) * g.R + t) * g.SKP + sl * KC;
+                acc += dot_slice<cKC>(w, qin(j) + sl * KC, KC);
+            }
+            acc *= sign;
+            const auto rg = tb.RG + ((size_t)(ni.z - tb.c0) * g.R + t) * g.SNU;
+            const auto u = uin(i);
+            for (int k = 2 * sl; k < g.NUP; k += 2 * KS) {
+                const d2v m = ld2(rg + k), v = ld2(u + k);
+                acc = fma(m.x, v.x, acc);
+                acc = fma(m.y, v.y, acc);
+            }
+            acc = ks_reduce<KS>(acc);
+            if (sl == 0) {
+                if (t < g.nu) dout(i)[t] = acc;
+                else qout(i)[t - g.nu] = -xin(i)[t - g.nu] + acc;
+            }
+        }
+    }
+}
+
+template <int NXc, int NUc, class TB, class INF, class QI, class XI, class UI, class QO, class DO>
+__device__ __forceinline__ void back_fold(const Dev& p, const TB& tb, const INF& inf, int b, int e, QI qin,
+                                          double sign, XI xin, UI uin, QO qout, DO dout, int tid, int nthr) {
+    const int items = (e - b) * (NXc ? NXc + NUc : p.nx + p.nu);
+    if (items * 4 <= nthr) back_fold_ks<4, NXc, NUc>(p, tb, inf, b, e, qin, sign, xin, uin, qout, dout, tid, nthr);
+    else if (items * 2 <= nthr) back_fold_ks<2, NXc, NUc>(p, tb, inf, b, e, qin, sign, xin, uin, qout, dout, tid, nthr);
+    else back_fold_ks<1, NXc, NUc>(p, tb, inf, b, e, qin, sign, xin, uin, qout, dout, tid, nthr);
 }
 
 // ---- forward: u_i = K x_i + d_i (nodes [b, e)), x_j = F [x_i; d_i] (their children) ---
@@ -470,7 +544,53 @@ __device__ __forceinline__ void dma_rows(ldsd* dst, int w, const double* src, in
         return c < cc ? src + (size_t)r * sstride + 2 * c : zp;
     });
 }
+// Matrix tables by vector loads instead of LDS-DMA (Dev::dyn_regtab): up to four regions
+// (n[k] doubles, even, 16-B aligned) copied in one pass — every thread issues all its
+// 16-B loads first, then writes them to LDS, so the regions cost one memory round trip
+// and no LDS-DMA issue slots (the tables are the same for every workgroup of a launch).
+struct TabCopy {
+    // four fixed slots (dynamically indexed arrays would live in scratch). Region bases are
+    // pre-shifted by the region's first chunk, so chunk c of the concatenation is
+    // base + 2 c for the region holding it.
+    ldsd *d0 = nullptr, *d1 = nullptr, *d2 = nullptr, *d3 = nullptr;
+    const glbd *s0 = nullptr, *s1 = nullptr, *s2 = nullptr, *s3 = nullptr;
+    int e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // cumulative chunk ends
+    int cnt = 0;
+    __device__ __forceinline__ void add(ldsd* d, const double* src, int nd) {
+        const int beg = e3, end = e3 + (nd >> 1);
+        const glbd* sg = (const glbd*)src - 2 * beg;
+        ldsd* dg = d - 2 * beg;
+        if (cnt == 0) { d0 = dg; s0 = sg; e0 = e1 = e2 = e3 = end; }
+        else if (cnt == 1) { d1 = dg; s1 = sg; e1 = e2 = e3 = end; }
+        else if (cnt == 2) { d2 = dg; s2 = sg; e2 = e3 = end; }
+        else { d3 = dg; s3 = sg; e3 = end; }
+        ++cnt;
+    }
+    __device__ __forceinline__ void run() const {
+        constexpr int U = 8;
+        const int tid = threadIdx.x, nthr = blockDim.x;
+        for (int base = 0; base < e3; base += U * nthr) {
+            d2v v[U];
+            _Pragma("unroll") for (int u = 0; u < U; ++u) {
+                const int c = base + u * nthr + tid;
+                const glbd* sp = c < e0 ? s0 : (c < e1 ? s1 : (c < e2 ? s2 : s3));
+                if (c < e3) v[u] = ld2(sp + 2 * c);
+            }
+            _Pragma("unroll") for (int u = 0; u < U; ++u) {
+                const int c = base + u * nthr + tid;
+                ldsd* dp = c < e0 ? d0 : (c < e1 ? d1 : (c < e2 ? d2 : d3));
+                if (c < e3) *(lds2*)(dp + 2 * c) = v[u];
+            }
+        }
+    }
+};
+
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// The CP stop flag, read by a kernel AFTER it has issued its prologue loads: the flag was
+// written by the previous launch (another XCD's L2), so the load costs a memory round trip,
+// and a scalar load is waited for where its value is first needed — at the top of the
+// kernel, that wait serialised the round trip ahead of the whole prologue.
+__device__ __forceinline__ int ctl_done(const Ctl* ctl) { return ctl ? ctl->done : 0; }
 
 // register path for odd sizes / unaligned rows (same result as dma_rows; used only when
 // nx or nu is odd)
@@ -528,16 +648,16 @@ struct TabSize {
 // LDS plan (doubles from the dynamic base), tier backward:
 //   [W (all kinds) | RG (classes c0..c1) | XQ rows (all subtree nodes, KP) | U rows (nonleaf, NUP)
 //    | P rows (maxch, PS) | NL records | CH records]
+// FOLD (one-phase levels): W -> WT (pairs p0..p1), no P rows.
 // The boundary level (s1) holds the leaves' x (q = -x) or q of the next tier's roots.
-template <int NXc, int NUc>
+template <int NXc, int NUc, bool FOLD>
 __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
                                                                 double* qbuf_, double* dbuf_, int s, int s1, int maxch,
-                                                                int c0, int c1, const Rec* __restrict__ sub_lv,
-                                                                TierArg ta) {
+                                                                int c0, int c1, int p0, int p1,
+                                                                const Rec* __restrict__ sub_lv, TierArg ta) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
     tstamp(p, pl, 0);
-    const int done = ctl ? ctl->done : 0;
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
     const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
@@ -545,9 +665,14 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     ldsd* smem = (ldsd*)smem_;
     const int L = s1 - s;
     const bool leaves = s1 == p.N;
-    const int oW = 0, oRG = oW + p.nkind * ts.W1, oXQ = oRG + (c1 - c0) * ts.RG1;
-    dma(smem + oW, p.dW, p.nkind * ts.W1);
-    dma(smem + oRG, p.dRG + (size_t)c0 * ts.RG1, (c1 - c0) * ts.RG1);
+    const int nW = FOLD ? (p1 - p0) * ts.W1 : p.nkind * ts.W1;
+    const int oW = 0, oRG = oW + nW, oXQ = oRG + (c1 - c0) * ts.RG1;
+    const double* srcW = FOLD ? p.dWT + (size_t)p0 * ts.W1 : p.dW;
+    const double* srcRG = p.dRG + (size_t)c0 * ts.RG1;
+    if (!p.dyn_regtab) {
+        dma(smem + oW, srcW, nW);
+        dma(smem + oRG, srcRG, (c1 - c0) * ts.RG1);
+    }
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
     lds_sync();
@@ -556,7 +681,7 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     ldsd* XQ = smem + oXQ;
     ldsd* U = XQ + (size_t)nall * g.KP;
     ldsd* PB = U + (size_t)nnl * g.NUP;
-    ldsd* NLd = PB + rup(maxch * g.PS, 2);
+    ldsd* NLd = PB + (FOLD ? 0 : rup(maxch * g.PS, 2));
     ldsd* CHd = NLd + 2 * nnl;
     for (int l = 0; l <= L; ++l) {
         const int cnt = pl.hi[l] - pl.lo[l];
@@ -572,7 +697,14 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
         }
         if (l > 0) dma(CHd + 2 * (pl.off[l] - 1), (const double*)(p.cinfo + pl.lo[l]), 2 * cnt);
     }
-    zero_fill(PB, maxch * g.PS, tid, nthr);
+    if (!FOLD) zero_fill(PB, maxch * g.PS, tid, nthr);
+    if (p.dyn_regtab) {
+        TabCopy tc;
+        tc.add(smem + oW, srcW, nW);
+        tc.add(smem + oRG, srcRG, (c1 - c0) * ts.RG1);
+        tc.run();
+    }
+    const int done = ctl_done(ctl);
     dma_wait();
     lds_sync();
     tstamp(p, pl, 2);
@@ -580,18 +712,30 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     tstamp(p, pl, 3);
     const ldsrec* NL = (const ldsrec*)NLd;
     const ldsrec* CH = (const ldsrec*)CHd;
-    const TabsT<const ldsd*, const ldsd*> tb{smem + oW, smem + oRG, nullptr, nullptr, c0, 0};
+    const TabsT<const ldsd*, const ldsd*> tb{smem + oW, smem + oRG, nullptr, nullptr, c0, FOLD ? p0 : 0};
     const GRows dg{(glbd*)dbuf_, 0, g.nu};
     for (int l = L - 1; l >= 0; --l) {
         const InfoT<const ldsrec*> inf{NL + pl.off[l], pl.lo[l], CH + pl.off[l + 1] - 1, pl.lo[l + 1]};
         const LRows xq_l{XQ + (size_t)pl.off[l] * g.KP, pl.lo[l], g.KP};
         const LRows xq_c{XQ + (size_t)pl.off[l + 1] * g.KP, pl.lo[l + 1], g.KP};
+        const LRows ur{U + (size_t)pl.off[l] * g.NUP, pl.lo[l], g.NUP};
+        if constexpr (FOLD) {
+            const double sign = (l + 1 == L && leaves) ? -1.0 : 1.0;
+            if (l > 0) {
+                back_fold<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], xq_c, sign, xq_l, ur, xq_l, dg, tid, nthr);
+            } else {
+                const GRows qroot{(glbd*)qbuf_, 0, g.KP};
+                back_fold<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], xq_c, sign, xq_l, ur, qroot, dg, tid, nthr);
+            }
+            lds_sync();
+            tstamp(p, pl, 4 + 2 * (L - 1 - l));
+            continue;
+        }
         const LRows pr{PB, pl.lo[l + 1], g.PS};
         back_phase_a<NXc, NUc>(p, tb, inf, pl.lo[l + 1], pl.hi[l + 1], xq_c, (l + 1 == L && leaves) ? -1.0 : 1.0, pr,
                                tid, nthr);
         lds_sync();
         tstamp(p, pl, 4 + 2 * (L - 1 - l));
-        const LRows ur{U + (size_t)pl.off[l] * g.NUP, pl.lo[l], g.NUP};
         if (l > 0) {
             back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, xq_l, dg, tid, nthr);
         } else {
@@ -614,7 +758,6 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
     tstamp(p, pl, 0);
-    const int done = ctl ? ctl->done : 0;
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
     const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
@@ -622,8 +765,10 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     ldsd* smem = (ldsd*)smem_;
     const int L = s1 - s;
     const int oKM = 0, oF = oKM + (c1 - c0) * ts.KM1, oXD = oF + (FL ? (p1 - p0) * ts.F1 : 0);
-    dma(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1);
-    if (FL) dma(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
+    if (!p.dyn_regtab) {
+        dma(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1);
+        if (FL) dma(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
+    }
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
     lds_sync();
@@ -661,6 +806,13 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
         const int cc = pl.hi[l + 1] - pl.lo[l + 1];
         dma(CHd + 2 * (pl.off[l + 1] - 1), (const double*)(p.cinfo + pl.lo[l + 1]), 2 * cc);
     }
+    if (p.dyn_regtab) {
+        TabCopy tc;
+        tc.add(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1);
+        if (FL) tc.add(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
+        tc.run();
+    }
+    const int done = ctl_done(ctl);
     dma_wait();
     lds_sync();
     tstamp(p, pl, 2);
@@ -689,40 +841,51 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
 // the top of the tree (stages < s, nodes 0..T-1) in one workgroup, backward then forward:
 //   [W | RG | KM | F (if FL) | XQ (T, KP) | QB (boundary, KP) | U (T, NUP) | XD (T, KF) |
 //    P (maxch, PS) | NL (T) | CH (T + nb - 1)]
-template <int NXc, int NUc, bool FL>
+// FOLD (one-phase backward levels): W -> WT (pairs 0..p1), no P rows.
+template <int NXc, int NUc, bool FL, bool FOLD>
 __global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
                                                         const double* qbuf_, const double* x0_, int s, int maxch,
                                                         int c1, int p1, int T, int nb) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
     tstamp(p, pl, 0);
-    const int done = ctl ? ctl->done : 0;
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
     const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
     const int tid = threadIdx.x, nthr = blockDim.x;
     ldsd* smem = (ldsd*)smem_;
     const bool leaves = s == p.N;
-    const int oW = 0, oRG = oW + p.nkind * ts.W1, oKM = oRG + c1 * ts.RG1, oF = oKM + c1 * ts.KM1;
+    const int nW = FOLD ? p1 * ts.W1 : p.nkind * ts.W1;
+    const int oW = 0, oRG = oW + nW, oKM = oRG + c1 * ts.RG1, oF = oKM + c1 * ts.KM1;
     const int oXQ = oF + (FL ? p1 * ts.F1 : 0), oQB = oXQ + T * g.KP, oU = oQB + nb * g.KP, oXD = oU + T * g.NUP;
-    const int oP = oXD + T * g.KF, oNL = oP + rup(maxch * g.PS, 2), oCH = oNL + 2 * T;
-    dma(smem + oW, p.dW, p.nkind * ts.W1);
-    dma(smem + oRG, p.dRG, c1 * ts.RG1);
-    dma(smem + oKM, p.dKM, c1 * ts.KM1);
-    if (FL) dma(smem + oF, p.dF, p1 * ts.F1);
+    const int oP = oXD + T * g.KF, oNL = oP + (FOLD ? 0 : rup(maxch * g.PS, 2)), oCH = oNL + 2 * T;
+    if (!p.dyn_regtab) {
+        dma(smem + oW, FOLD ? p.dWT : p.dW, nW);
+        dma(smem + oRG, p.dRG, c1 * ts.RG1);
+        dma(smem + oKM, p.dKM, c1 * ts.KM1);
+        if (FL) dma(smem + oF, p.dF, p1 * ts.F1);
+    }
     dma(smem + oNL, (const double*)p.ninfo, 2 * T);
     dma(smem + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1));
     if (tid <= s + 1) pl.sp[tid] = p.stage_ptr[tid];
     glbd* z = dyn_z(bf, zsel, ctl);
     rows_in(dmaok, smem + oXQ, g.KP, (const double*)z + p.X0, g.nx, g.nx, T, p.zpage, tid, nthr);
     if (leaves)
-        rows_in(dmaok, smem + oQB, g.KP, (const double*)z + p.X0 + (size_t)T * g.nx, g.nx, g.nx, nb, p.zpage, tid,
-                nthr);
+        rows_in(dmaok, smem + oQB, g.KP, (const double*)z + p.X0 + (size_t)T * g.nx, g.nx, g.nx, nb, p.zpage, tid, nthr);
     else
         dma(smem + oQB, qbuf_ + (size_t)T * g.KP, nb * g.KP);
     rows_in(dmaok, smem + oU, g.NUP, (const double*)z + p.U0, g.nu, g.nu, T, p.zpage, tid, nthr);
     zero_fill(smem + oXD, T * g.KF, tid, nthr);
-    zero_fill(smem + oP, maxch * g.PS, tid, nthr);
+    if (!FOLD) zero_fill(smem + oP, maxch * g.PS, tid, nthr);
+    if (p.dyn_regtab) {
+        TabCopy tc;
+        tc.add(smem + oW, FOLD ? p.dWT : p.dW, nW);
+        tc.add(smem + oRG, p.dRG, c1 * ts.RG1);
+        tc.add(smem + oKM, p.dKM, c1 * ts.KM1);
+        if (FL) tc.add(smem + oF, p.dF, p1 * ts.F1);
+        tc.run();
+    }
+    const int done = ctl_done(ctl);
     dma_wait();
     lds_sync();
     if (done) return;
@@ -739,6 +902,14 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl
     for (int t = s - 1; t >= 0; --t) {
         const int b = pl.sp[t], e = pl.sp[t + 1];
         const int cb = e, ce = pl.sp[t + 2];
+        if constexpr (FOLD) {
+            const double sign = (t + 1 == s && leaves) ? -1.0 : 1.0;
+            if (t + 1 < s) back_fold<NXc, NUc>(p, tb, inf, b, e, xq, sign, xq, ur, xq, dlds, tid, nthr);
+            else back_fold<NXc, NUc>(p, tb, inf, b, e, qb, sign, xq, ur, xq, dlds, tid, nthr);
+            lds_sync();
+            tstamp(p, pl, 2 + 2 * (s - 1 - t));
+            continue;
+        }
         const LRows pr{smem + oP, cb, g.PS};
         if (t + 1 < s) back_phase_a<NXc, NUc>(p, tb, inf, cb, ce, xq, 1.0, pr, tid, nthr);
         else back_phase_a<NXc, NUc>(p, tb, inf, cb, ce, qb, leaves ? -1.0 : 1.0, pr, tid, nthr);

@@ -76,6 +76,7 @@ struct Dev {
     // dynamics projection (raocp_dyn.hip header): per child kind W = [B'; A'], per class
     // RG = [R~^-1; G] and K, per (kind, parent class) pair F = [Abar | B]; padded rows
     const double* dW; const double* dRG; const double* dKM; const double* dF;
+    const double* dWT;     // per (kind, class) pair: [-Rinv B' ; A' - G B'] (one-phase backward level)
     int nkind;             // number of child kinds (rows of W)
     const double* zpage;   // 16 doubles of zeros (LDS-DMA source of padding)
     const Rec* crec;       // [n] {anc, iSQ, iSR, 0} (node 0: unused) — CP child blocks
@@ -91,6 +92,7 @@ struct Dev {
     int N;                 // last stage
     unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)
     int regstage;          // staging by vector loads + LDS stores instead of LDS-DMA (RAOCP_REGSTAGE)
+    int dyn_regtab;        // dynamics kernels stage their matrix tables by vector loads (RAOCP_DYN_REGTAB)
 };
 
 // diagnostic timestamp (100 MHz constant clock), thread 0 only, when enabled
