@@ -1535,7 +1535,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                                               rec(nc) + dbl(nl * nx) + dbl(nl) + rec(nl));
                 need_t = std::max(need_t, dbl(nc * nx) + dbl(nc * nu) + dbl(e7b - e7a) + dbl(Y) + dbl(np) +
                                               3 * dbl(nc) + rec(np) + rec(nc) + dbl(nl * nx) + dbl(e14b - e14a) +
-                                              2 * dbl(nl) + rec(nl) + nc * (nx + nu) + nl * nx);
+                                              2 * dbl(nl) + rec(nl) + nc * (nx + nu));
             }
             if (std::max(need_l, need_t) * 8 <= 64 * 1024 || B >= Bmax) break;
             B = std::min(Bmax, B * 2);

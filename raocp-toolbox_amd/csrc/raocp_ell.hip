@@ -395,10 +395,10 @@ __global__ void __launch_bounds__(512) k_ell_t(Dev p, const double* __restrict__
     const ldsd* D13 = g.dbl(eg + p.E13 + l0, nl);
     const ldsrec* LR = g.rec(p.lrec + (l0 - p.m), nl);  // {iSP, iBl, e14off, 0}
     g.issue(p.regstage);
-    // products sqrtQ_j eta3_j, sqrtR_j eta4_j (children), sqrtPf_l eta11_l (leaves) in LDS
+    // products sqrtQ_j eta3_j, sqrtR_j eta4_j (children) in LDS, summed per parent below; the
+    // leaves' sqrtPf_l eta11_l (+ eta14_l) go straight from the MFMA tile to x_l
     ldsd* PX = (ldsd*)ell_smem + 2 * g.total;
     ldsd* PU = PX + nc * nx;
-    ldsd* PL = PU + nc * nu;
     const Rec t3 = tb[3];
     FamRun<NXc, NUc> fr(Fam{p.SQ, t3.x, nx, c0, nc, D3}, Fam{p.SR, t3.y, nu, c0, nc, D4},
                         Fam{p.SP, t3.z, nx, l0, nl, D11});
@@ -408,12 +408,16 @@ __global__ void __launch_bounds__(512) k_ell_t(Dev p, const double* __restrict__
     fr.run([&](int j) { return j - c0; }, [&](int j) { return CR[j - c0].y; },
            [&](int j, int r, double v) { PX[(j - c0) * nx + r] = v; }, [&](int j) { return CR[j - c0].z; },
            [&](int j, int r, double v) { PU[(j - c0) * nu + r] = v; }, [&](int l) { return l - l0; },
-           [&](int l) { return LR[l - l0].x; }, [&](int l, int r, double v) { PL[(l - l0) * nx + r] = v; });
+           [&](int l) { return LR[l - l0].x; },
+           [&](int l, int r, double v) {
+               const int o14 = LR[l - l0].z;
+               zg[p.X0 + (size_t)l * nx + r] = o14 >= 0 ? v + D14[o14 - e14a + r] : v;
+           });
     lds_sync();
-    // x_i = [eta7_i]_x + sum_children (sqrtQ_j eta3_j) | u_i likewise | x_l = sqrtPf_l eta11_l
-    // + eta14_l | y = eta1 - b eta2 | s = eta2 | tau | leaf s, as one flat task list
+    // x_i = [eta7_i]_x + sum_children (sqrtQ_j eta3_j) | u_i likewise | y = eta1 - b eta2 |
+    // s = eta2 | tau | leaf s, as one flat task list
     const int G = 2 * p.cmax + 1;
-    const int nA = np * nx, nB = nA + np * nu, nC = nB + nl * nx, nD = nC + np * G, nE = nD + np, nF = nE + nc;
+    const int nA = np * nx, nB = nA + np * nu, nC = nB, nD = nC + np * G, nE = nD + np, nF = nE + nc;
     const int nH = nF + nl;
     for (int t = tid; t < nH; t += nt) {
         if (t < nB) {
@@ -425,12 +429,6 @@ __global__ void __launch_bounds__(512) k_ell_t(Dev p, const double* __restrict__
             for (int j = fr.z; j < fr.z + fr.y; ++j) acc += P[(j - c0) * n + r];
             if (isx) zg[p.X0 + (size_t)(i0 + q) * nx + r] = acc;
             else zg[p.U0 + (size_t)(i0 + q) * nu + r] = acc;
-        } else if (t < nC) {
-            const int e = t - nB, ll = e / nx, r = e - ll * nx;
-            const int o14 = LR[ll].z;
-            double acc = PL[e];
-            if (o14 >= 0) acc += D14[o14 - e14a + r];
-            zg[p.X0 + (size_t)(l0 + ll) * nx + r] = acc;
         } else if (t < nD) {  // y = eta1 - b eta2
             const int e = t - nC, q = e / G, k = e - q * G;
             const Rec fr = FR[q];
