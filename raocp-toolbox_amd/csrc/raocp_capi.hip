@@ -1529,7 +1529,17 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                         if (idx[q] != idx[a]) return -1;
                     return idx[a];
                 };
-                T[3] = raocp::Rec{uni(pr->i_sq, c0, c1), uni(pr->i_sr, c0, c1), uni(pr->i_sp, l0, l1), 0};
+                // regular block (k_ell_t's per-parent MFMA tiles): every parent has the same
+                // child count c <= 4 and its children are c0 + (i - i0) c + [0, c)
+                int creg = 0;
+                if (i1 > i0 && t->nch[i0] >= 1 && t->nch[i0] <= 4) {
+                    creg = t->nch[i0];
+                    for (int q = i0; q < i1 && creg; ++q)
+                        if (t->nch[q] != creg || t->ch_start[q] != c0 + (q - i0) * creg) creg = 0;
+                }
+                if (const char* e = getenv("RAOCP_ELLT_PARENT_TILES"))
+                    if (e[0] == '0') creg = 0;
+                T[3] = raocp::Rec{uni(pr->i_sq, c0, c1), uni(pr->i_sr, c0, c1), uni(pr->i_sp, l0, l1), creg};
                 const long np = i1 - i0, nc = c1 - c0, nl = l1 - l0, Y = y1 - y0;
                 need_l = std::max(need_l, dbl(np * nx) + dbl(np * nu) + dbl(Y) + dbl(np) + 2 * dbl(nc) + rec(np) +
                                               rec(nc) + dbl(nl * nx) + dbl(nl) + rec(nl));

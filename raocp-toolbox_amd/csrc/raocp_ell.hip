@@ -209,6 +209,17 @@ struct WFrag {
             b[s] = (r < n && k < n) ? M[k * n + r] : 0.0;
         }
     }
+    // one tile whose A-row of this lane is va (live) or zero
+    __device__ __forceinline__ d4 tile_at(const ldsd* va, int n, bool live) const {
+        const int hi = (threadIdx.x & 63) >> 4;
+        d4 acc = {0.0, 0.0, 0.0, 0.0};
+        _Pragma("unroll") for (int s = 0; s < KS; ++s) {
+            const int k = 4 * s + hi;
+            const double a = (live && k < n) ? va[k] : 0.0;
+            acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b[s], acc, 0, 0, 0);
+        }
+        return acc;
+    }
     // one 16-node tile: A from LDS rows src + slot(node) n
     template <class SlotF>
     __device__ __forceinline__ d4 tile(const ldsd* src, int n, int first, int cnt, SlotF slot) const {
@@ -250,6 +261,42 @@ __device__ __forceinline__ void fam_tiles(const Fam& F, const WFrag<NC>& wf, int
     }
 }
 
+// Per-parent tiles (k_ell_t on a regular block: C children per parent, children of block
+// parent p at rows p C + [0, C) of F.src). MFMA result element e of lane group h is A-row
+// h + 4e, so A-row h + 4e is given child e % C of parent h + 4 (e / C): the C products of
+// one parent land in one lane, which sums them in child order after base(p, r) and stores
+// the parent row with put(p, r, sum). A tile covers 4 (4 / C) parents.
+template <int C, int NC, class BaseF, class PutF>
+__device__ __forceinline__ void par_tiles_c(const Fam& F, const WFrag<NC>& wf, int r0, int part, int P, int np,
+                                            BaseF base, PutF put) {
+    constexpr int Q = 4 / C, PT = 4 * Q;
+    const int l = threadIdx.x & 63, lo = l & 15, hi = l >> 4, r = r0 + lo;
+    const int hA = lo & 3, eA = lo >> 2, pA = hA + 4 * (eA / C), kA = eA % C;
+    for (int ti = part; ti * PT < np; ti += P) {
+        const int pb = ti * PT;
+        const bool live = eA < Q * C && pb + pA < np;
+        const d4 d = wf.tile_at(F.src + (live ? (pb + pA) * C + kA : 0) * F.n, F.n, live);
+        _Pragma("unroll") for (int s = 0; s < Q; ++s) {
+            const int pp = pb + hi + 4 * s;
+            if (pp < np && r < F.n) {
+                double acc = base(pp, r);
+                _Pragma("unroll") for (int k = 0; k < C; ++k) acc += d[s * C + k];
+                put(pp, r, acc);
+            }
+        }
+    }
+}
+template <int NC, class BaseF, class PutF>
+__device__ __forceinline__ void par_tiles(int c, const Fam& F, const WFrag<NC>& wf, int r0, int part, int P, int np,
+                                          BaseF base, PutF put) {
+    switch (c) {
+        case 1: par_tiles_c<1, NC>(F, wf, r0, part, P, np, base, put); break;
+        case 2: par_tiles_c<2, NC>(F, wf, r0, part, P, np, base, put); break;
+        case 3: par_tiles_c<3, NC>(F, wf, r0, part, P, np, base, put); break;
+        default: par_tiles_c<4, NC>(F, wf, r0, part, P, np, base, put); break;
+    }
+}
+
 // the three product families of L / L^T: 0 = Q rows over the children, 1 = R rows over
 // the children, 2 = Pf rows over the leaves. Waves split the (family, row tile) streams;
 // prefetch() loads the first stream's weight fragments (call before the gather wait),
@@ -279,6 +326,19 @@ struct FamRun {
     }
     __device__ __forceinline__ void prefetch() {
         if (w < S * P) frag(w % S);
+    }
+    // k_ell_t on a regular block: families 0 / 1 as per-parent tiles (par_tiles), family 2
+    // as node tiles
+    template <class Base0, class PPut0, class Base1, class PPut1, class Slot2, class Tab2, class Put2>
+    __device__ __forceinline__ void run_par(int c, int np, Base0 b0, PPut0 q0, Base1 b1, PPut1 q1, Slot2 s2, Tab2 t2,
+                                            Put2 p2) {
+        for (int item = w; item < S * P; item += W) {
+            const int st = item % S, part = item / S;
+            if (item != w) frag(st);
+            if (st < S0) par_tiles<NXc>(c, F0, f0, 16 * st, part, P, np, b0, q0);
+            else if (st < S1) par_tiles<NUc>(c, F1, f1, 16 * (st - S0), part, P, np, b1, q1);
+            else fam_tiles<NXc>(F2, f2, 16 * (st - S1), part, P, s2, t2, p2);
+        }
     }
     template <class Slot0, class Tab0, class Put0, class Tab1, class Put1, class Slot2, class Tab2, class Put2>
     __device__ __forceinline__ void run(Slot0 s0, Tab0 t0, Put0 p0, Tab1 t1, Put1 p1, Slot2 s2, Tab2 t2, Put2 p2) {
@@ -405,19 +465,39 @@ __global__ void __launch_bounds__(512) k_ell_t(Dev p, const double* __restrict__
     fr.prefetch();
     dma_wait();
     lds_sync();
-    fr.run([&](int j) { return j - c0; }, [&](int j) { return CR[j - c0].y; },
-           [&](int j, int r, double v) { PX[(j - c0) * nx + r] = v; }, [&](int j) { return CR[j - c0].z; },
-           [&](int j, int r, double v) { PU[(j - c0) * nu + r] = v; }, [&](int l) { return l - l0; },
-           [&](int l) { return LR[l - l0].x; },
-           [&](int l, int r, double v) {
-               const int o14 = LR[l - l0].z;
-               zg[p.X0 + (size_t)l * nx + r] = o14 >= 0 ? v + D14[o14 - e14a + r] : v;
-           });
-    lds_sync();
-    // x_i = [eta7_i]_x + sum_children (sqrtQ_j eta3_j) | u_i likewise | y = eta1 - b eta2 |
-    // s = eta2 | tau | leaf s, as one flat task list
+    auto leaf_put = [&](int l, int r, double v) {
+        const int o14 = LR[l - l0].z;
+        zg[p.X0 + (size_t)l * nx + r] = o14 >= 0 ? v + D14[o14 - e14a + r] : v;
+    };
+    // regular block with uniform Q / R tables: the parents' x, u rows come straight out of
+    // the per-parent MFMA tiles (no product staging, no second barrier)
+    const bool par = t3.w > 0 && t3.x >= 0 && t3.y >= 0;
+    if (par) {
+        fr.run_par(
+            t3.w, np,
+            [&](int q, int r) {
+                const int o7 = FR[q].w;
+                return o7 >= 0 ? D7[o7 - e7a + r] : 0.0;
+            },
+            [&](int q, int r, double v) { zg[p.X0 + (size_t)(i0 + q) * nx + r] = v; },
+            [&](int q, int r) {
+                const int o7 = FR[q].w;
+                return o7 >= 0 ? D7[o7 - e7a + nx + r] : 0.0;
+            },
+            [&](int q, int r, double v) { zg[p.U0 + (size_t)(i0 + q) * nu + r] = v; }, [&](int l) { return l - l0; },
+            [&](int l) { return LR[l - l0].x; }, leaf_put);
+    } else {
+        fr.run([&](int j) { return j - c0; }, [&](int j) { return CR[j - c0].y; },
+               [&](int j, int r, double v) { PX[(j - c0) * nx + r] = v; }, [&](int j) { return CR[j - c0].z; },
+               [&](int j, int r, double v) { PU[(j - c0) * nu + r] = v; }, [&](int l) { return l - l0; },
+               [&](int l) { return LR[l - l0].x; }, leaf_put);
+        lds_sync();
+    }
+    // x_i = [eta7_i]_x + sum_children (sqrtQ_j eta3_j) | u_i likewise (unless done above) |
+    // y = eta1 - b eta2 | s = eta2 | tau | leaf s, as one flat task list
     const int G = 2 * p.cmax + 1;
-    const int nA = np * nx, nB = nA + np * nu, nC = nB, nD = nC + np * G, nE = nD + np, nF = nE + nc;
+    const int nA = par ? 0 : np * nx, nB = par ? 0 : nA + np * nu, nC = nB, nD = nC + np * G, nE = nD + np,
+              nF = nE + nc;
     const int nH = nF + nl;
     for (int t = tid; t < nH; t += nt) {
         if (t < nB) {
