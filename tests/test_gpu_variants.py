@@ -1,6 +1,7 @@
 """GPU parity of the opt-in kernel variants (measured slower on MI355X than the defaults,
 kept correct): L / L^T as streaming wave-task kernels (raocp_ells.hip, RAOCP_ELL_STREAM=1)
-and the CP stopping test fused into k_cpp's last block (RAOCP_FUSE_CHECK=1).
+and the CP stopping test fused into k_cpp's last block (RAOCP_FUSE_CHECK=1); and the
+default per-parent L^T tiles against the LDS-staged path (RAOCP_ELLT_PARENT_TILES=0).
 
 Tolerances as in test_gpu_parity.py.
 """
@@ -87,3 +88,23 @@ def test_fused_stopping_test_main_py(golden):
     assert status == 0 and solver.error_cache.shape == (937, 3)
     assert trace_rel_err(solver.error_cache, z["main/cp_error"]) <= 1e-8
     assert rel_err(solver.cache.get_primal_flat(), z["main/cp_z"]) <= 1e-9
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, "4-modes"])
+def test_ell_t_parent_tiles_bit_identical_to_staged(cfg):
+    """k_ell_t's per-parent MFMA tiles (regular blocks, default) against the LDS-staged
+    product path (RAOCP_ELLT_PARENT_TILES=0): the children are summed in the same order, so
+    the results are bit-identical; both match the oracle. Config 4-modes mixes weight tables
+    (the staged path is taken there either way)."""
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(4 if cfg == "4-modes" else cfg)
+    if cfg == "4-modes":
+        r["Q"] = np.array([(1.0 + k) * q for k, q in enumerate(r["Q"])])
+    tree, prob = build_problem(r)
+    tiles = core.Cache(prob)
+    staged = _with_env({"RAOCP_ELLT_PARENT_TILES": "0"}, lambda: core.Cache(prob))
+    rng = np.random.default_rng(11)
+    ee = rng.standard_normal(tiles.dual_size)
+    a, b = tiles.native.ell_t(ee), staged.native.ell_t(ee)
+    assert np.array_equal(a, b)
+    assert rel_err(a, OracleProblem(prob).ell_t(ee)) <= 1e-12
