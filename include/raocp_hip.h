@@ -142,7 +142,10 @@ int raocp_dual_moreau(raocp_ctx* ctx, double alpha, const double* modified);
 int raocp_step_size(raocp_ctx* ctx, double* lambda_max, int max_it, double rtol);
 
 /* The whole Chambolle–Pock loop (Solver.chock, solver.py:97-171) on the device.
- * Starts from primal = (x0 at node 0, zeros) and dual = 0, runs until
+ * Starts from the context's current primal / dual (raocp_set_primal / raocp_set_dual;
+ * both zero after raocp_ctx_create) with x0 written into node 0's state, as the
+ * reference's chock continues from the cache's old primal / dual (solver.py:27-61,
+ * cache.py:79-82, 186-196); runs until
  * k >= max_iters or max(error) <= tol, like the reference. Outputs:
  *   status    0 converged (k < max_iters) / 1 not converged (solver.py:166-169)
  *   iters     number of iterations run (rows of the error caches)
@@ -151,18 +154,12 @@ int raocp_step_size(raocp_ctx* ctx, double* lambda_max, int max_it, double rtol)
 int raocp_cp_run(raocp_ctx* ctx, const double* x0, int max_iters, double tol, double alpha,
                  int* status, int* iters, double* err_hist, double* delta_hist);
 
-/* Which CP driver raocp_cp_run / raocp_cp_bench use on this context: the persistent
- * engine (ONE launch per solve; *cut = its cut stage s > 0, *workgroups = 1 + #stage-s
- * subtrees) or the graph-replayed multi-kernel iteration (*cut = 0). The engine is
- * opt-in (RAOCP_MEGA=1 at context creation) and planned when the tree fits it;
- * RAOCP_MEGA_CUT=s forces a cut stage. *dyn_cut > 0: inside the graph-replayed
- * iteration each dynamics projection is ONE launch of the dynamics-only engine cut at
- * that stage (RAOCP_DYN_ENGINE=1, RAOCP_DYN_ENGINE_CUT=s) instead of one launch per tier. */
-int raocp_engine_info(raocp_ctx* ctx, int* cut, int* workgroups, int* dyn_cut);
-
-/* Benchmark helpers (bench.py): run exactly `iters` CP iterations (tol = 0) on the
- * device (one persistent launch, or graph-replayed), without host syncs inside;
- * returns device ms. */
+/* Benchmark helpers (bench.py): raocp_cp_bench runs exactly `iters` CP iterations
+ * (tol = 0) from (x0 at node 0, zeros) / 0 on the device, graph-replayed (whole
+ * batches of 24 iterations, then one remainder batch), without host syncs inside;
+ * returns device ms. raocp_cp_prepare captures the graphs a run of `iters` iterations
+ * uses, so the timed call launches them without capturing. */
+int raocp_cp_prepare(raocp_ctx* ctx, int iters);
 int raocp_cp_bench(raocp_ctx* ctx, const double* x0, int iters, double alpha, float* ms);
 /* Time `reps` back-to-back launches of L (op=0) or L^T (op=1) on device-resident
  * vectors with HIP events on the context's stream; returns average ms per launch. */

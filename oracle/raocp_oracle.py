@@ -538,12 +538,17 @@ class OracleProblem:
         derr = np.array([np.max(np.abs(v), initial=0.0) for v in (dl0, dl1, dl2)])
         return zp, ep, err, derr
 
-    def chock(self, x0, max_iters=10, tol=1e-5, alpha=None):
-        """solver.py:97-171. Returns (status, error_cache (k x 3), delta_error_cache, z, eta, alpha)."""
+    def chock(self, x0, max_iters=10, tol=1e-5, alpha=None, p0=None, d0=None):
+        """solver.py:97-171. Returns (status, error_cache (k x 3), delta_error_cache, z, eta, alpha).
+        p0 / d0: the cached old primal / dual the loop continues from (a second chock on the
+        same Solver, cache.py:58-66, 186-196); x0 overwrites node 0's state (cache.py:79-82)."""
         if alpha is None:
             _, alpha = self.step_size()
         p = self.initial_primal(x0)
-        d = np.zeros(self.D)
+        if p0 is not None:
+            p = np.array(p0, dtype=float, copy=True)
+            p[self.X0:self.X0 + self.nx] = np.asarray(x0, dtype=float).reshape(-1)
+        d = np.zeros(self.D) if d0 is None else np.array(d0, dtype=float, copy=True)
         errs, derrs = [], []
         k = 0
         while True:

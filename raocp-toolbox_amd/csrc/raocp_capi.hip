@@ -122,27 +122,14 @@ struct raocp_ctx {
     int n_ph = 0;
     bool has_x0 = false;
     std::vector<double> h_x0;
-    // persistent CP engine (raocp_mega.hip): one launch per solve when the plan fits
-    bool mega_ok = false;
-    int mega_s = 0, mega_nwg = 0;
-    size_t mega_lds = 0;
-    raocp::MegaArg mega{};
-    // L / L^T as streaming wave tasks (raocp_ells.hip), opt-in RAOCP_ELL_STREAM=1: on MI355X
-    // the node-range block kernels (raocp_ell.hip) are faster at configs 2 and 4
-    bool ells_on = false;
-    raocp::EllsPlan ells_l{}, ells_t{};
-    int ells_lb = 0, ells_tb = 0;
     unsigned* ticket = nullptr;  // k_cpp blocks done (fused stopping test)
     bool no_fuse_check = true;   // RAOCP_FUSE_CHECK=1: the stopping test inside k_cpp's last block
                                  // (measured slower than its own launch: DESIGN.md)
-    // dynamics-only engine (one launch per projection inside the CP graph)
-    bool dyn_ok = false;
-    int dyn_s = 0, dyn_nwg = 0;
-    size_t dyn_lds = 0;
-    raocp::MegaArg dyn{};
     // captured CP iterations
-    hipGraphExec_t graph = nullptr;
+    hipGraphExec_t graph = nullptr;      // kGraphBatch iterations (raocp_cp_run, raocp_cp_bench)
     int graph_iters = 0;
+    hipGraphExec_t graph_rem = nullptr;  // the remainder batch of raocp_cp_bench (exactly K iterations)
+    int graph_rem_iters = 0;
     std::vector<void*> allocs;
 
     template <class T>
@@ -239,10 +226,6 @@ void allow_lds(K kernel, size_t bytes) {
 struct EllOp {
     template <int NX, int NU>
     void run(raocp_ctx* c, const double* z, double* eta) {
-        if (c->ells_on) {  // streaming wave tasks (raocp_ells.hip)
-            raocp::k_ells<NX, NU><<<c->ells_lb, 256, 0, c->stream>>>(c->dev, c->ells_l, z, eta);
-            return;
-        }
         auto k = raocp::k_ell<NX, NU>;
         allow_lds(k, c->ell_lds);
         if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ell_lds, c->stream>>>(c->dev, z, eta);
@@ -253,10 +236,6 @@ void launch_ell(raocp_ctx* c, const double* z, double* eta) { dispatch(c->nx, c-
 struct EllTOp {
     template <int NX, int NU>
     void run(raocp_ctx* c, const double* eta, double* z) {
-        if (c->ells_on) {
-            raocp::k_ellts<NX, NU><<<c->ells_tb, 256, 0, c->stream>>>(c->dev, c->ells_t, eta, z);
-            return;
-        }
         auto k = raocp::k_ell_t<NX, NU>;
         allow_lds(k, c->ellt_lds);
         if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ellt_lds, c->stream>>>(c->dev, eta, z);
@@ -269,18 +248,6 @@ struct DynOp {
     // tiers' forward sweeps (a shard exchanges the roots' q rows in between)
     template <int NX, int NU>
     void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part) {
-        if (c->dyn_ok && part == 0 && ctl && c->sh_R == 1 && !c->comm && !c->dev.stamps) {
-            raocp::MegaArg a = c->dyn;
-            const int w3 = zsel % 3;
-            a.Z[0] = a.Z[1] = a.Z[2] = w3 == 0 ? bf.z0 : (w3 == 1 ? bf.z1 : bf.z2);  // projects Z[1] only
-            a.x0 = c->x0;
-            a.ctl = c->ctl;
-            a.stamps = nullptr;
-            auto k = raocp::k_mega<NX, NU, true>;
-            allow_lds(k, c->dyn_lds);
-            k<<<c->dyn_nwg, raocp::kMegaDynThreads, c->dyn_lds, c->stream>>>(c->dev, a, ctl);
-            return;
-        }
         const int s = c->cut;
         const int B = c->dyn_block;
         // diagnostics: each launch stamps into its own 64-slot region
@@ -513,20 +480,21 @@ int enqueue_shard_iteration(raocp_ctx* c) {
     shard_unpack_x1(c);
     launch_cpp(c);
     raocp::k_cp_reduce<<<1, kBlock, 0, c->stream>>>(c->ctl, c->redpart, c->cp_rows, c->red8);
-    if ((rc = rccl_check(g_rccl.all_reduce(c->red8, c->red8, 8, ncclFloat64, ncclMax, comm, c->stream),
+    if ((rc = rccl_check(g_rccl.all_reduce(c->red8, c->red8, 16, ncclFloat64, ncclMax, comm, c->stream),
                          "ncclAllReduce(max)")))
         return rc;
     raocp::k_cp_check_red<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->red8);
     return RAOCP_OK;
 }
 
-void enqueue_cp_iteration(raocp_ctx* c, int it) {
+// returns the first failure of an RCCL call (launch errors surface at the next sync)
+int enqueue_cp_iteration(raocp_ctx* c, int it) {
     const raocp::Bufs keep = c->bufs;
     c->bufs = rotated(c, it);
     if (c->comm) {
-        (void)enqueue_shard_iteration(c);
+        const int rc = enqueue_shard_iteration(c);
         c->bufs = keep;
-        return;
+        return rc;
     }
     launch_dynamics(c, c->bufs, 1, c->ctl);
     launch_cpd(c);
@@ -534,6 +502,7 @@ void enqueue_cp_iteration(raocp_ctx* c, int it) {
     launch_cpp(c, fuse);
     c->bufs = keep;
     if (!fuse) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
+    return RAOCP_OK;
 }
 
 
@@ -541,6 +510,13 @@ int set_ctl_alpha(raocp_ctx* c, double alpha) {
     HIPCHK(hipMemcpyAsync(&c->ctl->alpha, &alpha, sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return RAOCP_OK;
+}
+
+void drop_graphs(raocp_ctx* c) {
+    if (c->graph) (void)hipGraphExecDestroy(c->graph);
+    if (c->graph_rem) (void)hipGraphExecDestroy(c->graph_rem);
+    c->graph = c->graph_rem = nullptr;
+    c->graph_iters = c->graph_rem_iters = 0;
 }
 
 int ensure_hist(raocp_ctx* c, size_t rows) {
@@ -553,19 +529,27 @@ int ensure_hist(raocp_ctx* c, size_t rows) {
     int rc = c->alloc(&c->hist, rows * 6);
     if (rc) return rc;
     c->hist_rows = rows;
-    // the graph references the history buffer
-    if (c->graph) {
-        (void)hipGraphExecDestroy(c->graph);
-        c->graph = nullptr;
-        c->graph_iters = 0;
-    }
+    drop_graphs(c);  // the graphs reference the history buffer
     return RAOCP_OK;
 }
 
-// Reset the iterate to (x0 at node 0, zeros) / 0 and prepare ctl for a CP run.
-int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double alpha) {
-    for (int b = 0; b < 3; ++b) HIPCHK(hipMemsetAsync(c->Z[b], 0, c->P * sizeof(double), c->stream));
-    for (int b = 0; b < 2; ++b) HIPCHK(hipMemsetAsync(c->E[b], 0, c->D * sizeof(double), c->stream));
+// Prepare a CP run: the starting primal / dual go to Z[0] / E[0] and ctl is reset.
+// warm: start from the context's current primal / dual (the reference's chock continues
+// from the cached old primal / dual, solver.py:27-61 with cache.py:58-66, 186-196), with
+// x0 written into node 0's state (cache_initial_state, cache.py:79-82); otherwise from
+// (x0 at node 0, zeros) / 0.
+int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double alpha, bool warm = false) {
+    if (warm) {
+        if (c->cur_z != c->Z[0])
+            HIPCHK(hipMemcpyAsync(c->Z[0], c->cur_z, c->P * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        if (c->cur_e != c->E[0])
+            HIPCHK(hipMemcpyAsync(c->E[0], c->cur_e, c->D * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    } else {
+        HIPCHK(hipMemsetAsync(c->Z[0], 0, c->P * sizeof(double), c->stream));
+        HIPCHK(hipMemsetAsync(c->E[0], 0, c->D * sizeof(double), c->stream));
+    }
+    for (int b = 1; b < 3; ++b) HIPCHK(hipMemsetAsync(c->Z[b], 0, c->P * sizeof(double), c->stream));
+    HIPCHK(hipMemsetAsync(c->E[1], 0, c->D * sizeof(double), c->stream));
     HIPCHK(hipMemsetAsync(c->XI2, 0, c->D * sizeof(double), c->stream));
     HIPCHK(hipMemcpyAsync(c->Z[0] + c->dev.X0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
     HIPCHK(hipMemcpyAsync(c->x0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
@@ -583,42 +567,61 @@ int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double al
     return RAOCP_OK;
 }
 
+// the captured batch of `iters` CP iterations: kGraphBatch in the main slot, any other
+// count (a benchmark's remainder, always launched after whole batches, so it also starts
+// at k = 0 mod 6) in the remainder slot
 int ensure_graph(raocp_ctx* c, int iters) {
     if (c->eager) return RAOCP_OK;
-    if (c->graph && c->graph_iters == iters) return RAOCP_OK;
-    if (c->graph) {
-        (void)hipGraphExecDestroy(c->graph);
-        c->graph = nullptr;
+    const bool rem = iters != kGraphBatch;
+    hipGraphExec_t& slot = rem ? c->graph_rem : c->graph;
+    int& slot_iters = rem ? c->graph_rem_iters : c->graph_iters;
+    if (slot && slot_iters == iters) return RAOCP_OK;
+    if (slot) {
+        (void)hipGraphExecDestroy(slot);
+        slot = nullptr;
     }
     hipGraph_t g = nullptr;
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
-    for (int it = 0; it < iters; ++it) enqueue_cp_iteration(c, it);
+    int rc_enq = RAOCP_OK;
+    for (int it = 0; it < iters && rc_enq == RAOCP_OK; ++it) rc_enq = enqueue_cp_iteration(c, it);
     hipError_t e = hipStreamEndCapture(c->stream, &g);
+    if (rc_enq != RAOCP_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        if (!c->comm) return rc_enq;
+        // an RCCL shard whose collectives cannot be captured: launch iterations eagerly
+        c->eager = true;
+        if (getenv("RAOCP_VERBOSE")) fprintf(stderr, "[raocp] RCCL capture failed (%s): eager launches\n", g_err.c_str());
+        return RAOCP_OK;
+    }
     if (e == hipSuccess) {
-        e = hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0);
+        e = hipGraphInstantiate(&slot, g, nullptr, nullptr, 0);
         (void)hipGraphDestroy(g);
     }
     if (e != hipSuccess) {
         if (!c->comm) return fail(RAOCP_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
         // an RCCL shard whose collectives cannot be captured: launch iterations eagerly
         (void)hipGetLastError();
-        c->graph = nullptr;
+        slot = nullptr;
         c->eager = true;
         if (getenv("RAOCP_VERBOSE")) fprintf(stderr, "[raocp] RCCL graph capture failed (%s): eager launches\n", hipGetErrorString(e));
         return RAOCP_OK;
     }
-    c->graph_iters = iters;
+    slot_iters = iters;
     return RAOCP_OK;
 }
 
 // launch one batch of `iters` CP iterations (the captured graph, or eagerly)
 int launch_batch(raocp_ctx* c, int iters) {
     if (c->eager) {
-        for (int it = 0; it < iters; ++it) enqueue_cp_iteration(c, it);
+        for (int it = 0; it < iters; ++it) {
+            const int rc = enqueue_cp_iteration(c, it);
+            if (rc) return rc;
+        }
         HIPCHK(hipGetLastError());
         return RAOCP_OK;
     }
-    HIPCHK(hipGraphLaunch(c->graph, c->stream));
+    HIPCHK(hipGraphLaunch(iters == kGraphBatch ? c->graph : c->graph_rem, c->stream));
     return RAOCP_OK;
 }
 
@@ -720,252 +723,22 @@ int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& prange
     return RAOCP_OK;
 }
 
-// ---- persistent CP engine plan (raocp_mega.hip). Cut stage s: workgroup 0 = stages
-// 0..s-1 (level s = the roots, q / x exchanged), workgroup 1+k = the subtree of the k-th
-// stage-s node, levels 0..N-s. The plan exists when every workgroup's LDS fits and the grid
-// (1 + #roots workgroups, one per CU) is co-resident. Opt-in: RAOCP_MEGA=1 (default off);
-// RAOCP_MEGA_CUT=s forces a cut.
-struct EnginePlan {
-    bool ok = false;
-    int s = 0, nwg = 0;
-    size_t lds = 0;
-    raocp::MegaArg a{};
-};
 
-// dyn: the dynamics-only engine (no phase stage, no L tables, 1024 threads)
-int engine_plan(raocp_ctx* c, const raocp_tree_desc* t, bool dyn, EnginePlan* out) {
-    using raocp::kMegaLev;
-    using raocp::Rec;
-    out->ok = false;
-    const int N = c->N, nx = c->nx, nu = c->nu;
-    const int nthreads = dyn ? raocp::kMegaDynThreads : raocp::kMegaThreads;
-    int cus = 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess || cus <= 0)
-        cus = 256;
-    const size_t lds_cap = 160 * 1024 - 4096;  // dynamic LDS budget (static arrays + slack)
-    int forced = -1;
-    if (const char* e = getenv(dyn ? "RAOCP_DYN_ENGINE_CUT" : "RAOCP_MEGA_CUT")) forced = atoi(e);
-    struct Cand {
-        int s = 0;
-        long cost = 0;
-        size_t lds = 0;
-        int maxch = 0, stage_cap = 0;
-        std::vector<Rec> lv;
-        std::vector<int> wl;
-    };
-    Cand best;
-    bool have = false;
-    for (int s = 1; s < N; ++s) {
-        if (forced > 0 && s != forced) continue;
-        const int nsub = c->stage_ptr[s + 1] - c->stage_ptr[s];
-        const int L = N - s;
-        if (s > kMegaLev || L > kMegaLev || nsub + 1 > cus) continue;
-        Cand cd;
-        cd.s = s;
-        const int nwg = 1 + nsub;
-        cd.lv.assign((size_t)nwg * (kMegaLev + 1), Rec{0, 0, 0, 0});
-        cd.wl.assign(nwg, 0);
-        int maxch = 1;
-        long top_nodes = c->stage_ptr[s], sub_max = 0;
-        // top
-        for (int l = 0; l <= s; ++l) {
-            const int lo = c->stage_ptr[l], hi = c->stage_ptr[l + 1];
-            cd.lv[l] = Rec{lo, hi, lo, 0};
-            if (l >= 1) maxch = std::max(maxch, hi - lo);
-        }
-        cd.wl[0] = s;
-        // subtrees
-        bool ok = true;
-        for (int k = 0; k < nsub && ok; ++k) {
-            Rec* lv = cd.lv.data() + (size_t)(1 + k) * (kMegaLev + 1);
-            int lo = c->stage_ptr[s] + k, hi = lo + 1, off = 0;
-            for (int l = 0; l <= L; ++l) {
-                lv[l] = Rec{lo, hi, off, 0};
-                off += hi - lo;
-                if (l >= 1) maxch = std::max(maxch, hi - lo);
-                if (l < L) {
-                    if (lo >= c->m) { ok = false; break; }
-                    const int nlo = t->ch_start[lo], nhi = t->ch_start[hi - 1] + t->nch[hi - 1];
-                    lo = nlo;
-                    hi = nhi;
-                }
-            }
-            sub_max = std::max<long>(sub_max, off);
-            cd.wl[1 + k] = L;
-        }
-        if (!ok) continue;
-        cd.maxch = maxch;
-        // LDS: the stage gets what the largest workgroup leaves of the budget; it must hold
-        // the operands of any single level of the dual / primal phases (raocp_mega.hip)
-        const int ncl_top = c->cls_ptr[s], ncl_sub = c->cls_ptr[N] - c->cls_ptr[s];
-        const int nmat = dyn ? 0 : c->n_sq * nx * nx + c->n_sr * nu * nu + c->n_sp * nx * nx;
-        const long budget = (long)(lds_cap / 8);
-        long cap = budget, need1 = 0;
-        auto rup2 = [](long v) { return (v + 1) / 2 * 2; };
-        auto level_need = [&](const Rec* lv, int nl, bool leaves) {
-            long mx = 0;
-            for (int l = 0; l < nl; ++l) {
-                const long cp = lv[l].y - lv[l].x, cc = lv[l + 1].y - lv[l + 1].x;
-                mx = std::max(mx, 2 * (rup2(cp * nx) + 4) + 2 * (rup2(cp * nu) + 4) + 2 * cp + 4 + 2 * cc + 4);
-                mx = std::max(mx, 3 * (rup2(cc * nx) + 4) + 3 * (rup2(cc * nu) + 4) + 2 * cc + 4 + 2 * cp + 4);
-            }
-            if (leaves) {
-                const long cl = lv[nl].y - lv[nl].x;
-                mx = std::max(mx, 3 * (rup2(cl * nx) + 4) + 2 * cl + 4);
-            }
-            return mx;
-        };
-        {
-            const raocp::MegaLds m0(c->nkind, ncl_top, c->stage_ptr[s + 1], c->stage_ptr[s], maxch, nsub, nx, nu, nmat, 0,
-                                    nthreads);
-            cap = std::min<long>(cap, budget - (m0.total - (m0.oNL - m0.oXQ)));
-            need1 = std::max(need1, level_need(cd.lv.data(), s, false));
-        }
-        for (int k = 0; k < nsub; ++k) {
-            const Rec* lv = cd.lv.data() + (size_t)(1 + k) * (kMegaLev + 1);
-            const int nall = lv[L].z + (lv[L].y - lv[L].x), nnl = lv[L].z;
-            const raocp::MegaLds m1(c->nkind, ncl_sub, nall, nnl, maxch, 0, nx, nu, nmat, 0, nthreads);
-            cap = std::min<long>(cap, budget - (m1.total - (m1.oNL - m1.oXQ)));
-            need1 = std::max(need1, level_need(lv, L, true));
-        }
-        if (dyn) cap = 0;
-        else if (cap < need1) continue;
-        cap = cap / 2 * 2;
-        size_t lds = 0;
-        {
-            const raocp::MegaLds m0(c->nkind, ncl_top, c->stage_ptr[s + 1], c->stage_ptr[s], maxch, nsub, nx, nu, nmat,
-                                    (int)cap, nthreads);
-            lds = std::max(lds, (size_t)m0.total * 8);
-        }
-        for (int k = 0; k < nsub; ++k) {
-            const Rec* lv = cd.lv.data() + (size_t)(1 + k) * (kMegaLev + 1);
-            const int nall = lv[L].z + (lv[L].y - lv[L].x), nnl = lv[L].z;
-            const raocp::MegaLds m1(c->nkind, ncl_sub, nall, nnl, maxch, 0, nx, nu, nmat, (int)cap, nthreads);
-            lds = std::max(lds, (size_t)m1.total * 8);
-        }
-        if (lds > lds_cap) continue;
-        cd.lds = lds;
-        cd.stage_cap = (int)cap;
-        // cost: full engine: the larger of the top and a subtree (phases) plus the levels of
-        // both sweeps; dynamics only: the passes of every level step on the critical path
-        // (top levels, then the widest subtree's), a pass being one row per lane
-        if (dyn) {
-            long passes = 0;
-            const int R = nx + nu;
-            for (int l = 0; l <= s; ++l) passes += 1 + (long)(c->stage_ptr[l + 1] - c->stage_ptr[l]) * R / nthreads;
-            const Rec* lv1 = cd.lv.data() + (size_t)(kMegaLev + 1);
-            for (int l = 0; l <= L; ++l) passes += 1 + (long)(lv1[l].y - lv1[l].x) * R / nthreads;
-            cd.cost = passes;
-        } else {
-            cd.cost = std::max(top_nodes, sub_max) * 4 + 2 * (long)N;
-        }
-        if (!have || cd.cost < best.cost || (cd.cost == best.cost && cd.s > best.s)) {
-            best = cd;
-            have = true;
-        }
+// Every entry point that takes a context runs on that context's device: the current
+// device is switched for the call and restored afterwards (a process may hold contexts
+// on several devices; allocations and graph captures must land on c->device).
+struct DevGuard {
+    int prev = -1;
+    explicit DevGuard(const raocp_ctx* c) {
+        if (!c) return;
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != c->device) (void)hipSetDevice(c->device);
+        else prev = -1;
     }
-    if (!have) return RAOCP_OK;
-    const int s = best.s, nsub = c->stage_ptr[s + 1] - c->stage_ptr[s], nwg = 1 + nsub;
-    raocp::MegaArg& a = out->a;
-    int rc;
-    const raocp::Rec* dlv = nullptr;
-    const int* dwl = nullptr;
-    if ((rc = c->upload_vec(&dlv, best.lv)) || (rc = c->upload_vec(&dwl, best.wl))) return rc;
-    a.lv = dlv;
-    a.wl = dwl;
-    a.ups = c->KP + 16;
-    a.dns = raocp::rup(nx + 1, 2) + 2;
-    if ((rc = c->alloc(&a.up, (size_t)nsub * a.ups)) || (rc = c->alloc(&a.dn, (size_t)nsub * a.dns)) ||
-        (rc = c->alloc(&a.up_flag, (size_t)nsub + 64)) || (rc = c->alloc(&a.dn_flag, 64)))
-        return rc;
-    a.s = s;
-    a.nsub = nsub;
-    a.c_top1 = c->cls_ptr[s];
-    a.c_sub0 = c->cls_ptr[s];
-    a.c_sub1 = c->cls_ptr[N];
-    a.maxch = best.maxch;
-    a.stage_cap = best.stage_cap;
-    a.timeout = 20000000;  // 0.2 s per wait (100 MHz)
-    if ((rc = c->alloc(&a.epoch, 64))) return rc;
-    if (hipMemset(a.up_flag, 0, (size_t)(nsub + 64) * sizeof(unsigned)) != hipSuccess ||
-        hipMemset(a.dn_flag, 0, 64 * sizeof(unsigned)) != hipSuccess || hipMemset(a.epoch, 0, 64 * sizeof(unsigned)) != hipSuccess)
-        return fail(RAOCP_ERR_HIP, "memset");
-    out->s = s;
-    out->nwg = nwg;
-    out->lds = best.lds;
-    out->ok = true;
-    if (getenv("RAOCP_VERBOSE"))
-        fprintf(stderr, "[raocp] %s engine: cut stage %d, %d workgroups, LDS %zu B\n", dyn ? "dynamics" : "persistent CP", s,
-                nwg, best.lds);
-    return RAOCP_OK;
-}
-
-int mega_plan(raocp_ctx* c, const raocp_tree_desc* t) {
-    int rc;
-    c->mega_ok = c->dyn_ok = false;
-    // full engine: opt-in (RAOCP_MEGA=1); on MI355X the graph-replayed launches are faster
-    // (persistent engine)
-    const char* on = getenv("RAOCP_MEGA");
-    if (on && atoi(on) != 0) {
-        EnginePlan e;
-        if ((rc = engine_plan(c, t, false, &e))) return rc;
-        c->mega_ok = e.ok;
-        c->mega_s = e.s;
-        c->mega_nwg = e.nwg;
-        c->mega_lds = e.lds;
-        c->mega = e.a;
-    }
-    // dynamics-only engine inside the CP graph: RAOCP_DYN_ENGINE=1
-    const char* dn = getenv("RAOCP_DYN_ENGINE");
-    if (dn && atoi(dn) != 0) {
-        EnginePlan e;
-        if ((rc = engine_plan(c, t, true, &e))) return rc;
-        c->dyn_ok = e.ok;
-        c->dyn_s = e.s;
-        c->dyn_nwg = e.nwg;
-        c->dyn_lds = e.lds;
-        c->dyn = e.a;
-    }
-    return RAOCP_OK;
-}
-
-struct MegaOp {
-    template <int NX, int NU>
-    void run(raocp_ctx* c, hipError_t* err) {
-        auto k = raocp::k_mega<NX, NU, false>;
-        hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->mega_lds);
-        const Ctl* none = nullptr;
-        if (e == hipSuccess) {
-            void* args[] = {(void*)&c->dev, (void*)&c->mega, (void*)&none};
-            e = hipLaunchCooperativeKernel((const void*)k, dim3(c->mega_nwg), dim3(raocp::kMegaThreads), args,
-                                           (unsigned)c->mega_lds, c->stream);
-        }
-        *err = e;
+    ~DevGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
     }
 };
-
-// one persistent launch: iterations 0 .. (stop) after cp_init (buffers reset, first half step)
-int mega_launch(raocp_ctx* c, int max_iters, double tol, double alpha, unsigned long long* stamps = nullptr) {
-    raocp::MegaArg& a = c->mega;
-    for (int b = 0; b < 3; ++b) a.Z[b] = c->Z[b];
-    for (int b = 0; b < 2; ++b) a.E[b] = c->E[b];
-    a.xi2 = c->XI2;
-    a.x0 = c->x0;
-    a.hist = c->hist;
-    a.ctl = c->ctl;
-    a.alpha = alpha;
-    a.tol = tol;
-    a.max_iters = max_iters;
-    a.stamps = stamps;
-    HIPCHK(hipMemsetAsync(a.up_flag, 0, (size_t)(a.nsub + 64) * sizeof(unsigned), c->stream));
-    HIPCHK(hipMemsetAsync(a.dn_flag, 0, 64 * sizeof(unsigned), c->stream));
-    hipError_t e = hipSuccess;
-    dispatch(c->nx, c->nu, MegaOp{}, c, &e);
-    if (e != hipSuccess) return fail(RAOCP_ERR_HIP, std::string("persistent CP launch: ") + hipGetErrorString(e));
-    return RAOCP_OK;
-}
-
-bool mega_on(const raocp_ctx* c) { return c->mega_ok && !c->comm && c->sh_R == 1; }
 
 }  // namespace
 
@@ -1012,7 +785,13 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         (rc = check_group(nx + nu + cmax + 1, "CP primal nonleaf")))
         return rc;
 
+    int prev_dev = -1;
+    (void)hipGetDevice(&prev_dev);
     HIPCHK(hipSetDevice(device));
+    struct Restore {
+        int d;
+        ~Restore() { if (d >= 0) (void)hipSetDevice(d); }
+    } restore_{prev_dev != device ? prev_dev : -1};
     raocp_ctx* c = new raocp_ctx();
     c->device = device;
     c->n = n; c->m = m; c->nx = nx; c->nu = nu; c->cmax = cmax; c->N = N;
@@ -1601,19 +1380,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     c->cur_z = c->Z[0];
     c->cur_e = c->E[0];
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
-    if ((rc = mega_plan(c, t))) return bail(rc);
-    {
-        const int rtx = cdiv(nx, 16), rtu = cdiv(nu, 16), tc = cdiv(n - 1, 16), tl = cdiv(n - m, 16), tp = cdiv(m, 16);
-        const int per = 64 * raocp::kEllsE;
-        const long ny = c->dev.T0 - c->dev.Y0;
-        const long totl = ny + m + (n - 1) + (long)m * (nx + nu) + (n - m) + (long)(n - m) * nx;
-        const long tott = (long)m + (n - 1) + (n - m);
-        c->ells_l = raocp::EllsPlan{tc * rtx, tc * rtu, tl * rtx, rtx, rtu, (int)((totl + per - 1) / per)};
-        c->ells_t = raocp::EllsPlan{tp * rtx, tp * rtu, tl * rtx, rtx, rtu, (int)((tott + per - 1) / per)};
-        c->ells_lb = cdiv(c->ells_l.nQ + c->ells_l.nR + c->ells_l.nP + c->ells_l.ncopy, 4);
-        c->ells_tb = cdiv(c->ells_t.nQ + c->ells_t.nR + c->ells_t.nP + c->ells_t.ncopy, 4);
-        if (const char* e = getenv("RAOCP_ELL_STREAM")) c->ells_on = atoi(e) != 0;
-    }
     c->dev.dyn_regtab = 0;  // RAOCP_DYN_REGTAB=1: dynamics tables by vector loads instead of LDS-DMA
     if (const char* e = getenv("RAOCP_DYN_REGTAB")) c->dev.dyn_regtab = atoi(e) != 0;
     c->dev.regstage = 0;  // RAOCP_REGSTAGE=1: k_ell's gather by vector loads (measured slower)
@@ -1627,9 +1393,10 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
 
 void raocp_ctx_destroy(raocp_ctx* c) {
     if (!c) return;
+    DevGuard dg_(c);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm && g_rccl.destroy) (void)g_rccl.destroy((ncclComm_t)c->comm);
-    if (c->graph) (void)hipGraphExecDestroy(c->graph);
+    drop_graphs(c);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1637,6 +1404,7 @@ void raocp_ctx_destroy(raocp_ctx* c) {
 }
 
 int raocp_sizes(raocp_ctx* c, int64_t* P, int64_t* D) {
+    DevGuard dg_(c);
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     if (P) *P = c->P;
     if (D) *D = c->D;
@@ -1644,6 +1412,7 @@ int raocp_sizes(raocp_ctx* c, int64_t* P, int64_t* D) {
 }
 
 int raocp_ell(raocp_ctx* c, const double* z, double* eta, int flags) {
+    DevGuard dg_(c);
     if (!c || !z || !eta) return fail(RAOCP_ERR_ARG, "null argument");
     int rc;
     if (flags & RAOCP_DEVICE_PTR) {
@@ -1659,6 +1428,7 @@ int raocp_ell(raocp_ctx* c, const double* z, double* eta, int flags) {
 }
 
 int raocp_ell_t(raocp_ctx* c, const double* eta, double* z, int flags) {
+    DevGuard dg_(c);
     if (!c || !z || !eta) return fail(RAOCP_ERR_ARG, "null argument");
     int rc;
     if (flags & RAOCP_DEVICE_PTR) {
@@ -1674,6 +1444,7 @@ int raocp_ell_t(raocp_ctx* c, const double* eta, double* z, int flags) {
 }
 
 int raocp_set_primal(raocp_ctx* c, const double* z, int flags) {
+    DevGuard dg_(c);
     if (!c || !z) return fail(RAOCP_ERR_ARG, "null argument");
     int rc = copy_in(c, c->cur_z, z, c->P, flags);
     if (rc) return rc;
@@ -1681,10 +1452,12 @@ int raocp_set_primal(raocp_ctx* c, const double* z, int flags) {
     return RAOCP_OK;
 }
 int raocp_get_primal(raocp_ctx* c, double* z, int flags) {
+    DevGuard dg_(c);
     if (!c || !z) return fail(RAOCP_ERR_ARG, "null argument");
     return copy_out(c, z, c->cur_z, c->P, flags);
 }
 int raocp_set_dual(raocp_ctx* c, const double* e, int flags) {
+    DevGuard dg_(c);
     if (!c || !e) return fail(RAOCP_ERR_ARG, "null argument");
     int rc = copy_in(c, c->cur_e, e, c->D, flags);
     if (rc) return rc;
@@ -1692,11 +1465,13 @@ int raocp_set_dual(raocp_ctx* c, const double* e, int flags) {
     return RAOCP_OK;
 }
 int raocp_get_dual(raocp_ctx* c, double* e, int flags) {
+    DevGuard dg_(c);
     if (!c || !e) return fail(RAOCP_ERR_ARG, "null argument");
     return copy_out(c, e, c->cur_e, c->D, flags);
 }
 
 int raocp_set_initial_state(raocp_ctx* c, const double* x0) {
+    DevGuard dg_(c);
     if (!c || !x0) return fail(RAOCP_ERR_ARG, "null argument");
     c->h_x0.assign(x0, x0 + c->nx);
     HIPCHK(hipMemcpy(c->x0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice));
@@ -1705,6 +1480,7 @@ int raocp_set_initial_state(raocp_ctx* c, const double* x0) {
 }
 
 int raocp_relax_s0(raocp_ctx* c, double alpha) {
+    DevGuard dg_(c);
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     raocp::k_relax_s0<<<1, 1, 0, c->stream>>>(c->dev, c->cur_z, alpha);
     HIPCHK(hipGetLastError());
@@ -1713,6 +1489,7 @@ int raocp_relax_s0(raocp_ctx* c, double alpha) {
 }
 
 int raocp_project_on_dynamics(raocp_ctx* c) {
+    DevGuard dg_(c);
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     if (!c->has_x0) return fail(RAOCP_ERR_STATE, "initial state not cached (call cache_initial_state first)");
     const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
@@ -1735,6 +1512,7 @@ int raocp_project_on_dynamics(raocp_ctx* c) {
 }
 
 int raocp_project_on_kernel(raocp_ctx* c) {
+    DevGuard dg_(c);
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     const Launch L = groups(c->cmax + 1, c->m);
     raocp::k_kernel_proj<<<L.blocks, kBlock, 0, c->stream>>>(c->dev, c->cur_z);
@@ -1744,6 +1522,7 @@ int raocp_project_on_kernel(raocp_ctx* c) {
 }
 
 int raocp_prox_f(raocp_ctx* c, double alpha) {
+    DevGuard dg_(c);
     int rc;
     if ((rc = raocp_relax_s0(c, alpha)) || (rc = raocp_project_on_dynamics(c)) || (rc = raocp_project_on_kernel(c)))
         return rc;
@@ -1751,6 +1530,7 @@ int raocp_prox_f(raocp_ctx* c, double alpha) {
 }
 
 int raocp_prox_gconj(raocp_ctx* c, double alpha) {
+    DevGuard dg_(c);
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     int rc = set_ctl_alpha(c, alpha);
     if (rc) return rc;
@@ -1765,6 +1545,7 @@ int raocp_prox_gconj(raocp_ctx* c, double alpha) {
 }
 
 int raocp_dual_scale(raocp_ctx* c, double alpha) {
+    DevGuard dg_(c);
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     raocp::k_div<<<std::min(2048, cdiv((int)c->D, kBlock)), kBlock, 0, c->stream>>>(c->cur_e, alpha, (int)c->D);
     HIPCHK(hipGetLastError());
@@ -1773,6 +1554,7 @@ int raocp_dual_scale(raocp_ctx* c, double alpha) {
 }
 
 int raocp_dual_add_halves(raocp_ctx* c) {
+    DevGuard dg_(c);
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     const Dev& D = c->dev;
     const int nb = cdiv(c->n, kBlock);
@@ -1786,6 +1568,7 @@ int raocp_dual_add_halves(raocp_ctx* c) {
 }
 
 int raocp_dual_project(raocp_ctx* c, int which) {
+    DevGuard dg_(c);
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     HIPCHK(hipMemsetAsync(&c->ctl->flags, 0, sizeof(int), c->stream));
     const int mode = (which & 1 ? raocp::kDualNonleaf : 0) | (which & 2 ? raocp::kDualLeaf : 0);
@@ -1798,6 +1581,7 @@ int raocp_dual_project(raocp_ctx* c, int which) {
 }
 
 int raocp_dual_moreau(raocp_ctx* c, double alpha, const double* modified) {
+    DevGuard dg_(c);
     if (!c || !modified) return fail(RAOCP_ERR_ARG, "null argument");
     int rc = copy_in(c, c->tmpD, modified, c->D, 0);
     if (rc) return rc;
@@ -1847,6 +1631,7 @@ static int dev_dot(raocp_ctx* c, const double* a, const double* b, int n, double
 }
 
 int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
+    DevGuard dg_(c);
     if (!c || !lambda_max) return fail(RAOCP_ERR_ARG, "null argument");
     if (max_it <= 0) max_it = 300;
     if (rtol <= 0) rtol = 1e-14;
@@ -1909,19 +1694,14 @@ int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
 
 int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, double alpha, int* status, int* iters,
                  double* err_hist, double* delta_hist) {
+    DevGuard dg_(c);
     if (!c || !x0) return fail(RAOCP_ERR_ARG, "null argument");
     if (max_iters < 0) return fail(RAOCP_ERR_ARG, "max_iters must be >= 0");
     int rc;
     if ((rc = ensure_hist(c, (size_t)max_iters + 1))) return rc;
     if ((rc = raocp_set_initial_state(c, x0))) return rc;
-    if ((rc = cp_init(c, x0, max_iters, tol, alpha))) return rc;
-    if (mega_on(c)) {
-        if ((rc = mega_launch(c, max_iters, tol, alpha))) return rc;
-        HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
-        if (c->h_ctl->flags & 2) return fail(RAOCP_ERR_HIP, "persistent CP engine: hand-off timed out");
-        if (!c->h_ctl->done) return fail(RAOCP_ERR_STATE, "persistent CP engine ended without a stopping decision");
-    } else {
+    if ((rc = cp_init(c, x0, max_iters, tol, alpha, true))) return rc;
+    {
         const int batch = kGraphBatch;
         if ((rc = ensure_graph(c, batch))) return rc;
         for (;;) {
@@ -1947,41 +1727,40 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     return RAOCP_OK;
 }
 
-int raocp_engine_info(raocp_ctx* c, int* cut, int* workgroups, int* dyn_cut) {
-    if (!c) return fail(RAOCP_ERR_ARG, "null argument");
-    const bool on = mega_on(c);
-    if (cut) *cut = on ? c->mega_s : 0;
-    if (workgroups) *workgroups = on ? c->mega_nwg : 0;
-    if (dyn_cut) *dyn_cut = (c->dyn_ok && c->sh_R == 1 && !c->comm) ? c->dyn_s : 0;
+int raocp_cp_prepare(raocp_ctx* c, int iters) {
+    DevGuard dg_(c);
+    if (!c || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
+    int rc;
+    if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
+    if (iters / kGraphBatch && (rc = ensure_graph(c, kGraphBatch))) return rc;
+    if (iters % kGraphBatch && (rc = ensure_graph(c, iters % kGraphBatch))) return rc;
     return RAOCP_OK;
 }
 
 int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, float* ms) {
+    DevGuard dg_(c);
     if (!c || !x0 || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
     int rc;
     if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
-    const int batch = kGraphBatch;
-    const bool mg = mega_on(c);
-    if (!mg && (rc = ensure_graph(c, batch))) return rc;
+    const int batch = kGraphBatch, full = iters / batch, rem = iters % batch;
+    if (full && (rc = ensure_graph(c, batch))) return rc;
+    if (rem && (rc = ensure_graph(c, rem))) return rc;
     if ((rc = cp_init(c, x0, iters - 1, 0.0, alpha))) return rc;
     hipEvent_t e0, e1;
     HIPCHK(hipEventCreate(&e0));
     HIPCHK(hipEventCreate(&e1));
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventRecord(e0, c->stream));
-    if (mg) {
-        if ((rc = mega_launch(c, iters - 1, 0.0, alpha))) return rc;
-    } else {
-        for (int done = 0; done < iters; done += batch)
-            if ((rc = launch_batch(c, batch))) return rc;
-    }
+    // exactly `iters` iterations' kernels: whole batches, then the remainder batch
+    for (int b = 0; b < full; ++b)
+        if ((rc = launch_batch(c, batch))) return rc;
+    if (rem && (rc = launch_batch(c, rem))) return rc;
     HIPCHK(hipEventRecord(e1, c->stream));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     HIPCHK(hipMemcpy(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
-    if (c->h_ctl->flags & 2) return fail(RAOCP_ERR_HIP, "persistent CP engine: hand-off timed out");
     if (c->h_ctl->final_k != iters - 1) return fail(RAOCP_ERR_STATE, "bench did not run the requested iterations");
     c->cur_z = c->Z[iters % 3];
     c->cur_e = c->E[iters % 2];
@@ -1992,6 +1771,7 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
 // stamps enabled (k_dyn_top: prologue, each backward / forward stage); returns up to
 // `cap` raw 100 MHz timestamps.
 int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
+    DevGuard dg_(c);
     if (!c || !out || cap <= 0) return fail(RAOCP_ERR_ARG, "bad argument");
     unsigned long long* st = nullptr;
     int rc = c->alloc(&st, (size_t)cap);
@@ -2006,19 +1786,6 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
         int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
         if (rc2) return rc2;
         launch_cpp(c);
-    } else if (which && which[0] == 'm' && mega_on(c)) {
-        // persistent engine: 8 iterations; stamps of workgroup 0 (top) then 1 (a subtree), 64 each
-        std::vector<double> x0(c->nx, 0.0);
-        c->dev = saved;
-        if (cap < 128) return fail(RAOCP_ERR_ARG, "engine stamps need cap >= 128");
-        int rc2 = cp_init(c, x0.data(), 7, 0.0, 0.3);
-        if (rc2) return rc2;
-        unsigned long long* all = nullptr;
-        if ((rc2 = c->alloc(&all, (size_t)c->mega_nwg * 64))) return rc2;
-        HIPCHK(hipMemset(all, 0, (size_t)c->mega_nwg * 64 * sizeof(unsigned long long)));
-        if ((rc2 = mega_launch(c, 7, 0.0, 0.3, all))) return rc2;
-        HIPCHK(hipStreamSynchronize(c->stream));
-        HIPCHK(hipMemcpy(st, all, 128 * sizeof(unsigned long long), hipMemcpyDeviceToDevice));
     } else if (which && which[0] == 'l') {  // k_ell on the staging buffers
         launch_ell(c, c->tmpP, c->tmpD);
     } else if (which && which[0] == 't') {  // k_ell_t
@@ -2035,6 +1802,7 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
 
 // ---- subtree sharding ---------------------------------------------------------------
 int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
+    DevGuard dg_(c);
     if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(RAOCP_ERR_ARG, "bad shard arguments");
     // one shard is the unsharded solve, unless forced (tests run the exchange path with R = 1)
     if (nranks == 1 && !getenv("RAOCP_SHARD_FORCE")) return RAOCP_OK;
@@ -2087,17 +1855,14 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     if ((rc = build_cp_blocks(c, pr_, lr_))) return rc;
     if ((rc = c->alloc(&c->x2_send, (size_t)xmax * c->KP)) || (rc = c->alloc(&c->x2_recv, (size_t)nranks * xmax * c->KP)) ||
         (rc = c->alloc(&c->x1_send, (size_t)2 * xmax)) || (rc = c->alloc(&c->x1_recv, (size_t)2 * nranks * xmax)) ||
-        (rc = c->alloc(&c->red8, 8)) || (rc = c->upload_vec(&c->d_slc, slc)))
+        (rc = c->alloc(&c->red8, 16)) || (rc = c->upload_vec(&c->d_slc, slc)))
         return rc;
-    if (c->graph) {
-        (void)hipGraphExecDestroy(c->graph);
-        c->graph = nullptr;
-        c->graph_iters = 0;
-    }
+    drop_graphs(c);
     return RAOCP_OK;
 }
 
 int raocp_shard_owned(raocp_ctx* c, int32_t* lo, int32_t* hi, int cap) {
+    DevGuard dg_(c);
     if (!c || !lo || !hi) return fail(RAOCP_ERR_ARG, "null argument");
     for (int t = 0; t <= c->N && t < cap; ++t) {
         lo[t] = c->sh_S > 0 ? c->own_lo[t] : c->stage_ptr[t];
@@ -2117,6 +1882,7 @@ int raocp_comm_unique_id(unsigned char* out128) {
 }
 
 int raocp_comm_init(raocp_ctx* c, const unsigned char* id128, int nranks, int rank) {
+    DevGuard dg_(c);
     if (!c || !id128) return fail(RAOCP_ERR_ARG, "null argument");
     if (c->sh_R != nranks || c->sh_r != rank) return fail(RAOCP_ERR_STATE, "call raocp_shard_setup with the same ranks first");
     int rc;
@@ -2127,11 +1893,7 @@ int raocp_comm_init(raocp_ctx* c, const unsigned char* id128, int nranks, int ra
     ncclComm_t comm = nullptr;
     if ((rc = rccl_check(g_rccl.init_rank(&comm, nranks, id, rank), "ncclCommInitRank"))) return rc;
     c->comm = comm;
-    if (c->graph) {
-        (void)hipGraphExecDestroy(c->graph);
-        c->graph = nullptr;
-        c->graph_iters = 0;
-    }
+    drop_graphs(c);
     return RAOCP_OK;
 }
 
@@ -2140,6 +1902,7 @@ int raocp_comm_init(raocp_ctx* c, const unsigned char* id128, int nranks, int ra
 int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, double tol, double alpha, int* status,
                        int* iters, double* err_hist, double* delta_hist) {
     if (!cs || R < 1 || !x0) return fail(RAOCP_ERR_ARG, "null argument");
+    DevGuard dg_(cs[0]);
     for (int r = 0; r < R; ++r)
         if (!cs[r] || cs[r]->sh_R != R || cs[r]->sh_r != r) return fail(RAOCP_ERR_STATE, "shards not set up for this group");
     int rc;
@@ -2154,7 +1917,7 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
         for (int r = 0; r < R; ++r) HIPCHK(hipStreamSynchronize(cs[r]->stream));
         return RAOCP_OK;
     };
-    std::vector<double> red(8 * R);
+    std::vector<double> red(16 * R);
     for (int k = 0;; ++k) {
         for (int r = 0; r < R; ++r) {
             raocp_ctx* c = cs[r];
@@ -2182,17 +1945,17 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
             shard_unpack_x1(c);
             launch_cpp(c);
             raocp::k_cp_reduce<<<1, kBlock, 0, c->stream>>>(c->ctl, c->redpart, c->cp_rows, c->red8);
-            HIPCHK(hipMemcpyAsync(red.data() + 8 * r, c->red8, 8 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+            HIPCHK(hipMemcpyAsync(red.data() + 16 * r, c->red8, 16 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
         }
         if ((rc = sync_all())) return rc;
-        double g[8];
-        for (int q = 0; q < 8; ++q) {
+        double g[16];
+        for (int q = 0; q < 16; ++q) {
             g[q] = red[q];
-            for (int r = 1; r < R; ++r) g[q] = std::max(g[q], red[8 * r + q]);
+            for (int r = 1; r < R; ++r) g[q] = std::max(g[q], red[16 * r + q]);
         }
         for (int r = 0; r < R; ++r) {
             raocp_ctx* c = cs[r];
-            HIPCHK(hipMemcpyAsync(c->red8, g, 8 * sizeof(double), hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->red8, g, 16 * sizeof(double), hipMemcpyHostToDevice, c->stream));
             raocp::k_cp_check_red<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->red8);
             HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
         }
@@ -2221,6 +1984,7 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
 }
 
 int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
+    DevGuard dg_(c);
     if (!c || reps < 1 || !ms_per_launch) return fail(RAOCP_ERR_ARG, "bad argument");
     // random inputs (seed 1), resident in HBM
     std::vector<double> hz(c->P), he(c->D);

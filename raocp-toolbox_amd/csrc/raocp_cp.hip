@@ -47,8 +47,8 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
         eo[e] = ep;
         const double x2 = (dv - ep) / alpha + b;
         xi2[e] = x2;
-        m2 = fmax(m2, fabs(x2));
-        m5 = fmax(m5, fabs(ep - dv));
+        m2 = nmax(m2, fabs(x2));
+        m5 = nmax(m5, fabs(ep - dv));
     };
     if (bid < nbF) {
         const Rec t0 = ((crec4*)p.cpd_tab)[2 * bid], t1 = ((crec4*)p.cpd_tab)[2 * bid + 1];
@@ -295,12 +295,12 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
 // ==============================================================================
 // block-wide max of non-negative doubles, returned in every thread
 __device__ __forceinline__ double block_max_val(double v, double* s_red) {
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    for (int off = 32; off > 0; off >>= 1) v = nmax(v, __shfl_xor(v, off, 64));
     __syncthreads();
     if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
     __syncthreads();
     double b = s_red[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) b = fmax(b, s_red[i]);
+    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) b = nmax(b, s_red[i]);
     return b;
 }
 
@@ -310,13 +310,13 @@ __device__ __forceinline__ double block_max_val(double v, double* s_red) {
 __device__ void cp_check_last(Ctl* ctl, double* hist, const double* part, int rows, unsigned* ticket, double* s_red) {
     double m[6] = {0, 0, 0, 0, 0, 0};
     for (int r = threadIdx.x; r < rows; r += blockDim.x)
-        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = fmax(m[q], ld_sc1(part + (size_t)r * 6 + q));
+        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], ld_sc1(part + (size_t)r * 6 + q));
     double M[6];
     _Pragma("unroll") for (int q = 0; q < 6; ++q) M[q] = block_max_val(m[q], s_red);
     if (threadIdx.x != 0) return;
     const int k = ctl->k;
     for (int q = 0; q < 6; ++q) hist[(size_t)k * 6 + q] = M[q];
-    const double err = fmax(fmax(M[0], M[1]), M[2]);
+    const double err = nmax(nmax(M[0], M[1]), M[2]);
     if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
         ctl->done = 1;
         ctl->final_k = k;
@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
         const double x0v = x1 + lc;
         const double dl1 = zz - pp;
         const double dl0 = dl1 + w;
-        m0 = fmax(m0, fabs(x0v)); m1 = fmax(m1, fabs(x1)); m3 = fmax(m3, fabs(dl0)); m4 = fmax(m4, fabs(dl1));
+        m0 = nmax(m0, fabs(x0v)); m1 = nmax(m1, fabs(x1)); m3 = nmax(m3, fabs(dl0)); m4 = nmax(m4, fabs(dl1));
     };
     if (bid < nbF) {
         const Rec t0 = ((crec4*)p.cpd_tab)[2 * bid], t1 = ((crec4*)p.cpd_tab)[2 * bid + 1];

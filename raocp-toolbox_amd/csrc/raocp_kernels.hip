@@ -123,6 +123,11 @@ __device__ __forceinline__ int cdiv_dev(int a, int b) { return (a + b - 1) / b; 
 
 __device__ __forceinline__ u64 dbits(double v) { return (u64)__double_as_longlong(v); }
 
+// max for the residual reductions: a NaN operand wins (fmax would drop it). The reference
+// takes its inf-norms with numpy, which propagates NaN, so a NaN residual fails the
+// stopping test `max(error) <= tol` there (solver.py:137-161) and must fail it here too.
+__device__ __forceinline__ double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
+
 // ---- batched dot products ----------------------------------------------------------
 // All loads of a chunk are issued before its FMAs (a sched_barrier keeps hipcc from
 // interleaving each load with its FMA, which pays the memory latency per element);
@@ -243,14 +248,14 @@ __device__ __forceinline__ void dot_lt3(PM m, int ms, PV dA, PV dP, PV cc, int n
 // block-wide max of non-negative doubles -> one plain store per block (the per-block
 // partials are reduced by k_cp_check; no atomics on a single hot address)
 __device__ void block_max_store(double v, double* dst, double* s_red) {
-    for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+    for (int off = 32; off > 0; off >>= 1) v = nmax(v, __shfl_xor(v, off, 64));
     const int w = threadIdx.x >> 6;
     __syncthreads();
     if ((threadIdx.x & 63) == 0) s_red[w] = v;
     __syncthreads();
     if (threadIdx.x == 0) {
         double b = s_red[0];
-        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) b = fmax(b, s_red[i]);
+        for (int i = 1; i < (int)(blockDim.x >> 6); ++i) b = nmax(b, s_red[i]);
         *dst = b;
     }
 }
@@ -288,7 +293,6 @@ __device__ __forceinline__ int dma_any(ldsd* dst, PT src, int nbytes, int* rot =
 }
 
 #include "raocp_ell.hip"
-#include "raocp_ells.hip"
 
 // ==============================================================================
 // AVaR kernel projection of (y_i, tau_children, s_children) (cache.py:290-317),
@@ -403,7 +407,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_primal(Dev p, Ctl* __restrict__ c
         const double x0v = x1 + ltxi2;
         const double dl1 = zz - pp;
         const double dl0 = dl1 + w;
-        m0 = fmax(m0, fabs(x0v)); m1 = fmax(m1, fabs(x1)); m3 = fmax(m3, fabs(dl0)); m4 = fmax(m4, fabs(dl1));
+        m0 = nmax(m0, fabs(x0v)); m1 = nmax(m1, fabs(x1)); m3 = nmax(m3, fabs(dl0)); m4 = nmax(m4, fabs(dl1));
     };
     if (bid < nbA) {
         const int G = nx + nu + p.cmax + 1;
@@ -593,8 +597,8 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
             const double de = d[e];
             const double x2 = (de - ep) / alpha + b;
             xi2[e] = x2;
-            m2 = fmax(m2, fabs(x2));
-            m5 = fmax(m5, fabs(ep - de));
+            m2 = nmax(m2, fabs(x2));
+            m5 = nmax(m5, fabs(ep - de));
         }
     };
     if (WITH_L && bid < nbA) {
@@ -684,8 +688,8 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
             eo[e] = ep;
             const double x2 = (dv - ep) / alpha + bb;
             xi2[e] = x2;
-            m2 = fmax(m2, fabs(x2));
-            m5 = fmax(m5, fabs(ep - dv));
+            m2 = nmax(m2, fabs(x2));
+            m5 = nmax(m5, fabs(ep - dv));
         }
     } else if (bid < nbA) {  // standalone prox_g* (no L): direct global reads
         // child block j: rows eta3 (nx), eta4 (nu), eta5, eta6 -> one SOC of dim nx+nu+2
@@ -864,7 +868,6 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
 }
 
 #include "raocp_cp.hip"
-#include "raocp_mega.hip"
 
 // ---- element-wise dual sub-steps of prox_g* (cache.py:329-347, 392-393)
 __global__ void k_div(double* __restrict__ x, double a, int n) {
@@ -887,18 +890,18 @@ __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, con
     if (ctl->done) return;
     double m[6] = {0, 0, 0, 0, 0, 0};
     for (int r = threadIdx.x; r < rows; r += blockDim.x)
-        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = fmax(m[q], part[(size_t)r * 6 + q]);
+        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], part[(size_t)r * 6 + q]);
     _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = m[q];
     __syncthreads();
     for (int w = blockDim.x / 2; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w)
-            _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = fmax(s_m[q][threadIdx.x], s_m[q][threadIdx.x + w]);
+            _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = nmax(s_m[q][threadIdx.x], s_m[q][threadIdx.x + w]);
         __syncthreads();
     }
     if (threadIdx.x != 0) return;
     const int k = ctl->k;
     for (int q = 0; q < 6; ++q) hist[(size_t)k * 6 + q] = s_m[q][0];
-    const double err = fmax(fmax(s_m[0][0], s_m[1][0]), s_m[2][0]);
+    const double err = nmax(nmax(s_m[0][0], s_m[1][0]), s_m[2][0]);  // NaN: not converged
     if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
         ctl->done = 1;
         ctl->final_k = k;
@@ -936,31 +939,39 @@ __global__ void k_unpack2(const double* __restrict__ recv, double* __restrict__ 
         }
     }
 }
-// local part of k_cp_check: this shard's six maxima -> red6 (then all-reduced with max)
+// local part of k_cp_check: this shard's six maxima -> red6[0..5], the NaN-in-box flag -> red6[6],
+// NaN-maximum flags -> red6[8..13] (16 doubles, then all-reduced with max)
 __global__ void __launch_bounds__(kBlock) k_cp_reduce(const Ctl* ctl, const double* __restrict__ part, int rows,
                                                       double* red6) {
     __shared__ double s_m[6][kBlock];
     if (ctl->done) return;
     double m[6] = {0, 0, 0, 0, 0, 0};
     for (int r = threadIdx.x; r < rows; r += blockDim.x)
-        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = fmax(m[q], part[(size_t)r * 6 + q]);
+        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], part[(size_t)r * 6 + q]);
     _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = m[q];
     __syncthreads();
     for (int w = blockDim.x / 2; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w)
-            _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = fmax(s_m[q][threadIdx.x], s_m[q][threadIdx.x + w]);
+            _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = nmax(s_m[q][threadIdx.x], s_m[q][threadIdx.x + w]);
         __syncthreads();
     }
     if (threadIdx.x < 6) red6[threadIdx.x] = s_m[threadIdx.x][0];
     if (threadIdx.x == 6) red6[6] = (ctl->flags & 1) ? 1.0 : 0.0;  // NaN-in-box flag, all-reduced too
     if (threadIdx.x == 7) red6[7] = 0.0;
+    // a NaN maximum is flagged in slots 8..13 (RCCL's max need not propagate NaN)
+    if (threadIdx.x >= 8 && threadIdx.x < 16)
+        red6[threadIdx.x] = (threadIdx.x < 14 && s_m[threadIdx.x - 8][0] != s_m[threadIdx.x - 8][0]) ? 1.0 : 0.0;
 }
 // history + stopping test on the all-reduced maxima (same decision on every shard)
 __global__ void k_cp_check_red(Ctl* ctl, double* hist, const double* __restrict__ red6) {
     if (threadIdx.x != 0 || ctl->done) return;
     const int k = ctl->k;
-    for (int q = 0; q < 6; ++q) hist[(size_t)k * 6 + q] = red6[q];
-    const double err = fmax(fmax(red6[0], red6[1]), red6[2]);
+    double M[6];
+    for (int q = 0; q < 6; ++q) {
+        M[q] = red6[8 + q] > 0.0 ? __builtin_nan("") : red6[q];
+        hist[(size_t)k * 6 + q] = M[q];
+    }
+    const double err = nmax(nmax(M[0], M[1]), M[2]);  // NaN: not converged
     if (red6[6] > 0.0) ctl->flags |= 1;
     if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
         ctl->done = 1;

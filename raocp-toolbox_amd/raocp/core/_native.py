@@ -23,7 +23,7 @@ EXPORTED_SYMBOLS = [
     "raocp_ctx_create", "raocp_ctx_destroy", "raocp_last_error", "raocp_sizes", "raocp_ell", "raocp_ell_t",
     "raocp_set_primal", "raocp_get_primal", "raocp_set_dual", "raocp_get_dual", "raocp_set_initial_state",
     "raocp_prox_f", "raocp_relax_s0", "raocp_project_on_dynamics", "raocp_project_on_kernel", "raocp_prox_gconj",
-    "raocp_step_size", "raocp_cp_run", "raocp_engine_info", "raocp_cp_bench", "raocp_op_bench",
+    "raocp_step_size", "raocp_cp_run", "raocp_cp_prepare", "raocp_cp_bench", "raocp_op_bench",
     "raocp_dual_scale", "raocp_dual_add_halves", "raocp_dual_project", "raocp_dual_moreau",
     "raocp_device_synchronize", "raocp_debug_dyn_stamps",
     "raocp_shard_setup", "raocp_shard_owned", "raocp_comm_unique_id", "raocp_comm_init", "raocp_group_cp_run",
@@ -89,7 +89,7 @@ def load_library():
         "raocp_step_size": (c_int, [vp, _f64p, c_int, c_double]),
         "raocp_cp_run": (c_int, [vp, vp, c_int, c_double, c_double, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                  vp, vp]),
-        "raocp_engine_info": (c_int, [vp, ctypes.POINTER(c_int), ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+        "raocp_cp_prepare": (c_int, [vp, c_int]),
         "raocp_cp_bench": (c_int, [vp, vp, c_int, c_double, ctypes.POINTER(ctypes.c_float)]),
         "raocp_op_bench": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_float)]),
         "raocp_dual_scale": (c_int, [vp, c_double]),
@@ -293,9 +293,15 @@ class NativeContext:
         self._check(self._lib.raocp_step_size(self._h, ctypes.byref(lam), int(max_it), float(rtol)))
         return lam.value
 
-    def cp_run(self, x0, max_iters, tol, alpha):
+    def cp_run(self, x0, max_iters, tol, alpha, warm=False):
+        """The CP loop on the device. warm=False starts from (x0 at node 0, zeros) / 0;
+        warm=True from the context's current primal / dual (set_primal / set_dual), x0
+        written into node 0's state, as the reference's chock continues from the cache."""
         self._require_l()
         x0 = self._vec(x0, self._packed.nx)
+        if not warm:
+            self.set_primal(np.zeros(self.P))
+            self.set_dual(np.zeros(self.D))
         err = np.zeros((max_iters + 1, 3))
         derr = np.zeros((max_iters + 1, 3))
         status, iters = ctypes.c_int(), ctypes.c_int()
@@ -304,21 +310,9 @@ class NativeContext:
         k = iters.value
         return status.value, err[:k].copy(), derr[:k].copy()
 
-    def engine_info(self):
-        """(cut stage, workgroups) of the persistent CP engine, or (0, 0) when the context
-        runs the graph-replayed multi-kernel iteration."""
-        cut, wg, dc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        self._check(self._lib.raocp_engine_info(self._h, ctypes.byref(cut), ctypes.byref(wg), ctypes.byref(dc)))
-        return cut.value, wg.value
-
-    def dyn_engine_cut(self):
-        """cut stage of the dynamics-only engine used inside the CP iteration (0: tier launches)"""
-        cut, wg, dc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-        self._check(self._lib.raocp_engine_info(self._h, ctypes.byref(cut), ctypes.byref(wg), ctypes.byref(dc)))
-        return dc.value
-
-    def engine_cut(self):
-        return self.engine_info()[0]
+    def cp_prepare(self, iters):
+        """Capture the CP graphs an `iters`-iteration cp_bench launches (outside timing)."""
+        self._check(self._lib.raocp_cp_prepare(self._h, int(iters)))
 
     def cp_bench(self, x0, iters, alpha):
         self._require_l()

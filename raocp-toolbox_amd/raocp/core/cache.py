@@ -198,6 +198,12 @@ class Cache:
         self.__old_primal_flat = self.__ctx.get_primal()
         self.__old_dual_flat = self.__ctx.get_dual()
 
+    def seed_device_iterate(self):
+        """Load the 'old' primal / dual (the iterate the reference's CP loop continues from,
+        cache.py:58-66) into the device context before a solve."""
+        self.__ctx.set_primal(self.__old_primal_flat)
+        self.__ctx.set_dual(self.__old_dual_flat)
+
     def _set_old(self, z, eta):
         self.__old_primal_flat = np.asarray(z, dtype=np.float64).copy()
         self.__old_dual_flat = np.asarray(eta, dtype=np.float64).copy()

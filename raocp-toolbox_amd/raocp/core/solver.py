@@ -4,7 +4,8 @@
 (replacing ARPACK `eigs`, solver.py:104-118), then `raocp_cp_run`, which
 replays the CP iteration as a captured hipGraph (dynamics sweeps, fused
 L + prox_g* + xi2 kernel, fused L^T + AVaR-kernel projection + residual kernel,
-on-device stopping test) and only syncs with the host every 16 iterations.
+on-device stopping test) and only syncs with the host every 24 iterations. Like the
+reference, a solve continues from the cache's current (old) primal / dual.
 Residual histories, return codes and the two timer prints are the reference's.
 The host-orchestrated half steps (`primal_k_plus_half` ...) are kept for API
 parity; each of their operators is still a HIP kernel.
@@ -99,9 +100,13 @@ class Solver:
         else:
             self.__parameter_1 = self.__parameter_2 = float(step_size)
         x0 = np.asarray(initial_state, dtype=np.float64).reshape(-1)
+        # the loop continues from the cached old primal / dual (x0 in node 0's state), as
+        # the reference's does: a second chock warm-starts from the first one's iterate
+        self.__cache.seed_device_iterate()
         print("timer started")
         tick = time.perf_counter()
-        status, err, derr = self.__cache.native.cp_run(x0, int(max_iters), float(tol), self.__parameter_1)
+        status, err, derr = self.__cache.native.cp_run(x0, int(max_iters), float(tol), self.__parameter_1,
+                                                       warm=True)
         tock = time.perf_counter()
         print(f"timer stopped in {tock - tick:0.4f} seconds")
         self.__error = list(err[-1])

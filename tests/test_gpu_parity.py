@@ -5,7 +5,14 @@ the oracle at sizes the oracle finishes in seconds.
 Tolerances: fp64 everywhere. Single operator applications 1e-12 relative (only the
 summation order differs from numpy/BLAS); CP residual traces 1e-8 relative per
 entry (BASELINE.json north_star: "within 1e-8 relative").
+
+Tests that exercise the dynamics projection run under both of its engines: the tiered
+subtree kernels (default) and the per-stage fallback that trees whose subtrees do not
+fit LDS take (RAOCP_DYN_PER_STAGE=1 at context creation), via the `dyn` parameter.
 """
+import contextlib
+import os
+
 import numpy as np
 import pytest
 
@@ -17,6 +24,21 @@ pytestmark = pytest.mark.gpu
 
 OPS = ["main", "ops2x2", "bin6", "c1n5"]
 PROX = ["main", "bin6", "cache3", "c1n5"]
+DYN = ["tiers", "per_stage"]
+
+
+@contextlib.contextmanager
+def dyn_engine(mode):
+    """Contexts created inside use the tiered dynamics kernels or the per-stage fallback."""
+    old = os.environ.get("RAOCP_DYN_PER_STAGE")
+    os.environ["RAOCP_DYN_PER_STAGE"] = "1" if mode == "per_stage" else "0"
+    try:
+        yield
+    finally:
+        if old is None:
+            os.environ.pop("RAOCP_DYN_PER_STAGE", None)
+        else:
+            os.environ["RAOCP_DYN_PER_STAGE"] = old
 
 
 @pytest.fixture(scope="module")
@@ -75,10 +97,12 @@ def test_adjoint_identity(ops_kat, name):
         assert abs(a - b) <= 1e-10 * max(1.0, abs(a))
 
 
+@pytest.mark.parametrize("dyn", DYN)
 @pytest.mark.parametrize("name", PROX)
-def test_prox_f_and_steps_match_reference(prox_kat, name):
+def test_prox_f_and_steps_match_reference(prox_kat, name, dyn):
     z = prox_kat
-    r, cache = _cache(z, name)
+    with dyn_engine(dyn):
+        r, cache = _cache(z, name)
     alpha = float(z[f"{name}/prox_alpha"])
     zin = z[f"{name}/prox_z"]
     cache.cache_initial_state(r["x0"].reshape(-1, 1))
@@ -115,21 +139,22 @@ def test_prox_gconj_and_steps_match_reference(prox_kat, name):
     assert rel_err(cache.get_dual_flat(), z[f"{name}/prox_modify_halves"]) <= 1e-15
 
 
-def _run_chock(z, name, pin):
+def _run_chock(z, name, pin, dyn="tiers"):
     r, tree, prob = problem_from_golden(z, name)
-    solver = core.Solver(problem_spec=prob)
+    with dyn_engine(dyn):
+        solver = core.Solver(problem_spec=prob)
     alpha = float(z[f"{name}/cp_alpha"]) if pin else None
     status = solver.chock(initial_state=r["x0"].reshape(-1, 1), max_iters=int(z[f"{name}/cp_max_iters"]),
                           tol=float(z[f"{name}/cp_tol"]), step_size=alpha)
     return solver, status
 
 
-@pytest.mark.parametrize("pin", [True, False])
-def test_main_py_trace(golden, pin):
+@pytest.mark.parametrize("pin,dyn", [(True, "tiers"), (False, "tiers"), (True, "per_stage")])
+def test_main_py_trace(golden, pin, dyn):
     """main.py end to end: 937 iterations, status 0, residual trace vs the reference's
     (which itself matches the published 4-3-residuals.tex to 3.4e-12)."""
     z = golden("main_trace")
-    solver, status = _run_chock(z, "main", pin)
+    solver, status = _run_chock(z, "main", pin, dyn)
     assert status == int(z["main/cp_status"]) == 0
     err = solver.error_cache
     assert err.shape == z["main/cp_error"].shape == (937, 3)
@@ -143,10 +168,11 @@ def test_main_py_trace(golden, pin):
         assert abs(solver.step_size - float(z["main/cp_alpha"])) <= 1e-12 * float(z["main/cp_alpha"])
 
 
+@pytest.mark.parametrize("dyn", DYN)
 @pytest.mark.parametrize("name", ["bin6", "c1n5", "ops2x2"])
-def test_small_trajectories(golden, name):
+def test_small_trajectories(golden, name, dyn):
     z = golden("traj_small")
-    solver, status = _run_chock(z, name, True)
+    solver, status = _run_chock(z, name, True, dyn)
     assert status == int(z[f"{name}/cp_status"])
     assert trace_rel_err(solver.error_cache, z[f"{name}/cp_error"]) <= 1e-8
     assert trace_rel_err(solver.delta_error_cache, z[f"{name}/cp_delta_error"]) <= 1e-8
@@ -189,12 +215,14 @@ def test_nan_in_box_raises(golden):
 # ---------------------------------------------------------------------------------------
 # the benchmark configuration (BASELINE configs[1]: 8,191 nodes, nx=20, nu=8) vs the oracle
 # ---------------------------------------------------------------------------------------
-@pytest.fixture(scope="module")
-def c2():
+@pytest.fixture(scope="module", params=DYN)
+def c2(request):
     from oracle.raocp_oracle import OracleProblem
     r = recipe_config(2)
     tree, prob = build_problem(r)
-    return r, prob, core.Cache(prob), OracleProblem(prob)
+    with dyn_engine(request.param):
+        cache = core.Cache(prob)
+    return r, prob, cache, OracleProblem(prob)
 
 
 def test_c2_operators_vs_oracle(c2):
@@ -251,8 +279,9 @@ def test_large_operators_vs_oracle(cfg):
     assert abs(a - b) <= 1e-10 * max(abs(a), 1.0)
 
 
-@pytest.mark.parametrize("cfg", [2, 3])
-def test_projections_full_size_vs_oracle_and_idempotent(cfg):
+@pytest.mark.parametrize("dyn", DYN)
+@pytest.mark.parametrize("cfg", [2, 3, 4])
+def test_projections_full_size_vs_oracle_and_idempotent(cfg, dyn):
     """The dynamics and kernel projections (cache.py:259-317) at the HBM-sized configs:
     against the oracle, and size-independent properties: a projection applied twice is
     the projection (idempotence), and its output satisfies x_j = A_j x_i + B_j u_i,
@@ -260,7 +289,9 @@ def test_projections_full_size_vs_oracle_and_idempotent(cfg):
     from oracle.raocp_oracle import OracleProblem
     r = recipe_config(cfg)
     tree, prob = build_problem(r)
-    cache, orc = core.Cache(prob), OracleProblem(prob)
+    with dyn_engine(dyn):
+        cache = core.Cache(prob)
+    orc = OracleProblem(prob)
     nat = cache.native
     rng = np.random.default_rng(17)
     zz = rng.standard_normal(cache.primal_size)
@@ -284,3 +315,74 @@ def test_projections_full_size_vs_oracle_and_idempotent(cfg):
     assert rel_err(z2, orc.project_on_kernel(zz)) <= 1e-12
     nat.project_on_kernel()
     assert rel_err(nat.get_primal(), z2) <= 1e-12
+
+
+@pytest.mark.parametrize("cfg", [3, 4])
+def test_large_cp_trace_vs_oracle(cfg):
+    """The whole CP loop (solver.py:124-161) at the HBM-sized configs (SURVEY.md 8(d)
+    config 3: Markov 4 modes, 87,381 nodes, nx = 20; config 4: branching 3, 88,573 nodes,
+    nx = 32, nu = 12): the fused CP kernels, the dynamics tiers and prox g* at those sizes,
+    10 iterations against the oracle; then prox g* alone on a random dual."""
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(cfg)
+    tree, prob = build_problem(r)
+    cache, orc = core.Cache(prob), OracleProblem(prob)
+    alpha = 0.999 / cache.native.step_size()
+    status, err, derr = cache.native.cp_run(r["x0"], 9, 0.0, alpha)
+    st_o, err_o, derr_o, z_o, e_o, _ = orc.chock(r["x0"], 9, 0.0, alpha=alpha)
+    assert status == st_o == 1 and err.shape == (10, 3)
+    assert trace_rel_err(err, err_o) <= 1e-8
+    assert trace_rel_err(derr, derr_o) <= 1e-8
+    assert rel_err(cache.get_primal_flat(), z_o) <= 1e-10
+    assert rel_err(cache.get_dual_flat(), e_o) <= 1e-10
+    ee = np.random.default_rng(23).standard_normal(cache.dual_size)
+    cache.set_dual_flat(ee)
+    cache.proximal_of_g_conjugate(0.3)
+    assert rel_err(cache.get_dual_flat(), orc.prox_gconj(ee, 0.3)) <= 1e-12
+
+
+def test_chock_warm_starts_like_reference(golden):
+    """A second chock continues from the first one's iterate with the new x0 in node 0's
+    state (solver.py:27-61 read the cache's old primal / dual; cache.py:79-82), and a dual
+    made current by set_dual + update_cache is where the next solve starts."""
+    from oracle.raocp_oracle import OracleProblem
+    z = golden("main_trace")
+    r, tree, prob = problem_from_golden(z, "main")
+    alpha = float(z["main/cp_alpha"])
+    x0 = r["x0"].reshape(-1, 1)
+    orc = OracleProblem(prob)
+    s = core.Solver(problem_spec=prob)
+    s.chock(x0, max_iters=20, tol=0.0, step_size=alpha)
+    _, err1, _, zo, eo, _ = orc.chock(x0, 20, 0.0, alpha=alpha)
+    assert trace_rel_err(s.error_cache, err1) <= 1e-8
+    x0b = 0.5 * x0
+    assert s.chock(x0b, max_iters=15, tol=0.0, step_size=alpha) == 1
+    _, err2, derr2, zo2, eo2, _ = orc.chock(x0b, 15, 0.0, alpha=alpha, p0=zo, d0=eo)
+    assert trace_rel_err(s.error_cache, err2) <= 1e-8
+    assert trace_rel_err(s.delta_error_cache, derr2) <= 1e-8
+    assert rel_err(s.cache.get_primal_flat(), zo2) <= 1e-9
+    assert rel_err(s.cache.get_dual_flat(), eo2) <= 1e-9
+    # a dual set and committed before the first solve
+    s2 = core.Solver(problem_spec=prob)
+    # a dual as prox g* leaves it (placeholder slots exactly 0, as in every reference dual)
+    e0 = orc.prox_gconj(np.random.default_rng(3).standard_normal(s2.cache.dual_size), alpha)
+    s2.cache.set_dual(s2.cache._blocks_d(e0))
+    s2.cache.update_cache()
+    s2.chock(x0, max_iters=10, tol=0.0, step_size=alpha)
+    _, err3, _, zo3, _, _ = orc.chock(x0, 10, 0.0, alpha=alpha, p0=np.zeros(orc.P), d0=e0)
+    assert trace_rel_err(s2.error_cache, err3) <= 1e-8
+    assert rel_err(s2.cache.get_primal_flat(), zo3) <= 1e-9
+
+
+def test_nan_initial_state_is_not_converged(golden):
+    """A NaN in x0 on a problem without boxes: the residuals are NaN, `max(error) <= tol`
+    is false every iteration (solver.py:137-161), so the solve runs to max_iters and
+    returns 1 with NaN in the error cache (the max reductions propagate NaN)."""
+    z = golden("ops_kat")
+    r, tree, prob = problem_from_golden(z, "ops2x2")
+    s = core.Solver(problem_spec=prob)
+    x0 = r["x0"].astype(float).copy()
+    x0[0] = np.nan
+    assert s.chock(x0.reshape(-1, 1), max_iters=5, tol=1e-3, step_size=0.1) == 1
+    assert s.error_cache.shape == (6, 3)
+    assert np.isnan(s.error_cache).any()

@@ -1,7 +1,7 @@
 """GPU parity of the opt-in kernel variants (measured slower on MI355X than the defaults,
-kept correct): L / L^T as streaming wave-task kernels (raocp_ells.hip, RAOCP_ELL_STREAM=1)
-and the CP stopping test fused into k_cpp's last block (RAOCP_FUSE_CHECK=1); and the
-default per-parent L^T tiles against the LDS-staged path (RAOCP_ELLT_PARENT_TILES=0).
+kept correct): the CP stopping test fused into k_cpp's last block (RAOCP_FUSE_CHECK=1);
+and the default per-parent L^T tiles against the LDS-staged path
+(RAOCP_ELLT_PARENT_TILES=0).
 
 Tolerances as in test_gpu_parity.py.
 """
@@ -28,39 +28,6 @@ def _with_env(env, fn):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-
-
-@pytest.mark.parametrize("name", ["main", "ops2x2", "bin6", "c1n5"])
-def test_streaming_ell_matches_reference(golden, name):
-    z = golden("ops_kat")
-    r, tree, prob = problem_from_golden(z, name)
-    cache = _with_env({"RAOCP_ELL_STREAM": "1"}, lambda: core.Cache(prob))
-    op = core.Operator(cache)
-    lz = op.linop_ell(z[f"{name}/ops_z"].reshape(-1, 1)).reshape(-1)
-    assert rel_err(lz, z[f"{name}/ops_Lz"]) <= 1e-12
-    lte = op.linop_ell_transpose(z[f"{name}/ops_eta"].reshape(-1, 1)).reshape(-1)
-    assert rel_err(lte, z[f"{name}/ops_LTeta"]) <= 1e-12
-
-
-@pytest.mark.parametrize("cfg", [2, 4, "4-modes"])
-def test_streaming_ell_large_vs_oracle(cfg):
-    """config 4 with a different cost per mode: tiles mixing weight tables take the per-lane path"""
-    from oracle.raocp_oracle import OracleProblem
-    r = recipe_config(4 if cfg == "4-modes" else cfg)
-    if cfg == "4-modes":
-        r["Q"] = np.array([(1.0 + k) * q for k, q in enumerate(r["Q"])])
-        r["R"] = np.array([(2.0 + k) * q for k, q in enumerate(r["R"])])
-    tree, prob = build_problem(r)
-    cache = _with_env({"RAOCP_ELL_STREAM": "1"}, lambda: core.Cache(prob))
-    orc = OracleProblem(prob)
-    rng = np.random.default_rng(5)
-    zz = rng.standard_normal(cache.primal_size)
-    ee = rng.standard_normal(cache.dual_size)
-    lz, lte = cache.native.ell(zz), cache.native.ell_t(ee)
-    assert rel_err(lz, orc.ell(zz)) <= 1e-12
-    assert rel_err(lte, orc.ell_t(ee)) <= 1e-12
-    a, b = zz @ lte, lz @ ee
-    assert abs(a - b) <= 1e-10 * max(abs(a), 1.0)
 
 
 def test_fused_stopping_test_c2_vs_oracle():
