@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Cache: the prox oracle of the CP loop (reference: raocp/core/cache.py:8-393).
 
 Same public methods and block-list conventions as the reference, but the

@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Constraint base class (reference: raocp/core/constraints/base_constraint.py:4-118).
 
 A constraint on node variables is written as  Gamma_x x + Gamma_u u  in a set C.

@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Convex cones and their projections (reference: raocp/core/constraints/cones.py:4-230).
 
 Host-side (numpy) versions, kept for API parity and for callers that project

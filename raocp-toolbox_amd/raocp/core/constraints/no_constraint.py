@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """The inactive constraint (reference: raocp/core/constraints/no_constraint.py:4-13).
 Loaded on every node by `RAOCP`; its dual slots (eta_7 / eta_14) stay placeholders."""
 import raocp.core.constraints.base_constraint as bc

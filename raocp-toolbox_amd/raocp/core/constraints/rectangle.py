@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Box constraint lo <= [x; u] <= hi (reference: raocp/core/constraints/rectangle.py:5-69).
 
 The GPU prox of g* clips with the same bounds (`raocp_hip.h`, box tables).

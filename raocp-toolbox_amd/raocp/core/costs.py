@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Quadratic stage/terminal cost (reference: raocp/core/costs.py:4-63).
 
 The operator L only ever uses the matrix square roots; they are computed once

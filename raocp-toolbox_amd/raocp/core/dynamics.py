@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Linear dynamics x+ = A x + B u (reference: raocp/core/dynamics.py:3-25)."""
 
 __all__ = ["Dynamics"]

@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Node-type tags (reference: raocp/core/nodes.py:3-31).
 
 `Nonleaf()` / `Leaf()` instances are passed to costs and constraints to say

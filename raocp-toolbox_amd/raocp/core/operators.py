@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Linear operator L of the CP splitting and its adjoint (reference: raocp/core/operators.py:5-120).
 
 `ell` / `ell_transpose` keep the reference's block-list calling convention: the

@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Risk-averse optimal control problem builder (reference: raocp/core/raocp_spec.py:7-198).
 
 Same fluent API. One deliberate difference: the reference deep-copies the

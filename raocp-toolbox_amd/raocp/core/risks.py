@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """AVaR risk measure as a conic ambiguity set (reference: raocp/core/risks.py:5-82).
 
 For a nonleaf node with c children and conditional probabilities p:

@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Scenario trees and the stopped-Markov-chain factory
 (reference: raocp/core/scenario_tree.py:21-351).
 

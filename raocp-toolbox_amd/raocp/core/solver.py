@@ -1,3 +1,5 @@
+# SPDX-License-Identifier: Apache-2.0
+# API restated from raocp-toolbox (Apache-2.0, Moran, Zhang, Sopasakis); see NOTICE.
 """Chambolle–Pock solver (reference: raocp/core/solver.py:12-253).
 
 `chock` runs the whole loop on the GPU: step size by device Lanczos on L'L
@@ -141,12 +143,56 @@ class Solver:
             print(f"{primal[i]}\n")
 
     @staticmethod
-    def _tikz_save(name):
+    def _tikz_save(name, fallback=None):
+        """tikzplotlib.save(name) as the reference does (solver.py:199, 253); tikzplotlib is
+        optional (absent in this image): `fallback(name)` then writes the file itself."""
         try:
             import tikzplotlib
-            tikzplotlib.save(name)
-        except Exception:  # tikzplotlib is optional (absent in this image)
-            pass
+        except ImportError:
+            if fallback is not None:
+                fallback(name)
+            return
+        tikzplotlib.save(name)
+
+    def _write_residuals_tex(self, name):
+        """The pgfplots file tikzplotlib writes for plot_residuals (the layout of the
+        reference's published 4-3-residuals.tex): log-y axis, one table per xi series."""
+        ec = np.atleast_2d(self.__error_cache)
+        colors = [("steelblue31119180", "31,119,180"), ("darkorange25512714", "255,127,14"),
+                  ("forestgreen4416044", "44,160,44")]
+        pos = ec[np.isfinite(ec) & (ec > 0)]
+        lines = ["% pgfplots residual trace (layout of tikzplotlib's output for Solver.plot_residuals)",
+                 "\\begin{tikzpicture}", ""]
+        lines += [f"\\definecolor{{{c}}}{{RGB}}{{{rgb}}}" for c, rgb in colors]
+        lines += ["", "\\begin{axis}[", "legend cell align={left},", "log basis y={10},",
+                  "title={Residual values of Chambolle-Pock algorithm iterations},", "xlabel={iteration},",
+                  f"xmin={-0.05 * (len(ec) - 1)!r}, xmax={1.05 * (len(ec) - 1)!r},"]
+        if pos.size:
+            lines.append(f"ymin={float(pos.min()) / 5!r}, ymax={float(pos.max()) * 2!r},")
+        lines += ["ylabel={log(residual value)},", "ymode=log", "]"]
+        for q, (c, _) in enumerate(colors):
+            lines += [f"\\addplot [thick, {c}]", "table {%"]
+            lines += [f"{k} {float(v)!r}" for k, v in enumerate(ec[:, q])]
+            lines += ["};", f"\\addlegendentry{{xi_{q}}}"]
+        lines += ["\\end{axis}", "", "\\end{tikzpicture}", ""]
+        with open(name, "w") as f:
+            f.write("\n".join(lines))
+
+    @staticmethod
+    def read_residuals_tex(name):
+        """The three xi series of a residuals .tex file (this class's or tikzplotlib's) as a
+        (k, 3) array."""
+        series, cur = [], None
+        for line in open(name):
+            line = line.strip()
+            if line.startswith("table {"):
+                cur = []
+            elif line.startswith("};") and cur is not None:
+                series.append(cur)
+                cur = None
+            elif cur is not None and line:
+                cur.append(float(line.split()[1]))
+        return np.array(series).T
 
     def plot_residuals(self, show=True):
         import matplotlib.pyplot as plt
@@ -157,7 +203,7 @@ class Solver:
         plt.ylabel(r"log(residual value)", fontsize=12)
         plt.xlabel(r"iteration", fontsize=12)
         plt.legend(("xi_0", "xi_1", "xi_2"))
-        self._tikz_save('4-3-residuals.tex')
+        self._tikz_save('4-3-residuals.tex', self._write_residuals_tex)
         if show:
             plt.show()
 

@@ -386,3 +386,52 @@ def test_nan_initial_state_is_not_converged(golden):
     assert s.chock(x0.reshape(-1, 1), max_iters=5, tol=1e-3, step_size=0.1) == 1
     assert s.error_cache.shape == (6, 3)
     assert np.isnan(s.error_cache).any()
+
+
+def test_output_utilities_headless(golden, tmp_path, capsys, monkeypatch):
+    """Solver.plot_residuals / plot_solution / print_states / print_inputs (solver.py:173-253)
+    after main.py's solve, with the Agg backend: the residual file carries the published
+    4-3-residuals.tex trace, every leaf-to-root path of the solution plot is the solved
+    iterate, and the prints list every state / input block."""
+    import matplotlib
+    matplotlib.use("Agg")
+    import matplotlib.pyplot as plt
+    z = golden("main_trace")
+    solver, status = _run_chock(z, "main", True)
+    monkeypatch.chdir(tmp_path)
+    plt.close("all")
+    solver.plot_residuals(show=False)
+    ax = plt.gca()
+    assert [ln.get_label() for ln in ax.get_legend().get_lines()] == ["xi_0", "xi_1", "xi_2"]
+    for q, ln in enumerate(ax.get_lines()[:3]):
+        assert trace_rel_err(ln.get_ydata(), z["main/cp_error"][:, q]) <= 1e-8
+    tex = core.Solver.read_residuals_tex(str(tmp_path / "4-3-residuals.tex"))
+    assert trace_rel_err(tex, z["main/tex_trace"]) <= 1e-8
+    plt.close("all")
+    solver.plot_solution(show=False)
+    fig = plt.gcf()
+    axs = np.array(fig.axes).reshape(2, -1)
+    r, tree, prob = problem_from_golden(z, "main")
+    nx, nu = 3, 2
+    assert axs.shape == (2, nx)
+    zf = solver.cache.get_primal_flat()
+    X = zf[:tree.num_nodes * nx].reshape(-1, nx)
+    leaves = tree.nodes_at_stage(tree.num_stages - 1)
+    for e in range(nx):
+        lines = axs[0, e].get_lines()
+        assert len(lines) == len(leaves)
+        j = leaves[0]
+        path = [X[j, e]]
+        while tree.ancestor_of(j) >= 0:
+            j = tree.ancestor_of(j)
+            path.append(X[j, e])
+        assert np.allclose(lines[0].get_ydata(), path, rtol=0, atol=0)
+    for e in range(nu):
+        assert len(axs[1, e].get_lines()) == len(leaves)
+    plt.close("all")
+    capsys.readouterr()
+    solver.print_states()
+    solver.print_inputs()
+    out = capsys.readouterr().out
+    assert out.startswith("states =\n")
+    assert out.count("[[") == tree.num_nodes + tree.num_nonleaf_nodes
