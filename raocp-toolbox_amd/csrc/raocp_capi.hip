@@ -102,8 +102,13 @@ struct raocp_ctx {
     size_t ell_lds = 0, ellt_lds = 0;
     size_t lds_cpd = 0, lds_cpp = 0;
     int cp_rows = 0;             // residual partial rows the CP iteration writes
+    // MFMA CP kernels (raocp_cp2.hip): block shape, grid, LDS bytes; v1 = the scalar kernels
+    int cp2_W = 4, cp2_FB = 1, cp2_LB = 16, cp2_nbF = 0, cp2_nbL = 0;
+    size_t lds_cpd2 = 0, lds_cpp2 = 0;
+    bool cp_v1 = false;          // RAOCP_CP_V1=1: the scalar k_cpd / k_cpp (raocp_cp.hip)
     // host copies the CP tables are (re)built from (build_cp_blocks)
     std::vector<int> h_yrel, h_chs, h_nch, h_pos7, h_pos14;
+    std::vector<int> h_isq, h_isr, h_isp;  // per-node weight table indices (uniform-table blocks)
     // subtree sharding (raocp_shard_setup): R shards own contiguous blocks of the
     // subtrees rooted at the top's boundary stage sh_S; the top is replicated
     int sh_R = 1, sh_r = 0, sh_S = 0;
@@ -377,6 +382,40 @@ raocp::Bufs rotated(raocp_ctx* c, int it) {
     return raocp::Bufs{c->Z[it % 3], c->Z[(it + 1) % 3], c->Z[(it + 2) % 3], c->E[it % 2], c->E[(it + 1) % 2]};
 }
 
+// the MFMA CP kernels are instantiated per (row tiles of nx, row tiles of nu)
+template <class F, class... A>
+void dispatch_rt(int nx, int nu, F f, A... a) {
+    const int rx = (nx + 15) / 16, ru = (nu + 15) / 16;
+    if (ru == 1) {
+        if (rx == 1) f.template run<1, 1>(a...);
+        else if (rx == 2) f.template run<2, 1>(a...);
+        else if (rx == 3) f.template run<3, 1>(a...);
+        else f.template run<4, 1>(a...);
+    } else {
+        if (rx == 1) f.template run<1, 2>(a...);
+        else if (rx == 2) f.template run<2, 2>(a...);
+        else if (rx == 3) f.template run<3, 2>(a...);
+        else f.template run<4, 2>(a...);
+    }
+}
+struct Cpd2Op {
+    template <int RX, int RU>
+    void run(raocp_ctx* c) {
+        auto k = raocp::k_cpd2<double, RX, RU>;
+        allow_lds(k, c->lds_cpd2);
+        k<<<c->cp2_nbF + c->cp2_nbL, 64 * c->cp2_W, c->lds_cpd2, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
+                                                                                c->redpart, c->cp2_nbF);
+    }
+};
+struct Cpp2Op {
+    template <int RX, int RU>
+    void run(raocp_ctx* c) {
+        auto k = raocp::k_cpp2<double, RX, RU>;
+        allow_lds(k, c->lds_cpp2);
+        k<<<c->cp2_nbF + c->cp2_nbL, 64 * c->cp2_W, c->lds_cpp2, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
+                                                                                c->redpart, c->cp2_nbF);
+    }
+};
 struct CpdOp {
     template <int NX, int NU>
     void run(raocp_ctx* c) {
@@ -396,8 +435,14 @@ struct CppOp {
                                                                      c->cp_nbF, c->hist, fuse ? c->ticket : nullptr);
     }
 };
-void launch_cpd(raocp_ctx* c) { dispatch(c->nx, c->nu, CpdOp{}, c); }
-void launch_cpp(raocp_ctx* c, bool fuse = false) { dispatch(c->nx, c->nu, CppOp{}, c, fuse); }
+void launch_cpd(raocp_ctx* c) {
+    if (c->cp_v1) dispatch(c->nx, c->nu, CpdOp{}, c);
+    else dispatch_rt(c->nx, c->nu, Cpd2Op{}, c);
+}
+void launch_cpp(raocp_ctx* c, bool fuse = false) {
+    if (c->cp_v1 || fuse) dispatch(c->nx, c->nu, CppOp{}, c, fuse);
+    else dispatch_rt(c->nx, c->nu, Cpp2Op{}, c);
+}
 // RAOCP_FUSE_CHECK=1: the unsharded CP iteration runs its stopping test inside k_cpp
 bool fuse_check(const raocp_ctx* c) { return !c->comm && c->sh_R == 1 && !c->no_fuse_check; }
 
@@ -683,6 +728,61 @@ long cp_need(const raocp_ctx* c, const std::vector<std::pair<int, int>>& pr_, co
     return w;
 }
 
+// ---- MFMA CP blocks (raocp_cp2.hip): LDS bytes of one block, mirroring StgB (worst-case
+// misalignment of each region: 15 B)
+long cp2_region(long nbytes) { return nbytes > 0 ? 16 * ((nbytes + 30) >> 4) + 16 : 16; }
+std::pair<long, long> cp2_block_need(const raocp_ctx* c, bool family, int a0, int a1, bool regular) {
+    const long nx = c->nx, nu = c->nu, w = sizeof(double);
+    auto R = [&](long cnt) { return cp2_region(cnt * w); };
+    auto Rr = [&](long cnt) { return cp2_region(cnt * 16); };
+    auto Ri = [&](long cnt) { return cp2_region(cnt * 4); };
+    const long nBx = (long)c->nbn * (nx + nu), nBlx = (long)c->nbl * nx;
+    if (family) {
+        const long P = a1 - a0;
+        const CpFam f = cp_fam(c, a0, a1);
+        const long C = f.ce - f.cb, Y = f.y1 - f.y0, E7n = f.e7b - f.e7a;
+        const long nd = 2 * R(P * nx) + 2 * R(P * nu) + 2 * R(Y) + 2 * R(P) + 3 * R(C) + R(Y) + R(P) + R(E7n) +
+                        R(C * nx) + R(C * nu) + 2 * R(C) + Rr(P) + Rr(C) + Ri(P) + 2 * R(nBx);
+        long npp = 3 * (R(Y) + R(P) + R(C * nx) + R(C * nu) + 2 * R(C) + R(E7n) + 3 * R(C)) + 2 * R(P * nx) +
+                   2 * R(P * nu) + 2 * R(Y) + 5 * R(C) + R(P) + Rr(P) + Rr(C);
+        if (!regular) npp += 3 * C * (nx + nu) * w;
+        return {nd, npp};
+    }
+    const long Lc = a1 - a0;
+    const long E14n = c->h_pos14[a1 - c->m] - c->h_pos14[a0 - c->m];
+    const long nd = 2 * R(Lc * nx) + 2 * R(Lc) + R(Lc * nx) + 2 * R(Lc) + R(E14n) + Rr(Lc) + 2 * R(nBlx);
+    const long npp = 3 * (R(Lc * nx) + R(E14n)) + 2 * R(Lc * nx) + Rr(Lc);
+    return {nd, npp};
+}
+
+// largest LDS bytes of a MFMA CP block over a range of parents (families of FB) or leaves (LB)
+long cp2_need(const raocp_ctx* c, int a, int b, int per, bool family);
+
+// the uniform table index of nodes [a, b) (-1 when they differ or the range is empty)
+int uniform_idx(const std::vector<int>& idx, int a, int b) {
+    if (b <= a) return -1;
+    for (int q = a + 1; q < b; ++q)
+        if (idx[q] != idx[a]) return -1;
+    return idx[a];
+}
+
+bool cp2_regular(const raocp_ctx* c, int i0, int i1) {
+    const CpFam f = cp_fam(c, i0, i1);
+    int creg = c->h_nch[i0] <= 4 ? c->h_nch[i0] : 0;
+    for (int q = i0; q < i1 && creg; ++q)
+        if (c->h_nch[q] != creg || c->h_chs[q] != f.cb + (q - i0) * creg) creg = 0;
+    return creg > 0 && uniform_idx(c->h_isq, f.cb, f.ce) >= 0 && uniform_idx(c->h_isr, f.cb, f.ce) >= 0;
+}
+long cp2_need(const raocp_ctx* c, int a, int b, int per, bool family) {
+    long w = 0;
+    for (int x0 = a; x0 < b; x0 += per) {
+        const int x1 = std::min(b, x0 + per);
+        const auto nd = cp2_block_need(c, family, x0, x1, family ? cp2_regular(c, x0, x1) : true);
+        w = std::max(w, std::max(nd.first, nd.second));
+    }
+    return w;
+}
+
 // (re)build the CP block table for the owned parent ranges and leaf ranges
 int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& pranges,
                     const std::vector<std::pair<int, int>>& lranges) {
@@ -720,6 +820,49 @@ int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& prange
     c->lds_cpd = (size_t)need_d * 8;
     c->lds_cpp = (size_t)need_p * 8;
     c->cp_rows = c->cp_nbF + c->cp_nbL;
+    // MFMA CP blocks (raocp_cp2.hip) over the same ranges
+    {
+        std::vector<raocp::Rec> fam2, leaf2;
+        long nd2 = 0, np2 = 0;
+        for (const auto& r : pranges)
+            for (int i0 = r.first; i0 < r.second; i0 += c->cp2_FB) {
+                const int i1 = std::min(r.second, i0 + c->cp2_FB);
+                const CpFam f = cp_fam(c, i0, i1);
+                // regular: every parent has the same child count creg <= 4, children in parent order
+                int creg = c->h_nch[i0] <= 4 ? c->h_nch[i0] : 0;
+                for (int q = i0; q < i1 && creg; ++q)
+                    if (c->h_nch[q] != creg || c->h_chs[q] != f.cb + (q - i0) * creg) creg = 0;
+                fam2.push_back(raocp::Rec{f.cb, f.ce, f.y0, f.y1});
+                fam2.push_back(raocp::Rec{f.e7a, f.e7b, i0, i1});
+                const int tq = uniform_idx(c->h_isq, f.cb, f.ce), tr = uniform_idx(c->h_isr, f.cb, f.ce);
+                fam2.push_back(raocp::Rec{tq, tr, creg, 0});
+                const auto nd = cp2_block_need(c, true, i0, i1, creg > 0 && tq >= 0 && tr >= 0);
+                nd2 = std::max(nd2, nd.first);
+                np2 = std::max(np2, nd.second);
+            }
+        for (const auto& r : lranges)
+            for (int l0 = r.first; l0 < r.second; l0 += c->cp2_LB) {
+                const int l1 = std::min(r.second, l0 + c->cp2_LB);
+                leaf2.push_back(raocp::Rec{c->h_pos14[l0 - c->m], c->h_pos14[l1 - c->m], l0, l1});
+                leaf2.push_back(raocp::Rec{uniform_idx(c->h_isp, l0, l1), 0, 0, 0});
+                const auto nd = cp2_block_need(c, false, l0, l1, true);
+                nd2 = std::max(nd2, nd.first);
+                np2 = std::max(np2, nd.second);
+            }
+        if (std::max(nd2, np2) > 150 * 1024)
+            return fail(RAOCP_ERR_ARG, "MFMA CP block does not fit LDS (nx, nu or branching too large)");
+        std::vector<raocp::Rec> tab2 = fam2;
+        tab2.insert(tab2.end(), leaf2.begin(), leaf2.end());
+        if (tab2.empty()) tab2.push_back(raocp::Rec{0, 0, 0, 0});
+        const raocp::Rec* dtab2 = nullptr;
+        if ((rc = c->upload_vec(&dtab2, tab2))) return rc;
+        c->dev.cp2_tab = dtab2;
+        c->cp2_nbF = (int)fam2.size() / raocp::kCpFamRecs;
+        c->cp2_nbL = (int)leaf2.size() / raocp::kCpLeafRecs;
+        c->lds_cpd2 = (size_t)nd2;
+        c->lds_cpp2 = (size_t)np2;
+        if (!c->cp_v1) c->cp_rows = c->cp2_nbF + c->cp2_nbL;
+    }
     return RAOCP_OK;
 }
 
@@ -1235,6 +1378,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         c->h_yrel = yrel;
         c->h_chs.assign(t->ch_start, t->ch_start + m);
         c->h_nch.assign(t->nch, t->nch + m);
+        c->h_isq.assign(pr->i_sq, pr->i_sq + n);
+        c->h_isr.assign(pr->i_sr, pr->i_sr + n);
+        c->h_isp.assign(pr->i_sp, pr->i_sp + n);
         c->n_sq = pr->n_sq;
         c->n_sr = pr->n_sr;
         c->n_sp = pr->n_sp;
@@ -1260,6 +1406,31 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         while (LB > 1 && cp_need(c, {}, alll, FB, LB) > kCpLds) LB = LB * 3 / 4;
         c->cp_FB = FB;
         c->cp_LB = LB;
+        // MFMA CP kernels: W waves per block, one 16-node tile per wave and pass; W from the
+        // tile count (about two blocks per CU), at least the lanes of a parent-row group
+        if (nx > 64 || nu > 32)
+            return bail(fail(RAOCP_ERR_ARG, "the CP kernels support nx <= 64 and nu <= 32"));
+        {
+            const long tiles = (long)(n - 1 + 15) / 16 + (long)(n - m + 15) / 16;
+            int W = (int)std::max(1L, std::min(4L, tiles / 512));
+            const int lanes = std::max(2 * cmax + 2 + nx + nu, cmax + 1);
+            W = std::max(W, (lanes + 63) / 64);
+            if (const char* e = getenv("RAOCP_CP2_W")) W = std::max(W, std::min(4, atoi(e)));
+            if (W > 4) return bail(fail(RAOCP_ERR_ARG, "parent rows exceed a 256-lane CP block (branching too large)"));
+            const double cavg = (double)(n - 1) / m;
+            c->cp2_W = W;
+            c->cp2_FB = std::max(1, (int)(16.0 * W / cavg + 1e-9));
+            c->cp2_LB = 16 * W;
+            if (const char* e = getenv("RAOCP_CP2_FB")) c->cp2_FB = std::max(1, atoi(e));
+            if (const char* e = getenv("RAOCP_CP2_LB")) c->cp2_LB = std::max(1, atoi(e));
+            // within 64 KB of LDS per block (two blocks per CU)
+            const long kLds2 = 64 * 1024;
+            while (c->cp2_FB > 1 && cp2_need(c, 0, m, c->cp2_FB, true) > kLds2)
+                c->cp2_FB = std::min(c->cp2_FB - 1, c->cp2_FB * 3 / 4);
+            while (c->cp2_LB > 1 && cp2_need(c, m, n, c->cp2_LB, false) > kLds2)
+                c->cp2_LB = std::min(c->cp2_LB - 1, c->cp2_LB * 3 / 4);
+            if (const char* e = getenv("RAOCP_CP_V1")) c->cp_v1 = atoi(e) != 0;
+        }
         if ((rc = build_cp_blocks(c, allp, alll))) return bail(rc);
     }
 
@@ -1359,7 +1530,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         const int g_dual = groups(nx + nu + 2, n - 1).blocks + groups(2 * cmax + 2 + nx + nu, m).blocks +
                            groups(2 * nx + 2, n - m).blocks;
         const int g_primal = groups(nx + nu + cmax + 1, m).blocks + groups(nx, n - m).blocks;
-        c->red_rows = std::max(std::max(g_dual, g_primal), c->cp_rows);
+        c->red_rows = std::max(std::max(g_dual, g_primal), std::max(c->cp_nbF + c->cp_nbL, c->cp2_nbF + c->cp2_nbL));
         if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
         if (hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)) != hipSuccess)
             return bail(fail(RAOCP_ERR_HIP, "memset"));

@@ -83,6 +83,7 @@ struct Dev {
     const Rec* frec;       // [m] {yrel, nch, ch_start, e7off} — CP family blocks (raocp_cp.hip)
     const Rec* lrec;       // [n-m] {iSP, iBl, e14off, 0} — CP leaf blocks
     const Rec* cpd_tab;    // per CP block: family {cb, ce, y0, y1}, {e7a, e7b}; leaf {e14a, e14b}
+    const Rec* cp2_tab;    // per MFMA CP block (raocp_cp2.hip): family 3 records, leaf 2
     int nBnl, nBl;         // box table counts
     const Rec* ell_tab;    // [L / L^T blocks][kEllRecs] node ranges (raocp_ell.hip)
     const Rec* dblk;       // [child blocks of the CP kernels] {first parent, last parent, 0, 0}
@@ -868,6 +869,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
 }
 
 #include "raocp_cp.hip"
+#include "raocp_cp2.hip"
 
 // ---- element-wise dual sub-steps of prox_g* (cache.py:329-347, 392-393)
 __global__ void k_div(double* __restrict__ x, double a, int n) {

@@ -402,7 +402,7 @@ def test_output_utilities_headless(golden, tmp_path, capsys, monkeypatch):
     plt.close("all")
     solver.plot_residuals(show=False)
     ax = plt.gca()
-    assert [ln.get_label() for ln in ax.get_legend().get_lines()] == ["xi_0", "xi_1", "xi_2"]
+    assert [t.get_text() for t in ax.get_legend().get_texts()] == ["xi_0", "xi_1", "xi_2"]
     for q, ln in enumerate(ax.get_lines()[:3]):
         assert trace_rel_err(ln.get_ydata(), z["main/cp_error"][:, q]) <= 1e-8
     tex = core.Solver.read_residuals_tex(str(tmp_path / "4-3-residuals.tex"))
