@@ -859,9 +859,17 @@ int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& prange
         c->dev.cp2_tab = dtab2;
         c->cp2_nbF = (int)fam2.size() / raocp::kCpFamRecs;
         c->cp2_nbL = (int)leaf2.size() / raocp::kCpLeafRecs;
+        // the MFMA kernels need every block's nodes on one weight table (per-mode tables the
+        // packer could not merge): otherwise the scalar kernels (raocp_cp.hip) run
+        for (int b = 0; b < c->cp2_nbF; ++b)
+            if (fam2[raocp::kCpFamRecs * b].y > fam2[raocp::kCpFamRecs * b].x &&
+                (fam2[raocp::kCpFamRecs * b + 2].x < 0 || fam2[raocp::kCpFamRecs * b + 2].y < 0))
+                c->cp_v1 = true;
+        for (int b = 0; b < c->cp2_nbL; ++b)
+            if (leaf2[raocp::kCpLeafRecs * b + 1].x < 0) c->cp_v1 = true;
         c->lds_cpd2 = (size_t)nd2;
         c->lds_cpp2 = (size_t)np2;
-        if (!c->cp_v1) c->cp_rows = c->cp2_nbF + c->cp2_nbL;
+        c->cp_rows = c->cp_v1 ? c->cp_nbF + c->cp_nbL : c->cp2_nbF + c->cp2_nbL;
     }
     return RAOCP_OK;
 }
@@ -1200,6 +1208,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         const std::vector<int>& pp = c->pair_ptr;
         const int PS = c->PS;
         auto stage_n = [&](int st) { return c->stage_ptr[st + 1] - c->stage_ptr[st]; };
+        int n_cus = 0;
+        if (hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cus <= 0)
+            n_cus = 256;
         auto level_cost = [&](double P, double C) { return 3.0 + (C * R + P * R + P * nu + C * nx) / 384.0; };
         auto recs = [](size_t cnt) { return 2 * cnt; };  // 16-B records in doubles
         // fold: one-phase backward levels (per-pair WT tables instead of per-kind W, no P rows)
@@ -1256,6 +1267,17 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 w.fl = false;
                 w.bf -= 8 * npr * F1;
                 w.cost += 2 * (b - a);
+            }
+            // the tier's subtrees run as rounds of co-resident workgroups (two 1024-lane
+            // workgroups per CU at most, fewer when their LDS does not fit): every round
+            // pays the levels again (measured at configs 3 / 4: deep tiers of thousands of
+            // subtrees lost to one-level tiers)
+            {
+                const size_t lds = std::max(w.bb, w.bf);
+                const long per_cu = std::max<long>(1, std::min<long>(2, lds ? (long)(160 * 1024 / lds) : 2));
+                const long nsub = c->stage_ptr[a + 1] - c->stage_ptr[a];
+                const long rounds = (nsub + (long)n_cus * per_cu - 1) / ((long)n_cus * per_cu);
+                w.cost *= (double)std::max<long>(1, rounds);
             }
             w.cost += 10.0;  // two launches and their prologues
             w.ok = w.bb <= kLds && w.bf <= kLds;
@@ -1411,11 +1433,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         if (nx > 64 || nu > 32)
             return bail(fail(RAOCP_ERR_ARG, "the CP kernels support nx <= 64 and nu <= 32"));
         {
-            const long tiles = (long)(n - 1 + 15) / 16 + (long)(n - m + 15) / 16;
-            int W = (int)std::max(1L, std::min(4L, tiles / 512));
+            // four waves per block measured faster than one or two at configs 2 and 4 (the
+            // per-block gather and barriers amortise over more tiles)
+            int W = 4;
             const int lanes = std::max(2 * cmax + 2 + nx + nu, cmax + 1);
             W = std::max(W, (lanes + 63) / 64);
-            if (const char* e = getenv("RAOCP_CP2_W")) W = std::max(W, std::min(4, atoi(e)));
+            if (const char* e = getenv("RAOCP_CP2_W")) W = std::max((lanes + 63) / 64, std::min(4, atoi(e)));
             if (W > 4) return bail(fail(RAOCP_ERR_ARG, "parent rows exceed a 256-lane CP block (branching too large)"));
             const double cavg = (double)(n - 1) / m;
             c->cp2_W = W;
@@ -1429,6 +1452,11 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 c->cp2_FB = std::min(c->cp2_FB - 1, c->cp2_FB * 3 / 4);
             while (c->cp2_LB > 1 && cp2_need(c, m, n, c->cp2_LB, false) > kLds2)
                 c->cp2_LB = std::min(c->cp2_LB - 1, c->cp2_LB * 3 / 4);
+            // small trees (config 2: 8,191 nodes, ~770 tiles) run the scalar kernels, which
+            // spread a latency-bound launch over more lanes (measured 17.0 / 21.1 us vs 21.3 /
+            // 23.6 us for k_cpd / k_cpp); from ~4k tiles the MFMA kernels win (config 4:
+            // 200 / 196 us vs 210 / 318 us; config 3 464 vs 505 us per iteration)
+            c->cp_v1 = (long)(n - 1 + 15) / 16 + (long)(n - m + 15) / 16 < 4096;
             if (const char* e = getenv("RAOCP_CP_V1")) c->cp_v1 = atoi(e) != 0;
         }
         if ((rc = build_cp_blocks(c, allp, alll))) return bail(rc);
@@ -1553,6 +1581,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
     c->dev.dyn_regtab = 0;  // RAOCP_DYN_REGTAB=1: dynamics tables by vector loads instead of LDS-DMA
     if (const char* e = getenv("RAOCP_DYN_REGTAB")) c->dev.dyn_regtab = atoi(e) != 0;
+    c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels
+    if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = atoi(e);
     c->dev.regstage = 0;  // RAOCP_REGSTAGE=1: k_ell's gather by vector loads (measured slower)
     if (const char* e = getenv("RAOCP_REGSTAGE")) c->dev.regstage = atoi(e) != 0;
     if ((rc = c->alloc(&c->ticket, 64))) return bail(rc);

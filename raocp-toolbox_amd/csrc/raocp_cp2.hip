@@ -12,7 +12,8 @@
 // LDS by LDS-DMA (one memory round trip; ranges are contiguous in the BFS numbering),
 // while each wave loads the weight fragments of its tiles into registers (the tables
 // are per mode and deduplicated, so a block's children usually share one table: the
-// host flags the block's table index, -1 when mixed). Then:
+// host flags the block's table index; a tree with a block whose nodes use different
+// tables runs the scalar kernels of raocp_cp.hip instead). Then:
 //   * the products sqrtQ x_anc(j), sqrtR u_anc(j) (k_cpd2), sqrtQ eta3_j, sqrtR eta4_j
 //     (k_cpp2) and sqrtPf x_l / sqrtPf eta11_l are 16-node x 16-row MFMA tiles
 //     (v_mfma_f64_16x16x4f64 / v_mfma_f32_16x16x4f32), one tile per wave;
@@ -188,36 +189,10 @@ __device__ __forceinline__ void tile3(const WFr<T, RT>& wf, int n, AF afun, type
     }
 }
 
-// Mixed tables (the block's nodes do not share one): the same accumulator slots by
-// per-lane dot products; node(e) gives the tile row's node (or -1), tab(node) its table,
-// vfun(node, k, v1, v2, v3) its A values.
-template <class T, int RT, int NS, class NF, class TF, class VF>
-__device__ __forceinline__ void tile_mixed(const T* tabs, int n, NF node, TF tab, VF vfun,
-                                           typename MF<T>::v4 (*acc)[RT]) {
-    const int lo = threadIdx.x & 15;
-    _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-        const int nd = node(e);
-        _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) {
-            const int r = 16 * rt + lo;
-            T s[NS];
-            _Pragma("unroll") for (int q = 0; q < NS; ++q) s[q] = T(0);
-            if (nd >= 0 && r < n) {
-                cglbp<T> M = (cglbp<T>)(tabs + (size_t)tab(nd) * n * n) + r;
-                for (int k = 0; k < n; ++k) {
-                    T v[3] = {T(0), T(0), T(0)};
-                    vfun(nd, k, v[0], v[1], v[2]);
-                    const T m = M[k * n];
-                    _Pragma("unroll") for (int q = 0; q < NS; ++q) s[q] = fma(m, v[q], s[q]);
-                }
-            }
-            _Pragma("unroll") for (int q = 0; q < NS; ++q) acc[q][rt][e] = s[q];
-        }
-    }
-}
-
 // block table of the CP kernels (host: build_cp_blocks): per family block
 //   {cb, ce, y0, y1}, {e7a, e7b, i0, i1}, {SQ table, SR table, regular child count, 0}
-// and per leaf block {e14a, e14b, l0, l1}, {SP table, 0, 0, 0}; tables -1 when mixed.
+// and per leaf block {e14a, e14b, l0, l1}, {SP table, 0, 0, 0} (always uniform tables: the
+// host falls back to raocp_cp.hip otherwise).
 constexpr int kCpFamRecs = 3;
 constexpr int kCpLeafRecs = 2;
 
@@ -255,11 +230,11 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
     const crec4* tab = (const crec4*)p.cp2_tab;
     StgB st{(ldsd*)smem_};
     double m2 = 0.0, m5 = 0.0;
-    T alpha = T(0);
+    T alpha = T(0), ra = T(0);  // alpha and 1 / alpha (products instead of divisions: 1 ulp)
     auto finish = [&](int e, T dv, T v, T pv, T b) {
         const T ep = alpha * (v - pv);
         eo[e] = ep;
-        const T x2 = (dv - ep) / alpha + b;
+        const T x2 = (dv - ep) * ra + b;
         xi2[e] = x2;
         m2 = nmax(m2, (double)fabs(x2));
         m5 = nmax(m5, (double)fabs(ep - dv));
@@ -299,11 +274,12 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
         if (tr >= 0) wr.load((const T*)p.SR, tr, nu);
         const int done = ctl->done;
         alpha = (T)ctl->alpha;
+        ra = T(1) / alpha;
         dma_wait();
         lds_sync();
         if (done) return;
         // (1) child tiles: eta3 (nx), eta4 (nu), eta5, eta6 -> one SOC of dim nx + nu + 2
-        const int ntc = (C + 15) >> 4;
+        const int ntc = (p.cp_dbg & 1) ? 0 : (C + 15) >> 4;
         for (int t = wv; t < ntc; t += nw) {
             const int j0 = 16 * t, ja = j0 + lo;
             const bool la = ja < C;
@@ -311,10 +287,6 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
             v4 ax[RTX], bx[RTX], au[RTU], bu[RTU];
             _Pragma("unroll") for (int r = 0; r < RTX; ++r) ax[r] = bx[r] = v4{0, 0, 0, 0};
             _Pragma("unroll") for (int r = 0; r < RTU; ++r) au[r] = bu[r] = v4{0, 0, 0, 0};
-            auto node = [&](int e) {
-                const int jn = j0 + MF<T>::row(h, e);
-                return jn < C ? jn : -1;
-            };
             if (tq >= 0) {
                 tile2<T, RTX>(wq, nx, [&](int k, T& a1, T& a2) {
                     if (la) {
@@ -323,16 +295,6 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                         a2 = z - q;
                     }
                 }, ax, bx);
-            } else {
-                v4 acc[2][RTX];
-                tile_mixed<T, RTX, 2>((const T*)p.SQ, nx, node, [&](int jn) { return CR[jn].y; },
-                                      [&](int jn, int k, T& a1, T& a2, T&) {
-                                          const int ai = CR[jn].x - i0;
-                                          const T z = Xz[ai * nx + k], q = Xp[ai * nx + k];
-                                          a1 = T(2) * z - q;
-                                          a2 = z - q;
-                                      }, acc);
-                _Pragma("unroll") for (int r = 0; r < RTX; ++r) { ax[r] = acc[0][r]; bx[r] = acc[1][r]; }
             }
             if (tr >= 0) {
                 tile2<T, RTU>(wr, nu, [&](int k, T& a1, T& a2) {
@@ -342,16 +304,6 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                         a2 = z - q;
                     }
                 }, au, bu);
-            } else {
-                v4 acc[2][RTU];
-                tile_mixed<T, RTU, 2>((const T*)p.SR, nu, node, [&](int jn) { return CR[jn].z; },
-                                      [&](int jn, int k, T& a1, T& a2, T&) {
-                                          const int ai = CR[jn].x - i0;
-                                          const T z = Uz[ai * nu + k], q = Up[ai * nu + k];
-                                          a1 = T(2) * z - q;
-                                          a2 = z - q;
-                                      }, acc);
-                _Pragma("unroll") for (int r = 0; r < RTU; ++r) { au[r] = acc[0][r]; bu[r] = acc[1][r]; }
             }
             // epilogue: the SOC of each of this lane group's 4 children
             _Pragma("unroll") for (int e = 0; e < 4; ++e) {
@@ -365,7 +317,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                     vx[rt] = T(0);
                     if (live && r < nx) {
                         const T dv = D3[jn * nx + r];
-                        vx[rt] = (dv + alpha * ax[rt][e]) / alpha;
+                        vx[rt] = (dv + alpha * ax[rt][e]) * ra;
                         ss += vx[rt] * vx[rt];
                     }
                 }
@@ -374,7 +326,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                     vu[rt] = T(0);
                     if (live && r < nu) {
                         const T dv = D4[jn * nu + r];
-                        vu[rt] = (dv + alpha * au[rt][e]) / alpha;
+                        vu[rt] = (dv + alpha * au[rt][e]) * ra;
                         ss += vu[rt] * vu[rt];
                     }
                 }
@@ -387,8 +339,8 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                     a5 = T(0.5) * (T(2) * zt - pt);
                     b5 = T(0.5) * (zt - pt);
                 }
-                const T v5 = (d5 + alpha * a5) / alpha + T(-0.5);
-                const T v6 = (d6 + alpha * a5) / alpha + T(0.5);
+                const T v5 = (d5 + alpha * a5) * ra + T(-0.5);
+                const T v6 = (d6 + alpha * a5) * ra + T(0.5);
                 ss += v5 * v5;
                 const T nf = sqrt(ss), tt = v6;
                 if (live) {
@@ -408,7 +360,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
             }
         }
         // (2) parent rows eta1 (2c+1), eta2, eta7 (nx+nu): lanes over rows
-        {
+        if (!(p.cp_dbg & 2)) {
             const int G = 2 * p.cmax + 2 + nx + nu, per = blockDim.x / G;
             const int gl = tid / G, r = tid - gl * G;
             for (int q0 = 0; q0 < P; q0 += per) {
@@ -420,7 +372,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                     const T zy = Yz[yo + r], py = Yp[yo + r];
                     const T av = T(2) * zy - py, bb = zy - py;
                     const T dv = D1[yo + r];
-                    const T v = (dv + alpha * av) / alpha;
+                    const T v = (dv + alpha * av) * ra;
                     finish(p.E1 + fr.x + r, dv, v, r < 2 * c ? fmax(v, T(0)) : v, bb);
                 } else if (r == 2 * p.cmax + 1) {
                     T bya = T(0), byb = T(0);
@@ -434,7 +386,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                     const T zs = Sz[ii], ps = Sp[ii];
                     const T av = (T(2) * zs - ps) - bya, bb = (zs - ps) - byb;
                     const T dv = D2[ii];
-                    const T v = (dv + alpha * av) / alpha;
+                    const T v = (dv + alpha * av) * ra;
                     finish(p.E2 + i, dv, v, fmax(v, T(0)), bb);
                 } else if (r >= 2 * p.cmax + 2 && fr.w >= 0) {
                     const int rr = r - (2 * p.cmax + 2);
@@ -442,7 +394,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                     const T pv_ = rr < nx ? Xp[ii * nx + rr] : Up[ii * nu + rr - nx];
                     const T av = T(2) * zv - pv_, bb = zv - pv_;
                     const T dv = D7[fr.w - e7a + rr];
-                    const T v = (dv + alpha * av) / alpha;
+                    const T v = (dv + alpha * av) * ra;
                     const int bi = BI[ii];
                     finish(fr.w + rr, dv, v, box_apply_t(v, BL[bi * (nx + nu) + rr], BH[bi * (nx + nu) + rr], ctl), bb);
                 }
@@ -471,10 +423,11 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
         if (tp >= 0) wp.load((const T*)p.SP, tp, nx);
         const int done = ctl->done;
         alpha = (T)ctl->alpha;
+        ra = T(1) / alpha;
         dma_wait();
         lds_sync();
         if (done) return;
-        const int ntl = (Lc + 15) >> 4;
+        const int ntl = (p.cp_dbg & 4) ? 0 : (Lc + 15) >> 4;
         for (int t = wv; t < ntl; t += nw) {
             const int q0 = 16 * t, qa = q0 + lo;
             const bool la = qa < Lc;
@@ -488,20 +441,6 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                         a2 = z - q;
                     }
                 }, ax, bx);
-            } else {
-                v4 acc[2][RTX];
-                tile_mixed<T, RTX, 2>((const T*)p.SP, nx,
-                                      [&](int e) {
-                                          const int qn = q0 + MF<T>::row(h, e);
-                                          return qn < Lc ? qn : -1;
-                                      },
-                                      [&](int qn) { return LR[qn].x; },
-                                      [&](int qn, int k, T& a1, T& a2, T&) {
-                                          const T z = Xz[qn * nx + k], q = Xp[qn * nx + k];
-                                          a1 = T(2) * z - q;
-                                          a2 = z - q;
-                                      }, acc);
-                _Pragma("unroll") for (int r = 0; r < RTX; ++r) { ax[r] = acc[0][r]; bx[r] = acc[1][r]; }
             }
             _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 const int qn = q0 + MF<T>::row(h, e);
@@ -513,7 +452,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                     const int r = 16 * rt + lo;
                     vx[rt] = T(0);
                     if (live && r < nx) {
-                        vx[rt] = (D11[qn * nx + r] + alpha * ax[rt][e]) / alpha;
+                        vx[rt] = (D11[qn * nx + r] + alpha * ax[rt][e]) * ra;
                         ss += vx[rt] * vx[rt];
                     }
                 }
@@ -528,8 +467,8 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                     b5 = T(0.5) * (zs - ps);
                     lr = LR[qn];
                 }
-                const T v12 = (d12 + alpha * a5) / alpha + T(-0.5);
-                const T v13 = (d13 + alpha * a5) / alpha + T(0.5);
+                const T v12 = (d12 + alpha * a5) * ra + T(-0.5);
+                const T v13 = (d13 + alpha * a5) * ra + T(0.5);
                 ss += v12 * v12;
                 const T nf = sqrt(ss), tt = v13;
                 if (live) {
@@ -540,7 +479,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
                             if (lr.z >= 0) {  // eta14 = x (box)
                                 const T zv = Xz[qn * nx + r], pv_ = Xp[qn * nx + r];
                                 const T dv = D14[lr.z - e14a + r];
-                                const T v = (dv + alpha * (T(2) * zv - pv_)) / alpha;
+                                const T v = (dv + alpha * (T(2) * zv - pv_)) * ra;
                                 finish(lr.z + r, dv, v, box_apply_t(v, BL[lr.y * nx + r], BH[lr.y * nx + r], ctl), zv - pv_);
                             }
                         }
@@ -582,10 +521,10 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
     const crec4* tab = (const crec4*)p.cp2_tab;
     StgB st{(ldsd*)smem_};
     double m0 = 0.0, m1 = 0.0, m3 = 0.0, m4 = 0.0;
-    T alpha = T(0);
+    T alpha = T(0), ra = T(0);
     // residual terms of one primal entry: pp = p, zz = z+, w = L^T(d - eta+), lc = L^T xi2
     auto account = [&](T pp, T zz, T w, T lc) {
-        const T x1 = (pp - zz) / alpha - w;
+        const T x1 = (pp - zz) * ra - w;
         const T x0v = x1 + lc;
         const T dl1 = zz - pp;
         const T dl0 = dl1 + w;
@@ -635,6 +574,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
         if (tr >= 0) wr.load((const T*)p.SR, tr, nu);
         const int done = ctl->done;
         alpha = (T)ctl->alpha;
+        ra = T(1) / alpha;
         dma_wait();
         lds_sync();
         if (done) return;
@@ -659,7 +599,8 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
             account(pp, zz, accW, accC);
         };
         // (1) x / u rows
-        if (creg > 0 && tq >= 0 && tr >= 0) {
+        if (p.cp_dbg & 1) {
+        } else if (creg > 0 && tq >= 0 && tr >= 0) {
             // regular block: per-parent tiles (4 (4 / c) parents per tile); x rows, then u rows
             const int Q = 4 / creg, PT = 4 * Q;
             const int hA = MF<T>::h_of(lo), eA = MF<T>::e_of(lo);
@@ -717,7 +658,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
                     const int j0 = 16 * t, ja = j0 + lo;
                     const bool la = ja < C;
                     v4 cc[3][RT];
-                    if (tu >= 0) {
+                    {
                         _Pragma("unroll") for (int r = 0; r < RT; ++r) cc[0][r] = cc[1][r] = cc[2][r] = v4{0, 0, 0, 0};
                         tile3<T, RT>(wf, n, [&](int k, T& a1, T& a2, T& a3) {
                             if (la) {
@@ -727,19 +668,6 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
                                 a3 = DD[2][ja * n + k];
                             }
                         }, cc[0], cc[1], cc[2]);
-                    } else {
-                        tile_mixed<T, RT, 3>(tabs, n,
-                                             [&](int e) {
-                                                 const int jn = j0 + MF<T>::row(h, e);
-                                                 return jn < C ? jn : -1;
-                                             },
-                                             [&](int jn) { return which == 0 ? CR[jn].y : CR[jn].z; },
-                                             [&](int jn, int k, T& a1, T& a2, T& a3) {
-                                                 const T va = DD[0][jn * n + k];
-                                                 a1 = va;
-                                                 a2 = DD[1][jn * n + k] - va;
-                                                 a3 = DD[2][jn * n + k];
-                                             }, cc);
                     }
                     _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                         const int jn = j0 + MF<T>::row(h, e);
@@ -774,7 +702,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
         // r_k = alpha_r y_k - y_{c+k} + y_{2c} - tau_k - s_k, w = (r - 1 sum(r) / (a + c)) / a,
         // a = alpha_r^2 + 3; y_k -= alpha_r w_k, y_{c+k} += w_k, y_{2c} -= sum(w), tau_k += w_k,
         // s_k += w_k). Lane rk < cmax: child rk; rk == cmax: y_2c (and the root's s_0).
-        {
+        if (!(p.cp_dbg & 2)) {
             const int cmax = p.cmax, G = cmax + 1, per = blockDim.x / G;
             const int gl = tid / G, rk = tid - gl * G, kb = gl * G;
             for (int q0 = 0; q0 < P; q0 += per) {
@@ -889,10 +817,11 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
         if (tp >= 0) wp.load((const T*)p.SP, tp, nx);
         const int done = ctl->done;
         alpha = (T)ctl->alpha;
+        ra = T(1) / alpha;
         dma_wait();
         lds_sync();
         if (done) return;
-        const int ntl = (Lc + 15) >> 4;
+        const int ntl = (p.cp_dbg & 4) ? 0 : (Lc + 15) >> 4;
         for (int t = wv; t < ntl; t += nw) {
             const int q0 = 16 * t, qa = q0 + lo;
             const bool la = qa < Lc;
@@ -907,19 +836,6 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
                         a3 = D11[2][qa * nx + k];
                     }
                 }, c3[0], c3[1], c3[2]);
-            } else {
-                tile_mixed<T, RTX, 3>((const T*)p.SP, nx,
-                                      [&](int e) {
-                                          const int qn = q0 + MF<T>::row(h, e);
-                                          return qn < Lc ? qn : -1;
-                                      },
-                                      [&](int qn) { return LR[qn].x; },
-                                      [&](int qn, int k, T& a1, T& a2, T& a3) {
-                                          const T va = D11[0][qn * nx + k];
-                                          a1 = va;
-                                          a2 = D11[1][qn * nx + k] - va;
-                                          a3 = D11[2][qn * nx + k];
-                                      }, c3);
             }
             _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 const int qn = q0 + MF<T>::row(h, e);

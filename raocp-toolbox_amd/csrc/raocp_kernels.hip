@@ -94,6 +94,7 @@ struct Dev {
     unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)
     int regstage;          // staging by vector loads + LDS stores instead of LDS-DMA (RAOCP_REGSTAGE)
     int dyn_regtab;        // dynamics kernels stage their matrix tables by vector loads (RAOCP_DYN_REGTAB)
+    int cp_dbg;            // timing diagnostics only (RAOCP_CP2_DBG bits): skip phases of k_cpd2 / k_cpp2
 };
 
 // diagnostic timestamp (100 MHz constant clock), thread 0 only, when enabled

@@ -28,17 +28,31 @@ DYN = ["tiers", "per_stage"]
 
 
 @contextlib.contextmanager
-def dyn_engine(mode):
-    """Contexts created inside use the tiered dynamics kernels or the per-stage fallback."""
-    old = os.environ.get("RAOCP_DYN_PER_STAGE")
-    os.environ["RAOCP_DYN_PER_STAGE"] = "1" if mode == "per_stage" else "0"
+def _env(key, value):
+    old = os.environ.get(key)
+    if value is None:
+        os.environ.pop(key, None)
+    else:
+        os.environ[key] = value
     try:
         yield
     finally:
         if old is None:
-            os.environ.pop("RAOCP_DYN_PER_STAGE", None)
+            os.environ.pop(key, None)
         else:
-            os.environ["RAOCP_DYN_PER_STAGE"] = old
+            os.environ[key] = old
+
+
+def dyn_engine(mode):
+    """Contexts created inside use the tiered dynamics kernels or the per-stage fallback."""
+    return _env("RAOCP_DYN_PER_STAGE", "1" if mode == "per_stage" else "0")
+
+
+def cp_kernels(mode):
+    """Contexts created inside use the CP kernels the library picks for the tree ("auto":
+    scalar below ~4k node tiles, MFMA above), the MFMA kernels (raocp_cp2.hip) or the
+    scalar ones (raocp_cp.hip)."""
+    return _env("RAOCP_CP_V1", {"auto": None, "mfma": "0", "scalar": "1"}[mode])
 
 
 @pytest.fixture(scope="module")
@@ -139,9 +153,9 @@ def test_prox_gconj_and_steps_match_reference(prox_kat, name):
     assert rel_err(cache.get_dual_flat(), z[f"{name}/prox_modify_halves"]) <= 1e-15
 
 
-def _run_chock(z, name, pin, dyn="tiers"):
+def _run_chock(z, name, pin, dyn="tiers", cpk="auto"):
     r, tree, prob = problem_from_golden(z, name)
-    with dyn_engine(dyn):
+    with dyn_engine(dyn), cp_kernels(cpk):
         solver = core.Solver(problem_spec=prob)
     alpha = float(z[f"{name}/cp_alpha"]) if pin else None
     status = solver.chock(initial_state=r["x0"].reshape(-1, 1), max_iters=int(z[f"{name}/cp_max_iters"]),
@@ -149,12 +163,13 @@ def _run_chock(z, name, pin, dyn="tiers"):
     return solver, status
 
 
-@pytest.mark.parametrize("pin,dyn", [(True, "tiers"), (False, "tiers"), (True, "per_stage")])
-def test_main_py_trace(golden, pin, dyn):
+@pytest.mark.parametrize("pin,dyn,cpk", [(True, "tiers", "auto"), (False, "tiers", "auto"), (True, "per_stage", "auto"),
+                                         (True, "tiers", "mfma")])
+def test_main_py_trace(golden, pin, dyn, cpk):
     """main.py end to end: 937 iterations, status 0, residual trace vs the reference's
     (which itself matches the published 4-3-residuals.tex to 3.4e-12)."""
     z = golden("main_trace")
-    solver, status = _run_chock(z, "main", pin, dyn)
+    solver, status = _run_chock(z, "main", pin, dyn, cpk)
     assert status == int(z["main/cp_status"]) == 0
     err = solver.error_cache
     assert err.shape == z["main/cp_error"].shape == (937, 3)
@@ -168,11 +183,11 @@ def test_main_py_trace(golden, pin, dyn):
         assert abs(solver.step_size - float(z["main/cp_alpha"])) <= 1e-12 * float(z["main/cp_alpha"])
 
 
-@pytest.mark.parametrize("dyn", DYN)
+@pytest.mark.parametrize("dyn,cpk", [("tiers", "auto"), ("per_stage", "auto"), ("tiers", "mfma")])
 @pytest.mark.parametrize("name", ["bin6", "c1n5", "ops2x2"])
-def test_small_trajectories(golden, name, dyn):
+def test_small_trajectories(golden, name, dyn, cpk):
     z = golden("traj_small")
-    solver, status = _run_chock(z, name, True, dyn)
+    solver, status = _run_chock(z, name, True, dyn, cpk)
     assert status == int(z[f"{name}/cp_status"])
     assert trace_rel_err(solver.error_cache, z[f"{name}/cp_error"]) <= 1e-8
     assert trace_rel_err(solver.delta_error_cache, z[f"{name}/cp_delta_error"]) <= 1e-8
@@ -215,12 +230,13 @@ def test_nan_in_box_raises(golden):
 # ---------------------------------------------------------------------------------------
 # the benchmark configuration (BASELINE configs[1]: 8,191 nodes, nx=20, nu=8) vs the oracle
 # ---------------------------------------------------------------------------------------
-@pytest.fixture(scope="module", params=DYN)
+@pytest.fixture(scope="module", params=[("tiers", "auto"), ("per_stage", "auto"), ("tiers", "mfma")],
+                ids=["tiers", "per_stage", "tiers-mfma"])
 def c2(request):
     from oracle.raocp_oracle import OracleProblem
     r = recipe_config(2)
     tree, prob = build_problem(r)
-    with dyn_engine(request.param):
+    with dyn_engine(request.param[0]), cp_kernels(request.param[1]):
         cache = core.Cache(prob)
     return r, prob, cache, OracleProblem(prob)
 
@@ -317,16 +333,21 @@ def test_projections_full_size_vs_oracle_and_idempotent(cfg, dyn):
     assert rel_err(nat.get_primal(), z2) <= 1e-12
 
 
-@pytest.mark.parametrize("cfg", [3, 4])
-def test_large_cp_trace_vs_oracle(cfg):
+@pytest.mark.parametrize("cfg,cpk", [(3, "auto"), (4, "auto"), (3, "scalar"), ("4-modes", "auto")])
+def test_large_cp_trace_vs_oracle(cfg, cpk):
     """The whole CP loop (solver.py:124-161) at the HBM-sized configs (SURVEY.md 8(d)
     config 3: Markov 4 modes, 87,381 nodes, nx = 20; config 4: branching 3, 88,573 nodes,
     nx = 32, nu = 12): the fused CP kernels, the dynamics tiers and prox g* at those sizes,
     10 iterations against the oracle; then prox g* alone on a random dual."""
     from oracle.raocp_oracle import OracleProblem
-    r = recipe_config(cfg)
+    r = recipe_config(4 if cfg == "4-modes" else cfg)
+    if cfg == "4-modes":  # a cost per mode: blocks mixing weight tables (scalar kernels)
+        r["Q"] = np.array([(1.0 + k) * q for k, q in enumerate(r["Q"])])
+        r["R"] = np.array([(2.0 + k) * q for k, q in enumerate(r["R"])])
     tree, prob = build_problem(r)
-    cache, orc = core.Cache(prob), OracleProblem(prob)
+    with cp_kernels(cpk):
+        cache = core.Cache(prob)
+    orc = OracleProblem(prob)
     alpha = 0.999 / cache.native.step_size()
     status, err, derr = cache.native.cp_run(r["x0"], 9, 0.0, alpha)
     st_o, err_o, derr_o, z_o, e_o, _ = orc.chock(r["x0"], 9, 0.0, alpha=alpha)
