@@ -87,7 +87,14 @@ typedef struct {
     const int32_t* i_a;     /* [n] */
     const int32_t* i_b;     /* [n] */
     const int32_t* i_k;     /* [m] class of nonleaf node i */
+    /* arithmetic of the context: RAOCP_F64 (the reference's) or RAOCP_F32 (BASELINE
+     * configs[4]: iterate, tables and products in fp32; vectors still cross the host
+     * boundary as fp64 arrays, device pointers (RAOCP_DEVICE_PTR) are then float*) */
+    int32_t dtype;
 } raocp_problem_desc;
+
+#define RAOCP_F64 0
+#define RAOCP_F32 1
 
 /* Create a context on HIP device `device`: validates the tree, uploads all tables
  * to HBM, allocates the iterate and work buffers. Replaces Cache.__init__

@@ -47,6 +47,9 @@ constexpr int kGraphBatch = 24;
 
 struct raocp_ctx {
     int device = 0;
+    bool f32 = false;            // RAOCP_F32: iterate, tables and products in fp32
+    bool dyn32 = false;          // the per-stage T-templated dynamics (raocp_dyn2.hip) is planned
+    int wsz = 8;                 // bytes per scalar of the iterate
     hipStream_t stream = nullptr;
     Dev dev{};
     int n = 0, m = 0, nx = 0, nu = 0, cmax = 0, N = 0;
@@ -197,17 +200,43 @@ int check_group(int G, const char* what) {
     return RAOCP_OK;
 }
 
+// host fp64 arrays <-> the context's device vectors (fp32 contexts convert on the host;
+// a device pointer is taken in the context's own type)
 int copy_in(raocp_ctx* c, double* dst, const double* src, size_t count, int flags) {
-    HIPCHK(hipMemcpyAsync(dst, src, count * sizeof(double),
+    if (c->f32 && !(flags & RAOCP_DEVICE_PTR)) {
+        std::vector<float> tmp(src, src + count);
+        HIPCHK(hipMemcpyAsync(dst, tmp.data(), count * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        return RAOCP_OK;
+    }
+    HIPCHK(hipMemcpyAsync(dst, src, count * c->wsz,
                           (flags & RAOCP_DEVICE_PTR) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->stream));
     return RAOCP_OK;
 }
 
 int copy_out(raocp_ctx* c, double* dst, const double* src, size_t count, int flags) {
-    HIPCHK(hipMemcpyAsync(dst, src, count * sizeof(double),
+    if (c->f32 && !(flags & RAOCP_DEVICE_PTR)) {
+        std::vector<float> tmp(count);
+        HIPCHK(hipMemcpyAsync(tmp.data(), src, count * sizeof(float), hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+        std::copy(tmp.begin(), tmp.end(), dst);
+        return RAOCP_OK;
+    }
+    HIPCHK(hipMemcpyAsync(dst, src, count * c->wsz,
                           (flags & RAOCP_DEVICE_PTR) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c->stream));
     if (!(flags & RAOCP_DEVICE_PTR)) HIPCHK(hipStreamSynchronize(c->stream));
     return RAOCP_OK;
+}
+
+// a table as the context's scalar type (fp32 contexts keep float arrays in the Dev's
+// double* fields; only the T-templated kernels read them)
+int upload_t(raocp_ctx* c, const double** dst, const std::vector<double>& v) {
+    if (!c->f32) return c->upload_vec(dst, v);
+    std::vector<float> f(v.begin(), v.end());
+    const float* p = nullptr;
+    int rc = c->upload_vec(&p, f);
+    *dst = (const double*)p;
+    return rc;
 }
 
 // ---- template dispatch on (nx, nu): exact sizes get fully unrolled kernels,
@@ -221,6 +250,22 @@ void dispatch(int nx, int nu, F f, A... a) {
     else f.template run<0, 0>(a...);
 }
 
+// the MFMA CP kernels are instantiated per (row tiles of nx, row tiles of nu)
+template <class F, class... A>
+void dispatch_rt(int nx, int nu, F f, A... a) {
+    const int rx = (nx + 15) / 16, ru = (nu + 15) / 16;
+    if (ru == 1) {
+        if (rx == 1) f.template run<1, 1>(a...);
+        else if (rx == 2) f.template run<2, 1>(a...);
+        else if (rx == 3) f.template run<3, 1>(a...);
+        else f.template run<4, 1>(a...);
+    } else {
+        if (rx == 1) f.template run<1, 2>(a...);
+        else if (rx == 2) f.template run<2, 2>(a...);
+        else if (rx == 3) f.template run<3, 2>(a...);
+        else f.template run<4, 2>(a...);
+    }
+}
 template <class K>
 void allow_lds(K kernel, size_t bytes) {
     if (bytes > 64 * 1024) (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -236,7 +281,25 @@ struct EllOp {
         if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ell_lds, c->stream>>>(c->dev, z, eta);
     }
 };
-void launch_ell(raocp_ctx* c, const double* z, double* eta) { dispatch(c->nx, c->nu, EllOp{}, c, z, eta); }
+template <class T>
+struct Ell2Op {
+    template <int RX, int RU>
+    void run(raocp_ctx* c, const double* z, double* eta, bool t) {
+        if (t) {
+            auto k = raocp::k_ellt2<T, RX, RU>;
+            allow_lds(k, c->lds_cpp2);
+            k<<<c->cp2_nbF + c->cp2_nbL, 64 * c->cp2_W, c->lds_cpp2, c->stream>>>(c->dev, z, eta, c->cp2_nbF);
+        } else {
+            auto k = raocp::k_ell2<T, RX, RU>;
+            allow_lds(k, c->lds_cpd2);
+            k<<<c->cp2_nbF + c->cp2_nbL, 64 * c->cp2_W, c->lds_cpd2, c->stream>>>(c->dev, z, eta, c->cp2_nbF);
+        }
+    }
+};
+void launch_ell(raocp_ctx* c, const double* z, double* eta) {
+    if (c->f32) dispatch_rt(c->nx, c->nu, Ell2Op<float>{}, c, z, eta, false);
+    else dispatch(c->nx, c->nu, EllOp{}, c, z, eta);
+}
 
 struct EllTOp {
     template <int NX, int NU>
@@ -246,7 +309,10 @@ struct EllTOp {
         if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ellt_lds, c->stream>>>(c->dev, eta, z);
     }
 };
-void launch_ell_t(raocp_ctx* c, const double* eta, double* z) { dispatch(c->nx, c->nu, EllTOp{}, c, eta, z); }
+void launch_ell_t(raocp_ctx* c, const double* eta, double* z) {
+    if (c->f32) dispatch_rt(c->nx, c->nu, Ell2Op<float>{}, c, eta, z, true);
+    else dispatch(c->nx, c->nu, EllTOp{}, c, eta, z);
+}
 
 struct DynOp {
     // part: 0 whole projection; 1 the tiers' backward sweeps only; 2 the top and the
@@ -382,22 +448,6 @@ raocp::Bufs rotated(raocp_ctx* c, int it) {
     return raocp::Bufs{c->Z[it % 3], c->Z[(it + 1) % 3], c->Z[(it + 2) % 3], c->E[it % 2], c->E[(it + 1) % 2]};
 }
 
-// the MFMA CP kernels are instantiated per (row tiles of nx, row tiles of nu)
-template <class F, class... A>
-void dispatch_rt(int nx, int nu, F f, A... a) {
-    const int rx = (nx + 15) / 16, ru = (nu + 15) / 16;
-    if (ru == 1) {
-        if (rx == 1) f.template run<1, 1>(a...);
-        else if (rx == 2) f.template run<2, 1>(a...);
-        else if (rx == 3) f.template run<3, 1>(a...);
-        else f.template run<4, 1>(a...);
-    } else {
-        if (rx == 1) f.template run<1, 2>(a...);
-        else if (rx == 2) f.template run<2, 2>(a...);
-        else if (rx == 3) f.template run<3, 2>(a...);
-        else f.template run<4, 2>(a...);
-    }
-}
 struct Cpd2Op {
     template <int RX, int RU>
     void run(raocp_ctx* c) {
@@ -586,9 +636,9 @@ int ensure_hist(raocp_ctx* c, size_t rows) {
 int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double alpha, bool warm = false) {
     if (warm) {
         if (c->cur_z != c->Z[0])
-            HIPCHK(hipMemcpyAsync(c->Z[0], c->cur_z, c->P * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->Z[0], c->cur_z, c->P * c->wsz, hipMemcpyDeviceToDevice, c->stream));
         if (c->cur_e != c->E[0])
-            HIPCHK(hipMemcpyAsync(c->E[0], c->cur_e, c->D * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(c->E[0], c->cur_e, c->D * c->wsz, hipMemcpyDeviceToDevice, c->stream));
     } else {
         HIPCHK(hipMemsetAsync(c->Z[0], 0, c->P * sizeof(double), c->stream));
         HIPCHK(hipMemsetAsync(c->E[0], 0, c->D * sizeof(double), c->stream));
@@ -596,8 +646,16 @@ int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double al
     for (int b = 1; b < 3; ++b) HIPCHK(hipMemsetAsync(c->Z[b], 0, c->P * sizeof(double), c->stream));
     HIPCHK(hipMemsetAsync(c->E[1], 0, c->D * sizeof(double), c->stream));
     HIPCHK(hipMemsetAsync(c->XI2, 0, c->D * sizeof(double), c->stream));
-    HIPCHK(hipMemcpyAsync(c->Z[0] + c->dev.X0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(hipMemcpyAsync(c->x0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    if (c->f32) {
+        const std::vector<float> f(x0, x0 + c->nx);
+        HIPCHK(hipMemcpyAsync((float*)c->Z[0] + c->dev.X0, f.data(), c->nx * sizeof(float), hipMemcpyHostToDevice,
+                              c->stream));
+        HIPCHK(hipMemcpyAsync(c->x0, f.data(), c->nx * sizeof(float), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));  // f leaves scope
+    } else {
+        HIPCHK(hipMemcpyAsync(c->Z[0] + c->dev.X0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
+        HIPCHK(hipMemcpyAsync(c->x0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice, c->stream));
+    }
     Ctl h{};
     h.alpha = alpha;
     h.k = 0;
@@ -732,7 +790,7 @@ long cp_need(const raocp_ctx* c, const std::vector<std::pair<int, int>>& pr_, co
 // misalignment of each region: 15 B)
 long cp2_region(long nbytes) { return nbytes > 0 ? 16 * ((nbytes + 30) >> 4) + 16 : 16; }
 std::pair<long, long> cp2_block_need(const raocp_ctx* c, bool family, int a0, int a1, bool regular) {
-    const long nx = c->nx, nu = c->nu, w = sizeof(double);
+    const long nx = c->nx, nu = c->nu, w = c->wsz;
     auto R = [&](long cnt) { return cp2_region(cnt * w); };
     auto Rr = [&](long cnt) { return cp2_region(cnt * 16); };
     auto Ri = [&](long cnt) { return cp2_region(cnt * 4); };
@@ -867,6 +925,9 @@ int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& prange
                 c->cp_v1 = true;
         for (int b = 0; b < c->cp2_nbL; ++b)
             if (leaf2[raocp::kCpLeafRecs * b + 1].x < 0) c->cp_v1 = true;
+        if (c->f32 && c->cp_v1)
+            return fail(RAOCP_ERR_ARG, "fp32 contexts need the nodes of every CP block on one weight table "
+                                       "(costs that differ per mode within a family)");
         c->lds_cpd2 = (size_t)nd2;
         c->lds_cpp2 = (size_t)np2;
         c->cp_rows = c->cp_v1 ? c->cp_nbF + c->cp_nbL : c->cp2_nbF + c->cp2_nbL;
@@ -943,9 +1004,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         int d;
         ~Restore() { if (d >= 0) (void)hipSetDevice(d); }
     } restore_{prev_dev != device ? prev_dev : -1};
+    if (pr->dtype != RAOCP_F64 && pr->dtype != RAOCP_F32) return fail(RAOCP_ERR_ARG, "dtype must be RAOCP_F64 or RAOCP_F32");
     raocp_ctx* c = new raocp_ctx();
     c->device = device;
     c->n = n; c->m = m; c->nx = nx; c->nu = nu; c->cmax = cmax; c->N = N;
+    c->f32 = pr->dtype == RAOCP_F32;
+    c->wsz = c->f32 ? 4 : 8;
     auto bail = [&](int code) { raocp_ctx_destroy(c); return code; };
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(RAOCP_ERR_HIP, "hipStreamCreate failed"));
@@ -1021,16 +1085,16 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         (rc = c->upload_vec(&D.nch, nch)) || (rc = c->upload_vec(&D.rank, rank)) || (rc = c->upload_vec(&D.yrel, yrel)) ||
         (rc = c->upload_vec(&D.e7off, e7off)) || (rc = c->upload_vec(&D.e14off, e14off)))
         return bail(rc);
-    if ((rc = c->upload_vec(&D.SQ, to_colmajor(pr->sqrt_q, pr->n_sq, nx, nx))) ||
-        (rc = c->upload_vec(&D.SR, to_colmajor(pr->sqrt_r, pr->n_sr, nu, nu))) ||
-        (rc = c->upload_vec(&D.SP, to_colmajor(pr->sqrt_pf, pr->n_sp, nx, nx))) ||
+    if ((rc = upload_t(c, &D.SQ, to_colmajor(pr->sqrt_q, pr->n_sq, nx, nx))) ||
+        (rc = upload_t(c, &D.SR, to_colmajor(pr->sqrt_r, pr->n_sr, nu, nu))) ||
+        (rc = upload_t(c, &D.SP, to_colmajor(pr->sqrt_pf, pr->n_sp, nx, nx))) ||
         (rc = c->upload(&D.SQr, pr->sqrt_q, (size_t)pr->n_sq * nx * nx)) ||
         (rc = c->upload(&D.SRr, pr->sqrt_r, (size_t)pr->n_sr * nu * nu)) ||
         (rc = c->upload(&D.SPr, pr->sqrt_pf, (size_t)pr->n_sp * nx * nx)) ||
         (rc = c->upload(&D.iSQ, pr->i_sq, n)) || (rc = c->upload(&D.iSR, pr->i_sr, n)) ||
-        (rc = c->upload(&D.iSP, pr->i_sp, n)) || (rc = c->upload(&D.alpha_r, pr->alpha_r, m)) ||
+        (rc = c->upload(&D.iSP, pr->i_sp, n)) || (rc = upload_t(c, &D.alpha_r, copy_table(pr->alpha_r, m))) ||
         ((D.nSQ = pr->n_sq), (D.nSR = pr->n_sr), (D.nSP = pr->n_sp), false) ||
-        (rc = c->upload(&D.cond, pr->cond, n)))
+        (rc = upload_t(c, &D.cond, copy_table(pr->cond, n))))
         return bail(rc);
     const int nbn = std::max(1, pr->n_box_nl), nbl = std::max(1, pr->n_box_l);
     std::vector<double> lo_nl(nbn * (nx + nu), 0.0), hi_nl(nbn * (nx + nu), 0.0), lo_l(nbl * nx, 0.0), hi_l(nbl * nx, 0.0);
@@ -1042,8 +1106,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         std::copy(pr->box_l_lo, pr->box_l_lo + lo_l.size(), lo_l.begin());
         std::copy(pr->box_l_hi, pr->box_l_hi + hi_l.size(), hi_l.begin());
     }
-    if ((rc = c->upload_vec(&D.blo_nl, lo_nl)) || (rc = c->upload_vec(&D.bhi_nl, hi_nl)) ||
-        (rc = c->upload_vec(&D.blo_l, lo_l)) || (rc = c->upload_vec(&D.bhi_l, hi_l)) ||
+    if ((rc = upload_t(c, &D.blo_nl, lo_nl)) || (rc = upload_t(c, &D.bhi_nl, hi_nl)) ||
+        (rc = upload_t(c, &D.blo_l, lo_l)) || (rc = upload_t(c, &D.bhi_l, hi_l)) ||
         (rc = c->upload(&D.iBnl, pr->i_box_nl, m)) || (rc = c->upload(&D.iBl, pr->i_box_l, n)))
         return bail(rc);
     // dynamics tables (raocp_dyn.hip header): per child kind W = [B'; A'], per class
@@ -1458,6 +1522,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             // 200 / 196 us vs 210 / 318 us; config 3 464 vs 505 us per iteration)
             c->cp_v1 = (long)(n - 1 + 15) / 16 + (long)(n - m + 15) / 16 < 4096;
             if (const char* e = getenv("RAOCP_CP_V1")) c->cp_v1 = atoi(e) != 0;
+            if (c->f32) c->cp_v1 = false;  // only the T-templated kernels run fp32
         }
         if ((rc = build_cp_blocks(c, allp, alll))) return bail(rc);
     }
@@ -1675,13 +1740,19 @@ int raocp_set_initial_state(raocp_ctx* c, const double* x0) {
     DevGuard dg_(c);
     if (!c || !x0) return fail(RAOCP_ERR_ARG, "null argument");
     c->h_x0.assign(x0, x0 + c->nx);
-    HIPCHK(hipMemcpy(c->x0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice));
+    if (c->f32) {
+        const std::vector<float> f(x0, x0 + c->nx);
+        HIPCHK(hipMemcpy(c->x0, f.data(), c->nx * sizeof(float), hipMemcpyHostToDevice));
+    } else {
+        HIPCHK(hipMemcpy(c->x0, x0, c->nx * sizeof(double), hipMemcpyHostToDevice));
+    }
     c->has_x0 = true;
     return RAOCP_OK;
 }
 
 int raocp_relax_s0(raocp_ctx* c, double alpha) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     raocp::k_relax_s0<<<1, 1, 0, c->stream>>>(c->dev, c->cur_z, alpha);
     HIPCHK(hipGetLastError());
@@ -1691,6 +1762,7 @@ int raocp_relax_s0(raocp_ctx* c, double alpha) {
 
 int raocp_project_on_dynamics(raocp_ctx* c) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     if (!c->has_x0) return fail(RAOCP_ERR_STATE, "initial state not cached (call cache_initial_state first)");
     const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
@@ -1714,6 +1786,7 @@ int raocp_project_on_dynamics(raocp_ctx* c) {
 
 int raocp_project_on_kernel(raocp_ctx* c) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     const Launch L = groups(c->cmax + 1, c->m);
     raocp::k_kernel_proj<<<L.blocks, kBlock, 0, c->stream>>>(c->dev, c->cur_z);
@@ -1732,6 +1805,7 @@ int raocp_prox_f(raocp_ctx* c, double alpha) {
 
 int raocp_prox_gconj(raocp_ctx* c, double alpha) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     int rc = set_ctl_alpha(c, alpha);
     if (rc) return rc;
@@ -1747,6 +1821,7 @@ int raocp_prox_gconj(raocp_ctx* c, double alpha) {
 
 int raocp_dual_scale(raocp_ctx* c, double alpha) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     raocp::k_div<<<std::min(2048, cdiv((int)c->D, kBlock)), kBlock, 0, c->stream>>>(c->cur_e, alpha, (int)c->D);
     HIPCHK(hipGetLastError());
@@ -1756,6 +1831,7 @@ int raocp_dual_scale(raocp_ctx* c, double alpha) {
 
 int raocp_dual_add_halves(raocp_ctx* c) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     const Dev& D = c->dev;
     const int nb = cdiv(c->n, kBlock);
@@ -1770,6 +1846,7 @@ int raocp_dual_add_halves(raocp_ctx* c) {
 
 int raocp_dual_project(raocp_ctx* c, int which) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     HIPCHK(hipMemsetAsync(&c->ctl->flags, 0, sizeof(int), c->stream));
     const int mode = (which & 1 ? raocp::kDualNonleaf : 0) | (which & 2 ? raocp::kDualLeaf : 0);
@@ -1783,6 +1860,7 @@ int raocp_dual_project(raocp_ctx* c, int which) {
 
 int raocp_dual_moreau(raocp_ctx* c, double alpha, const double* modified) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c || !modified) return fail(RAOCP_ERR_ARG, "null argument");
     int rc = copy_in(c, c->tmpD, modified, c->D, 0);
     if (rc) return rc;
@@ -1824,11 +1902,21 @@ static double tridiag_max_eig(const std::vector<double>& a, const std::vector<do
 
 static int dev_dot(raocp_ctx* c, const double* a, const double* b, int n, double* out) {
     const int nb = std::min(1024, cdiv(n, kBlock));
-    raocp::k_dot_partial<<<nb, kBlock, 0, c->stream>>>(a, b, n, c->part);
+    if (c->f32) raocp::k_dot_partial<float><<<nb, kBlock, 0, c->stream>>>((const float*)a, (const float*)b, n, c->part);
+    else raocp::k_dot_partial<double><<<nb, kBlock, 0, c->stream>>>(a, b, n, c->part);
     raocp::k_dot_final<<<1, kBlock, 0, c->stream>>>(c->part, nb, c->scal);
     HIPCHK(hipMemcpyAsync(out, c->scal, sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     return RAOCP_OK;
+}
+
+static void dev_scale_copy(raocp_ctx* c, int nb, double sc, const double* x, double* y, int n) {
+    if (c->f32) raocp::k_scale_copy<float><<<nb, kBlock, 0, c->stream>>>(sc, (const float*)x, (float*)y, n);
+    else raocp::k_scale_copy<double><<<nb, kBlock, 0, c->stream>>>(sc, x, y, n);
+}
+static void dev_axpby(raocp_ctx* c, int nb, double a, const double* x, double b, double* y, int n) {
+    if (c->f32) raocp::k_axpby<float><<<nb, kBlock, 0, c->stream>>>(a, (const float*)x, b, (float*)y, n);
+    else raocp::k_axpby<double><<<nb, kBlock, 0, c->stream>>>(a, x, b, y, n);
 }
 
 int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
@@ -1847,14 +1935,14 @@ int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
     std::normal_distribution<double> nd(0.0, 1.0);
     for (int i = 0; i < P; ++i) h[i] = nd(gen);
     h[c->dev.T0] = 0.0;  // tau_0 is outside the range of L'L (the reference's template keeps it 0)
-    HIPCHK(hipMemcpy(v, h.data(), P * sizeof(double), hipMemcpyHostToDevice));
+    if ((rc = copy_in(c, v, h.data(), P, 0))) return rc;
     HIPCHK(hipMemsetAsync(vprev, 0, P * sizeof(double), c->stream));
     HIPCHK(hipMemsetAsync(w, 0, P * sizeof(double), c->stream));
     HIPCHK(hipMemsetAsync(eta, 0, c->D * sizeof(double), c->stream));
     const int nbv = std::min(2048, cdiv(P, kBlock));
     double nrm2;
     if ((rc = dev_dot(c, v, v, P, &nrm2))) return rc;
-    raocp::k_scale_copy<<<nbv, kBlock, 0, c->stream>>>(1.0 / std::sqrt(nrm2), v, v, P);
+    dev_scale_copy(c, nbv, 1.0 / std::sqrt(nrm2), v, v, P);
     std::vector<double> al, be;
     double beta = 0.0, lam = 0.0, lam_prev = -1.0;
     int stable = 0;
@@ -1862,10 +1950,10 @@ int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
         launch_ell(c, v, eta);
         HIPCHK(hipMemsetAsync(w, 0, P * sizeof(double), c->stream));
         launch_ell_t(c, eta, w);          // w = L'L v (tau_0 = 0)
-        raocp::k_axpby<<<nbv, kBlock, 0, c->stream>>>(-beta, vprev, 1.0, w, P);
+        dev_axpby(c, nbv, -beta, vprev, 1.0, w, P);
         double a;
         if ((rc = dev_dot(c, w, v, P, &a))) return rc;
-        raocp::k_axpby<<<nbv, kBlock, 0, c->stream>>>(-a, v, 1.0, w, P);
+        dev_axpby(c, nbv, -a, v, 1.0, w, P);
         double bb;
         if ((rc = dev_dot(c, w, w, P, &bb))) return rc;
         al.push_back(a);
@@ -1880,8 +1968,8 @@ int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
         if (beta <= 1e-300) break;
         be.push_back(beta);
         // vprev <- v ; v <- w / beta
-        HIPCHK(hipMemcpyAsync(vprev, v, P * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
-        raocp::k_scale_copy<<<nbv, kBlock, 0, c->stream>>>(1.0 / beta, w, v, P);
+        HIPCHK(hipMemcpyAsync(vprev, v, P * c->wsz, hipMemcpyDeviceToDevice, c->stream));
+        dev_scale_copy(c, nbv, 1.0 / beta, w, v, P);
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1896,6 +1984,7 @@ int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
 int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, double alpha, int* status, int* iters,
                  double* err_hist, double* delta_hist) {
     DevGuard dg_(c);
+    if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 CP loop unavailable: no fp32 dynamics plan");
     if (!c || !x0) return fail(RAOCP_ERR_ARG, "null argument");
     if (max_iters < 0) return fail(RAOCP_ERR_ARG, "max_iters must be >= 0");
     int rc;
@@ -1930,6 +2019,7 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
 
 int raocp_cp_prepare(raocp_ctx* c, int iters) {
     DevGuard dg_(c);
+    if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 CP loop unavailable: no fp32 dynamics plan");
     if (!c || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
     int rc;
     if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
@@ -1940,6 +2030,7 @@ int raocp_cp_prepare(raocp_ctx* c, int iters) {
 
 int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, float* ms) {
     DevGuard dg_(c);
+    if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 CP loop unavailable: no fp32 dynamics plan");
     if (!c || !x0 || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
     int rc;
     if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
@@ -1973,6 +2064,7 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
 // `cap` raw 100 MHz timestamps.
 int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c || !out || cap <= 0) return fail(RAOCP_ERR_ARG, "bad argument");
     unsigned long long* st = nullptr;
     int rc = c->alloc(&st, (size_t)cap);
@@ -2004,6 +2096,7 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
 // ---- subtree sharding ---------------------------------------------------------------
 int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     DevGuard dg_(c);
+    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(RAOCP_ERR_ARG, "bad shard arguments");
     // one shard is the unsharded solve, unless forced (tests run the exchange path with R = 1)
     if (nranks == 1 && !getenv("RAOCP_SHARD_FORCE")) return RAOCP_OK;
@@ -2193,18 +2286,20 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
     std::normal_distribution<double> nd(0.0, 1.0);
     for (auto& v : hz) v = nd(gen);
     for (auto& v : he) v = nd(gen);
-    HIPCHK(hipMemcpy(c->tmpP, hz.data(), c->P * sizeof(double), hipMemcpyHostToDevice));
-    HIPCHK(hipMemcpy(c->tmpD, he.data(), c->D * sizeof(double), hipMemcpyHostToDevice));
+    int rci;
+    if ((rci = copy_in(c, c->tmpP, hz.data(), c->P, 0)) || (rci = copy_in(c, c->tmpD, he.data(), c->D, 0))) return rci;
+    HIPCHK(hipStreamSynchronize(c->stream));
     double* outP = c->Z[2];
     double* outD = c->E[1];
     // ops >= 2 time the CP kernels (or one role of them) on a valid control block
     if (op >= 2) {
+        if (c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 context: only L / L^T (op 0 / 1) can be timed");
         if (int rh = ensure_hist(c, (size_t)reps + 16)) return rh;
         std::vector<double> x0(c->nx, 0.0);
         int rc = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
         if (rc) return rc;
-        for (int b = 0; b < 3; ++b) HIPCHK(hipMemcpyAsync(c->Z[b], c->tmpP, c->P * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
-        for (int b = 0; b < 2; ++b) HIPCHK(hipMemcpyAsync(c->E[b], c->tmpD, c->D * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+        for (int b = 0; b < 3; ++b) HIPCHK(hipMemcpyAsync(c->Z[b], c->tmpP, c->P * c->wsz, hipMemcpyDeviceToDevice, c->stream));
+        for (int b = 0; b < 2; ++b) HIPCHK(hipMemcpyAsync(c->E[b], c->tmpD, c->D * c->wsz, hipMemcpyDeviceToDevice, c->stream));
     }
     auto run = [&]() {
         switch (op) {

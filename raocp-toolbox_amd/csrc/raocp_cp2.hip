@@ -112,26 +112,28 @@ __device__ __forceinline__ T box_apply_t(T v, T lo, T hi, Ctl* ctl) {
     return v;
 }
 
-// Weight fragments of one n x n table (column-major M[k n + r] = M_rk), RT row tiles:
-// b[rt][s] = M[row 16 rt + lo][k = 4 s + h]. Stationary in registers when small (STAT),
-// else read per use (L1 / L2 resident).
-template <class T, int RT>
+// Weight fragments of one table of R rows x K columns (column-major M[k R + r] = M_rk; the
+// L tables are square, R = K = n), RT row tiles: b[rt][s] = M[row 16 rt + lo][k = 4 s + h].
+// Stationary in registers when small (STAT), else read per use (L1 / L2 resident).
+template <class T, int RT, int KSM = 4 * RT>
 struct WFr {
-    static constexpr int KS = 4 * RT;  // k-steps of the largest n with RT row tiles
+    static constexpr int KS = KSM;  // k-steps of the largest K
     static constexpr bool STAT = RT * KS * sizeof(T) <= 32 * 8;
     typedef T bvec __attribute__((ext_vector_type(STAT ? RT * KS : 1)));
     bvec b;
     const T* M = nullptr;
-    int n = 0;
-    __device__ __forceinline__ void load(const T* tab, int t, int n_) {
-        n = n_;
-        M = tab + (size_t)t * n * n;
+    int R = 0, K = 0;
+    __device__ __forceinline__ void load(const T* tab, int t, int n) { load_rk(tab, t, n, n); }
+    __device__ __forceinline__ void load_rk(const T* tab, int t, int R_, int K_) {
+        R = R_;
+        K = K_;
+        M = tab + (size_t)t * R * K;
         if constexpr (STAT) {
             const int l = threadIdx.x & 63, lo = l & 15, h = l >> 4;
             _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) {
                 _Pragma("unroll") for (int s = 0; s < KS; ++s) {
                     const int r = 16 * rt + lo, k = 4 * s + h;
-                    b[rt * KS + s] = (r < n && k < n) ? ((cglbp<T>)M)[k * n + r] : T(0);
+                    b[rt * KS + s] = (r < R && k < K) ? ((cglbp<T>)M)[k * R + r] : T(0);
                 }
             }
         }
@@ -142,10 +144,25 @@ struct WFr {
         } else {
             const int l = threadIdx.x & 63, lo = l & 15, h = l >> 4;
             const int r = 16 * rt + lo, k = 4 * s + h;
-            return (r < n && k < n) ? ((cglbp<T>)M)[k * n + r] : T(0);
+            return (r < R && k < K) ? ((cglbp<T>)M)[k * R + r] : T(0);
         }
     }
 };
+
+// one A operand stream: acc[rt] += M (A rows); afun(k, a) gives this lane's A value at k
+template <class T, int RT, int KSM, class AF>
+__device__ __forceinline__ void tile1(const WFr<T, RT, KSM>& wf, int K, AF afun, typename MF<T>::v4 (&acc)[RT]) {
+    const int h = (threadIdx.x & 63) >> 4;
+    const int ks = (K + 3) >> 2;
+    _Pragma("unroll") for (int s = 0; s < KSM; ++s) {
+        if (s < ks) {
+            const int k = 4 * s + h;
+            T a = T(0);
+            if (k < K) afun(k, a);
+            _Pragma("unroll") for (int rt = 0; rt < RT; ++rt) acc[rt] = MF<T>::mma(a, wf.get(rt, s), acc[rt]);
+        }
+    }
+}
 
 // One 16-node tile of products with ONE table (wf) and two A operand streams:
 // acc1[rt] += M (A1 rows), acc2[rt] += M (A2 rows); afun(k, a1, a2) gives this lane's

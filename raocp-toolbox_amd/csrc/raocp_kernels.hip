@@ -871,6 +871,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
 
 #include "raocp_cp.hip"
 #include "raocp_cp2.hip"
+#include "raocp_ell2.hip"
 
 // ---- element-wise dual sub-steps of prox_g* (cache.py:329-347, 392-393)
 __global__ void k_div(double* __restrict__ x, double a, int n) {
@@ -984,11 +985,14 @@ __global__ void k_cp_check_red(Ctl* ctl, double* hist, const double* __restrict_
     }
 }
 
-// ---- vector helpers for Lanczos (step size)
-__global__ void k_dot_partial(const double* __restrict__ a, const double* __restrict__ b, int n, double* part) {
+// ---- vector helpers for Lanczos (step size); T = the context's scalar type, dot
+// products accumulate in fp64
+template <class T>
+__global__ void k_dot_partial(const T* __restrict__ a, const T* __restrict__ b, int n, double* part) {
     __shared__ double s[kBlock / 64];
     double acc = 0.0;
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) acc = fma(a[i], b[i], acc);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        acc = fma((double)a[i], (double)b[i], acc);
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
     if ((threadIdx.x & 63) == 0) s[threadIdx.x >> 6] = acc;
     __syncthreads();
@@ -1013,12 +1017,23 @@ __global__ void k_dot_final(const double* part, int nb, double* out) {
 }
 
 // y = a*x + b*y
-__global__ void k_axpby(double a, const double* __restrict__ x, double b, double* __restrict__ y, int n) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = a * x[i] + b * y[i];
+template <class T>
+__global__ void k_axpby(double a, const T* __restrict__ x, double b, T* __restrict__ y, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        y[i] = (T)(a * (double)x[i] + b * (double)y[i]);
 }
 
-__global__ void k_scale_copy(double s, const double* __restrict__ x, double* __restrict__ y, int n) {
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = s * x[i];
+template <class T>
+__global__ void k_scale_copy(double s, const T* __restrict__ x, T* __restrict__ y, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = (T)(s * (double)x[i]);
+}
+
+// fp64 <-> fp32 copies (the host boundary of an fp32 context)
+__global__ void k_to_f32(const double* __restrict__ x, float* __restrict__ y, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = (float)x[i];
+}
+__global__ void k_to_f64(const float* __restrict__ x, double* __restrict__ y, int n) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) y[i] = (double)x[i];
 }
 
 }  // namespace raocp

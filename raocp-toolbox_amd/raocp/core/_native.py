@@ -48,7 +48,9 @@ class ProblemDesc(ctypes.Structure):
                 ("i_box_nl", _i32p), ("i_box_l", _i32p),
                 ("n_a", ctypes.c_int32), ("n_b", ctypes.c_int32), ("n_k", ctypes.c_int32),
                 ("A", _f64p), ("B", _f64p), ("K", _f64p), ("Rinv", _f64p), ("M", _f64p),
-                ("i_a", _i32p), ("i_b", _i32p), ("i_k", _i32p)]
+                ("i_a", _i32p), ("i_b", _i32p), ("i_k", _i32p), ("dtype", ctypes.c_int32)]
+
+DTYPES = {"float64": 0, "float32": 1}
 
 
 class RaocpError(RuntimeError):
@@ -163,8 +165,11 @@ def group_cp_run(contexts, x0, max_iters, tol, alpha):
 class NativeContext:
     """One device context (raocp_ctx) holding a packed problem in HBM."""
 
-    def __init__(self, packed, device=None):
+    def __init__(self, packed, device=None, dtype="float64"):
         self._lib = load_library()
+        self.dtype = np.dtype(dtype).name
+        if self.dtype not in DTYPES:
+            raise ValueError(f"dtype {dtype}: float64 or float32")
         self._packed = packed  # keep arrays alive while the descriptors point at them
         p = packed
         self.tree_desc = TreeDesc(p.n, p.m, p.nx, p.nu, *[a.ctypes.data_as(_i32p) for a in
@@ -177,7 +182,7 @@ class NativeContext:
             p.n_box_nl, p.n_box_l, f(p.box_nl_lo), f(p.box_nl_hi), f(p.box_l_lo), f(p.box_l_hi),
             i(p.i_box_nl), i(p.i_box_l),
             p.A.shape[0], p.B.shape[0], p.K.shape[0],
-            f(p.A), f(p.B), f(p.K), f(p.Rinv), f(p.M), i(p.i_a), i(p.i_b), i(p.i_k))
+            f(p.A), f(p.B), f(p.K), f(p.Rinv), f(p.M), i(p.i_a), i(p.i_b), i(p.i_k), DTYPES[self.dtype])
         self.device = _default_device() if device is None else device
         h = ctypes.c_void_p()
         self._check(self._lib.raocp_ctx_create(ctypes.byref(self.tree_desc), ctypes.byref(self.prob_desc),

@@ -34,7 +34,7 @@ def _flatten(blocks):
 class Cache:
     """Oracle of functions for solving RAOCPs using proximal algorithms (HIP-backed)."""
 
-    def __init__(self, problem_spec: ps.RAOCP, device=None):
+    def __init__(self, problem_spec: ps.RAOCP, device=None, dtype="float64"):
         self.__raocp = problem_spec
         tree = problem_spec.tree
         self.__num_nodes = n = int(tree.num_nodes)
@@ -45,7 +45,9 @@ class Cache:
         self.__control_size = nu = problem_spec.control_dynamics_at_node(1).shape[1]
         self.__initial_state = None
         self.__packed = pack_problem(problem_spec)
-        self.__ctx = _native.NativeContext(self.__packed, device=device)
+        # dtype (extension): "float32" runs the iterate, tables and products in fp32
+        # (BASELINE configs[4]); vectors still cross this API as float64
+        self.__ctx = _native.NativeContext(self.__packed, device=device, dtype=dtype)
 
         # block shapes of the reference's lists (cache.py:126-170)
         nch = self.__packed.nch.astype(np.int64)

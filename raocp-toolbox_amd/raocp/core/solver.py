@@ -24,9 +24,9 @@ __all__ = ["Solver"]
 
 
 class Solver:
-    def __init__(self, problem_spec: spec.RAOCP, device=None):
+    def __init__(self, problem_spec: spec.RAOCP, device=None, dtype="float64"):
         self.__raocp = problem_spec
-        self.__cache = cache.Cache(self.__raocp, device=device)
+        self.__cache = cache.Cache(self.__raocp, device=device, dtype=dtype)
         self.__operator = ops.Operator(self.__cache)
         self.__initial_state = None
         self.__parameter_1 = None
