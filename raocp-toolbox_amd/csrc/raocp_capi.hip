@@ -49,6 +49,13 @@ struct raocp_ctx {
     int device = 0;
     bool f32 = false;            // RAOCP_F32: iterate, tables and products in fp32
     bool dyn32 = false;          // the per-stage T-templated dynamics (raocp_dyn2.hip) is planned
+    // per-stage MFMA dynamics (raocp_dyn2.hip): tables, node lists, tile lists per stage
+    bool dyn2 = false;           // fp32 contexts always; fp64 opt-in RAOCP_DYN2=1
+    const double *W2 = nullptr, *RG2 = nullptr, *KM2 = nullptr, *F2 = nullptr;
+    const int* d2_idx = nullptr;
+    const raocp::DynTile* d2_tiles = nullptr;
+    std::vector<int> d2_off;     // per stage t: [prod, node, fwdU, fwdX] tile offsets, 5 entries
+    double *Q2 = nullptr, *PA2 = nullptr, *Dd2 = nullptr;
     int wsz = 8;                 // bytes per scalar of the iterate
     hipStream_t stream = nullptr;
     Dev dev{};
@@ -314,6 +321,37 @@ void launch_ell_t(raocp_ctx* c, const double* eta, double* z) {
     else dispatch(c->nx, c->nu, EllTOp{}, c, eta, z);
 }
 
+// ---- per-stage MFMA dynamics (raocp_dyn2.hip) on z = the iterate to project
+template <class T>
+struct Dyn2Op {
+    template <int RX, int RU>
+    void run(raocp_ctx* c, double* z, const Ctl* ctl) {
+        const int N = c->N, nthr = 256, W = nthr / 64;
+        auto grid = [&](int nt) { return std::max(1, cdiv(nt, W)); };
+        for (int t = N - 1; t >= 0; --t) {
+            const int* o = &c->d2_off[(size_t)t * 5];
+            const bool leaf = t + 1 == N;
+            if (o[1] > o[0])
+                raocp::k_d2_prod<T, RX + RU, 4 * RX><<<grid(o[1] - o[0]), nthr, 0, c->stream>>>(
+                    c->dev, ctl, c->d2_tiles + o[0], o[1] - o[0], c->d2_idx, c->W2, leaf ? z : c->Q2,
+                    leaf ? c->dev.X0 : 0, leaf ? T(-1) : T(1), c->PA2);
+            if (o[2] > o[1])
+                raocp::k_d2_node<T, RX + RU, 4 * RU><<<grid(o[2] - o[1]), nthr, 0, c->stream>>>(
+                    c->dev, ctl, c->d2_tiles + o[1], o[2] - o[1], c->d2_idx, c->RG2, z, c->PA2, c->Q2, c->Dd2);
+        }
+        raocp::k_d2_x0<T><<<1, 64, 0, c->stream>>>(ctl, z, c->dev.X0, c->x0, c->nx);
+        for (int t = 0; t < N; ++t) {
+            const int* o = &c->d2_off[(size_t)t * 5];
+            if (o[3] > o[2])
+                raocp::k_d2_fwd<T, RU, 4 * RX, false><<<grid(o[3] - o[2]), nthr, 0, c->stream>>>(
+                    c->dev, ctl, c->d2_tiles + o[2], o[3] - o[2], c->d2_idx, c->KM2, z, c->Dd2);
+            if (o[4] > o[3])
+                raocp::k_d2_fwd<T, RX, 4 * (RX + RU), true><<<grid(o[4] - o[3]), nthr, 0, c->stream>>>(
+                    c->dev, ctl, c->d2_tiles + o[3], o[4] - o[3], c->d2_idx, c->F2, z, c->Dd2);
+        }
+    }
+};
+
 struct DynOp {
     // part: 0 whole projection; 1 the tiers' backward sweeps only; 2 the top and the
     // tiers' forward sweeps (a shard exchanges the roots' q rows in between)
@@ -393,6 +431,12 @@ struct DynOp {
 };
 // dynamics projection on z = Z[(k + zsel) % 3] (k from ctl when ctl != null, else 0)
 void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part = 0) {
+    if (c->dyn2) {
+        double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
+        if (c->f32) dispatch_rt(c->nx, c->nu, Dyn2Op<float>{}, c, z, ctl);
+        else dispatch_rt(c->nx, c->nu, Dyn2Op<double>{}, c, z, ctl);
+        return;
+    }
     dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl, part);
 }
 
@@ -448,19 +492,21 @@ raocp::Bufs rotated(raocp_ctx* c, int it) {
     return raocp::Bufs{c->Z[it % 3], c->Z[(it + 1) % 3], c->Z[(it + 2) % 3], c->E[it % 2], c->E[(it + 1) % 2]};
 }
 
+template <class T>
 struct Cpd2Op {
     template <int RX, int RU>
     void run(raocp_ctx* c) {
-        auto k = raocp::k_cpd2<double, RX, RU>;
+        auto k = raocp::k_cpd2<T, RX, RU>;
         allow_lds(k, c->lds_cpd2);
         k<<<c->cp2_nbF + c->cp2_nbL, 64 * c->cp2_W, c->lds_cpd2, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
                                                                                 c->redpart, c->cp2_nbF);
     }
 };
+template <class T>
 struct Cpp2Op {
     template <int RX, int RU>
     void run(raocp_ctx* c) {
-        auto k = raocp::k_cpp2<double, RX, RU>;
+        auto k = raocp::k_cpp2<T, RX, RU>;
         allow_lds(k, c->lds_cpp2);
         k<<<c->cp2_nbF + c->cp2_nbL, 64 * c->cp2_W, c->lds_cpp2, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2,
                                                                                 c->redpart, c->cp2_nbF);
@@ -486,12 +532,27 @@ struct CppOp {
     }
 };
 void launch_cpd(raocp_ctx* c) {
-    if (c->cp_v1) dispatch(c->nx, c->nu, CpdOp{}, c);
-    else dispatch_rt(c->nx, c->nu, Cpd2Op{}, c);
+    if (c->f32) dispatch_rt(c->nx, c->nu, Cpd2Op<float>{}, c);
+    else if (c->cp_v1) dispatch(c->nx, c->nu, CpdOp{}, c);
+    else dispatch_rt(c->nx, c->nu, Cpd2Op<double>{}, c);
 }
 void launch_cpp(raocp_ctx* c, bool fuse = false) {
-    if (c->cp_v1 || fuse) dispatch(c->nx, c->nu, CppOp{}, c, fuse);
-    else dispatch_rt(c->nx, c->nu, Cpp2Op{}, c);
+    if (c->f32) dispatch_rt(c->nx, c->nu, Cpp2Op<float>{}, c);
+    else if (c->cp_v1 || fuse) dispatch(c->nx, c->nu, CppOp{}, c, fuse);
+    else dispatch_rt(c->nx, c->nu, Cpp2Op<double>{}, c);
+}
+// the solve's first half step Z[1] = prox-part(Z[0] - alpha L^T E[0]) (s_0 relaxation,
+// kernel projection): k_cp_primal; an fp32 context runs k_cpp2 on {p = z+ = Z[0], d = eta+ =
+// E[0]} (its residual partials are overwritten by iteration 0 before they are read)
+void launch_first_half(raocp_ctx* c) {
+    if (!c->f32) {
+        launch_cp_primal(c, false);
+        return;
+    }
+    const raocp::Bufs keep = c->bufs;
+    c->bufs = raocp::Bufs{c->Z[0], c->Z[0], c->Z[1], c->E[0], c->E[0]};
+    launch_cpp(c);
+    c->bufs = keep;
 }
 // RAOCP_FUSE_CHECK=1: the unsharded CP iteration runs its stopping test inside k_cpp
 bool fuse_check(const raocp_ctx* c) { return !c->comm && c->sh_R == 1 && !c->no_fuse_check; }
@@ -666,7 +727,7 @@ int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double al
     h.tol = tol;
     *c->h_ctl = h;
     HIPCHK(hipMemcpyAsync(c->ctl, c->h_ctl, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
-    launch_cp_primal(c, false);
+    launch_first_half(c);
     return RAOCP_OK;
 }
 
@@ -1230,6 +1291,64 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         if ((rc = c->upload_vec(&D.dW, W)) || (rc = c->upload_vec(&D.dRG, RG)) || (rc = c->upload_vec(&D.dKM, KM)) ||
             (rc = c->upload_vec(&D.dF, F)) || (rc = c->upload_vec(&D.dWT, WT)))
             return bail(rc);
+        // per-stage MFMA dynamics (raocp_dyn2.hip): column-major tables M[k R + r] and, per
+        // stage, tiles of <= 16 nodes sharing a table (fp32 contexts; fp64 opt-in RAOCP_DYN2=1)
+        c->dyn2 = c->f32;
+        if (const char* e = getenv("RAOCP_DYN2")) c->dyn2 = c->dyn2 || atoi(e) != 0;
+        if (c->dyn2) {
+            const size_t nkd = std::max<size_t>(1, kinds.size()), npr = std::max<size_t>(1, pairs.size());
+            std::vector<double> W2(nkd * R * nx, 0.0), RG2((size_t)std::max(1, nk) * R * nu, 0.0),
+                KM2((size_t)std::max(1, nk) * nu * nx, 0.0), F2(npr * nx * (nx + nu), 0.0);
+            for (size_t q = 0; q < kinds.size(); ++q)
+                for (int r = 0; r < R; ++r)
+                    for (int k = 0; k < nx; ++k) W2[(q * nx + k) * R + r] = W[(q * R + r) * SKP + k];
+            for (int c_ = 0; c_ < nk; ++c_) {
+                for (int r = 0; r < R; ++r)
+                    for (int k = 0; k < nu; ++k) RG2[((size_t)c_ * nu + k) * R + r] = RG[((size_t)c_ * R + r) * SNU + k];
+                for (int r = 0; r < nu; ++r)
+                    for (int k = 0; k < nx; ++k) KM2[((size_t)c_ * nx + k) * nu + r] = KM[((size_t)c_ * nu + r) * SKP + k];
+            }
+            for (size_t q = 0; q < pairs.size(); ++q)
+                for (int r = 0; r < nx; ++r)
+                    for (int k = 0; k < nx + nu; ++k) F2[(q * (nx + nu) + k) * nx + r] = F[(q * nx + r) * SKF + k];
+            if ((rc = upload_t(c, &c->W2, W2)) || (rc = upload_t(c, &c->RG2, RG2)) || (rc = upload_t(c, &c->KM2, KM2)) ||
+                (rc = upload_t(c, &c->F2, F2)))
+                return bail(rc);
+            std::vector<int> idx;
+            std::vector<raocp::DynTile> tl;
+            // nodes [a, b) grouped by table (stable), cut into tiles of <= 16
+            auto add = [&](int a, int b, auto table_of) {
+                std::vector<std::pair<int, int>> it;
+                for (int v = a; v < b; ++v) it.push_back({table_of(v), v});
+                std::stable_sort(it.begin(), it.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+                for (size_t q = 0; q < it.size();) {
+                    size_t e = q;
+                    while (e < it.size() && e - q < 16 && it[e].first == it[q].first) ++e;
+                    tl.push_back(raocp::DynTile{(int)idx.size(), (int)(e - q), it[q].first, 0});
+                    for (size_t k = q; k < e; ++k) idx.push_back(it[k].second);
+                    q = e;
+                }
+            };
+            c->d2_off.assign((size_t)N * 5, 0);
+            for (int st = 0; st < N; ++st) {
+                int* o = &c->d2_off[(size_t)st * 5];
+                const int pb = c->stage_ptr[st], pe = c->stage_ptr[st + 1], cb_ = pe, ce_ = c->stage_ptr[st + 2];
+                o[0] = (int)tl.size();
+                add(cb_, ce_, [&](int j) { return kind[j]; });
+                o[1] = (int)tl.size();
+                add(pb, pe, [&](int i) { return pr->i_k[i]; });
+                o[2] = (int)tl.size();
+                add(pb, pe, [&](int i) { return pr->i_k[i]; });
+                o[3] = (int)tl.size();
+                add(cb_, ce_, [&](int j) { return pair[j]; });
+                o[4] = (int)tl.size();
+            }
+            if ((rc = c->upload_vec(&c->d2_idx, idx)) || (rc = c->upload_vec(&c->d2_tiles, tl)) ||
+                (rc = c->alloc(&c->Q2, (size_t)n * nx)) || (rc = c->alloc(&c->PA2, (size_t)n * R)) ||
+                (rc = c->alloc(&c->Dd2, (size_t)m * nu)))
+                return bail(rc);
+            c->dyn32 = c->f32;
+        }
         std::vector<raocp::Rec> ninfo(m), cinfo(n);
         for (int i = 0; i < m; ++i) ninfo[i] = raocp::Rec{t->ch_start[i], t->nch[i], pr->i_k[i], t->stage[i]};
         cinfo[0] = raocp::Rec{0, 0, -1, 0};
@@ -1762,7 +1881,7 @@ int raocp_relax_s0(raocp_ctx* c, double alpha) {
 
 int raocp_project_on_dynamics(raocp_ctx* c) {
     DevGuard dg_(c);
-    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
+    if (c && c->f32 && !c->dyn2) return fail(RAOCP_ERR_ARG, "fp32 context without a dynamics plan");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     if (!c->has_x0) return fail(RAOCP_ERR_STATE, "initial state not cached (call cache_initial_state first)");
     const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
@@ -2293,7 +2412,8 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
     double* outD = c->E[1];
     // ops >= 2 time the CP kernels (or one role of them) on a valid control block
     if (op >= 2) {
-        if (c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 context: only L / L^T (op 0 / 1) can be timed");
+        if (c->f32 && (!c->dyn32 || (op != 2 && op != 6 && op != 9)))
+            return fail(RAOCP_ERR_ARG, "fp32 context: ops 0, 1, 2, 6 and 9 can be timed");
         if (int rh = ensure_hist(c, (size_t)reps + 16)) return rh;
         std::vector<double> x0(c->nx, 0.0);
         int rc = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);

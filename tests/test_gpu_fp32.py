@@ -69,3 +69,41 @@ def test_fp32_rejects_mixed_weight_blocks(golden):
     from raocp.core._native import RaocpError
     with pytest.raises(RaocpError, match="one weight table"):
         core.Cache(prob, dtype="float32")
+
+
+def test_fp32_dynamics_projection_config5(c5):
+    """The per-stage MFMA dynamics sweep (raocp_dyn2.hip) in fp32 at config 5 against the
+    fp64 oracle (cache.py:259-288): 2e-5 relative to the largest entry (a backward and a
+    forward recursion of 9 stages of 64 x 80 products), and feasibility x_j = A_j x_i + B_j u_i
+    of its output to fp32 accuracy."""
+    r, prob, cache, orc = c5
+    rng = np.random.default_rng(17)
+    zz = rng.standard_normal(cache.primal_size)
+    cache.cache_initial_state(r["x0"])
+    cache.native.set_primal(zz)
+    cache.native.project_on_dynamics()
+    z1 = cache.native.get_primal()
+    ref = orc.project_on_dynamics(zz, r["x0"])
+    assert rel_err(z1, ref) <= 2e-5
+    X = z1[orc.X0:orc.U0].reshape(orc.n, orc.nx)
+    U = z1[orc.U0:orc.Y0].reshape(orc.m, orc.nu)
+    j = np.arange(1, orc.n, 997)
+    pred = np.stack([orc.A[orc.iA[k]] @ X[orc.anc[k]] + orc.B[orc.iB[k]] @ U[orc.anc[k]] for k in j])
+    assert np.max(np.abs(X[j] - pred)) <= 1e-5 * max(1.0, np.max(np.abs(X)))
+
+
+def test_fp32_cp_loop_config5_vs_oracle(c5):
+    """Three iterations of the whole CP loop (solver.py:124-161) in fp32 at config 5 against
+    the fp64 oracle with the same step size: residual traces within 1e-3 relative per entry
+    and the final iterate within 1e-4 of its largest entry (fp32 rounding through the
+    iteration's chain of L, prox and L^T)."""
+    r, prob, cache, orc = c5
+    lam = cache.native.step_size(rtol=1e-7)
+    alpha = 0.999 / lam
+    status, err, derr = cache.native.cp_run(r["x0"], 2, 0.0, alpha)
+    st_o, err_o, derr_o, z_o, e_o, _ = orc.chock(r["x0"], 2, 0.0, alpha=alpha)
+    assert status == st_o == 1 and err.shape == (3, 3)
+    assert np.max(np.abs(err - err_o) / np.abs(err_o)) <= 1e-3
+    assert np.max(np.abs(derr - derr_o) / np.abs(derr_o)) <= 1e-3
+    assert rel_err(cache.get_primal_flat(), z_o) <= 1e-4
+    assert rel_err(cache.get_dual_flat(), e_o) <= 1e-4

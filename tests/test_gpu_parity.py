@@ -456,3 +456,26 @@ def test_output_utilities_headless(golden, tmp_path, capsys, monkeypatch):
     out = capsys.readouterr().out
     assert out.startswith("states =\n")
     assert out.count("[[") == tree.num_nodes + tree.num_nonleaf_nodes
+
+
+@pytest.mark.parametrize("cfg", [2, 4])
+def test_dyn2_fp64_projection_and_cp_trace(cfg):
+    """The per-stage MFMA dynamics sweep (raocp_dyn2.hip, the engine of fp32 contexts) in
+    fp64 (RAOCP_DYN2=1): the projection against the oracle at 1e-11 and 10 CP iterations at
+    the trace tolerance."""
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(cfg)
+    tree, prob = build_problem(r)
+    with _env("RAOCP_DYN2", "1"):
+        cache = core.Cache(prob)
+    orc = OracleProblem(prob)
+    zz = np.random.default_rng(17).standard_normal(cache.primal_size)
+    cache.cache_initial_state(r["x0"])
+    cache.native.set_primal(zz)
+    cache.native.project_on_dynamics()
+    assert rel_err(cache.native.get_primal(), orc.project_on_dynamics(zz, r["x0"])) <= 1e-11
+    alpha = 0.999 / cache.native.step_size()
+    status, err, derr = cache.native.cp_run(r["x0"], 9, 0.0, alpha)
+    st_o, err_o, derr_o, z_o, e_o, _ = orc.chock(r["x0"], 9, 0.0, alpha=alpha)
+    assert trace_rel_err(err, err_o) <= 1e-8 and trace_rel_err(derr, derr_o) <= 1e-8
+    assert rel_err(cache.get_primal_flat(), z_o) <= 1e-10
