@@ -49,6 +49,8 @@ struct raocp_ctx {
     int device = 0;
     bool f32 = false;            // RAOCP_F32: iterate, tables and products in fp32
     bool dyn32 = false;          // the per-stage T-templated dynamics (raocp_dyn2.hip) is planned
+    bool ell3 = false;           // L by streaming wave tasks (raocp_ell3.hip)
+    int ell3_grid = 0;
     // per-stage MFMA dynamics (raocp_dyn2.hip): tables, node lists, tile lists per stage
     bool dyn2 = false;           // fp32 contexts always; fp64 opt-in RAOCP_DYN2=1
     const double *W2 = nullptr, *RG2 = nullptr, *KM2 = nullptr, *F2 = nullptr;
@@ -303,7 +305,18 @@ struct Ell2Op {
         }
     }
 };
+// L as streaming wave tasks (raocp_ell3.hip): compile-time sizes of the benchmark configs
+template <class T>
+bool launch_ell3(raocp_ctx* c, const double* z, double* eta) {
+    const int g = c->ell3_grid;
+    if (c->nx == 20 && c->nu == 8) raocp::k_ell3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, z, eta);
+    else if (c->nx == 32 && c->nu == 12) raocp::k_ell3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, z, eta);
+    else if (c->nx == 64 && c->nu == 16) raocp::k_ell3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, z, eta);
+    else return false;
+    return true;
+}
 void launch_ell(raocp_ctx* c, const double* z, double* eta) {
+    if (c->ell3 && (c->f32 ? launch_ell3<float>(c, z, eta) : launch_ell3<double>(c, z, eta))) return;
     if (c->f32) dispatch_rt(c->nx, c->nu, Ell2Op<float>{}, c, z, eta, false);
     else dispatch(c->nx, c->nu, EllOp{}, c, z, eta);
 }
@@ -1765,6 +1778,22 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
     c->dev.dyn_regtab = 0;  // RAOCP_DYN_REGTAB=1: dynamics tables by vector loads instead of LDS-DMA
     if (const char* e = getenv("RAOCP_DYN_REGTAB")) c->dev.dyn_regtab = atoi(e) != 0;
+    {
+        // L by streaming wave tasks (raocp_ell3.hip): compile-time sizes, and one sqrtQ / sqrtR
+        // table over all children and one sqrtPf over all leaves (the waves keep them in registers)
+        bool uni = (nx == 20 && nu == 8) || (nx == 32 && nu == 12) || (nx == 64 && nu == 16);
+        for (int j = 2; j < n && uni; ++j)
+            if (pr->i_sq[j] != pr->i_sq[1] || pr->i_sr[j] != pr->i_sr[1]) uni = false;
+        for (int l = m + 1; l < n && uni; ++l)
+            if (pr->i_sp[l] != pr->i_sp[m]) uni = false;
+        // measured (tools/ell3_check.py): config 2 fp64 4.9 vs 5.5 us, config 5 fp32 210 vs
+        // 265 us, config 4 fp64 equal; RAOCP_ELL3=0 keeps the block kernels
+        c->ell3 = uni;
+        if (const char* e = getenv("RAOCP_ELL3")) c->ell3 = uni && atoi(e) != 0;
+        const long tasks = (long)(n - 1 + 15) / 16 + (n - m + 15) / 16 + ((long)m * (nx + nu) + (c->dev.T0 - c->dev.Y0) + m + 63) / 64;
+        c->ell3_grid = (int)std::max(1L, std::min((tasks + 3) / 4, 4096L));
+        if (const char* e = getenv("RAOCP_ELL3_GRID")) c->ell3_grid = std::max(1, atoi(e));
+    }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels
     if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = atoi(e);
     c->dev.regstage = 0;  // RAOCP_REGSTAGE=1: k_ell's gather by vector loads (measured slower)
