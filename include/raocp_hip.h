@@ -165,8 +165,9 @@ int raocp_cp_run(raocp_ctx* ctx, const double* x0, int max_iters, double tol, do
  * (tol = 0) from (x0 at node 0, zeros) / 0 on the device, graph-replayed (whole
  * batches of 24 iterations, then one remainder batch), without host syncs inside;
  * returns device ms. raocp_cp_prepare captures the graphs a run of `iters` iterations
- * uses, so the timed call launches them without capturing. */
-int raocp_cp_prepare(raocp_ctx* ctx, int iters);
+ * uses and, given x0, also resets the iterate for it, so that a following
+ * raocp_cp_bench(ctx, NULL, iters, alpha, &ms) only launches the iterations. */
+int raocp_cp_prepare(raocp_ctx* ctx, const double* x0, int iters, double alpha);
 int raocp_cp_bench(raocp_ctx* ctx, const double* x0, int iters, double alpha, float* ms);
 /* Time `reps` back-to-back launches of L (op=0) or L^T (op=1) on device-resident
  * vectors with HIP events on the context's stream; returns average ms per launch. */

@@ -146,6 +146,8 @@ struct raocp_ctx {
     hipGraphExec_t graph = nullptr;      // kGraphBatch iterations (raocp_cp_run, raocp_cp_bench)
     int graph_iters = 0;
     hipGraphExec_t graph_rem = nullptr;  // the remainder batch of raocp_cp_bench (exactly K iterations)
+    int prepared = 0;                    // raocp_cp_prepare(x0) set up a run of this many iterations
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     int graph_rem_iters = 0;
     std::vector<void*> allocs;
 
@@ -1811,6 +1813,8 @@ void raocp_ctx_destroy(raocp_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->comm && g_rccl.destroy) (void)g_rccl.destroy((ncclComm_t)c->comm);
     drop_graphs(c);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -2165,7 +2169,7 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     return RAOCP_OK;
 }
 
-int raocp_cp_prepare(raocp_ctx* c, int iters) {
+int raocp_cp_prepare(raocp_ctx* c, const double* x0, int iters, double alpha) {
     DevGuard dg_(c);
     if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 CP loop unavailable: no fp32 dynamics plan");
     if (!c || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
@@ -2173,6 +2177,12 @@ int raocp_cp_prepare(raocp_ctx* c, int iters) {
     if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
     if (iters / kGraphBatch && (rc = ensure_graph(c, kGraphBatch))) return rc;
     if (iters % kGraphBatch && (rc = ensure_graph(c, iters % kGraphBatch))) return rc;
+    if (x0) {
+        // the run's initial state: the following raocp_cp_bench(ctx, NULL, iters, ...) starts here
+        if ((rc = cp_init(c, x0, iters - 1, 0.0, alpha))) return rc;
+        HIPCHK(hipStreamSynchronize(c->stream));
+        c->prepared = iters;
+    }
     return RAOCP_OK;
 }
 
@@ -2185,11 +2195,18 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     const int batch = kGraphBatch, full = iters / batch, rem = iters % batch;
     if (full && (rc = ensure_graph(c, batch))) return rc;
     if (rem && (rc = ensure_graph(c, rem))) return rc;
-    if ((rc = cp_init(c, x0, iters - 1, 0.0, alpha))) return rc;
-    hipEvent_t e0, e1;
-    HIPCHK(hipEventCreate(&e0));
-    HIPCHK(hipEventCreate(&e1));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (x0) {
+        if ((rc = cp_init(c, x0, iters - 1, 0.0, alpha))) return rc;
+    } else if (c->prepared != iters) {
+        return fail(RAOCP_ERR_STATE, "raocp_cp_bench without x0 needs raocp_cp_prepare(ctx, x0, iters, alpha) first");
+    }
+    c->prepared = 0;
+    if (!c->ev0) {
+        HIPCHK(hipEventCreate(&c->ev0));
+        HIPCHK(hipEventCreate(&c->ev1));
+    }
+    hipEvent_t e0 = c->ev0, e1 = c->ev1;
+    if (x0) HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventRecord(e0, c->stream));
     // exactly `iters` iterations' kernels: whole batches, then the remainder batch
     for (int b = 0; b < full; ++b)
@@ -2198,8 +2215,6 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     HIPCHK(hipEventRecord(e1, c->stream));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
     HIPCHK(hipMemcpy(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
     if (c->h_ctl->final_k != iters - 1) return fail(RAOCP_ERR_STATE, "bench did not run the requested iterations");
     c->cur_z = c->Z[iters % 3];

@@ -91,7 +91,7 @@ def load_library():
         "raocp_step_size": (c_int, [vp, _f64p, c_int, c_double]),
         "raocp_cp_run": (c_int, [vp, vp, c_int, c_double, c_double, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                  vp, vp]),
-        "raocp_cp_prepare": (c_int, [vp, c_int]),
+        "raocp_cp_prepare": (c_int, [vp, vp, c_int, c_double]),
         "raocp_cp_bench": (c_int, [vp, vp, c_int, c_double, ctypes.POINTER(ctypes.c_float)]),
         "raocp_op_bench": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_float)]),
         "raocp_dual_scale": (c_int, [vp, c_double]),
@@ -315,15 +315,19 @@ class NativeContext:
         k = iters.value
         return status.value, err[:k].copy(), derr[:k].copy()
 
-    def cp_prepare(self, iters):
-        """Capture the CP graphs an `iters`-iteration cp_bench launches (outside timing)."""
-        self._check(self._lib.raocp_cp_prepare(self._h, int(iters)))
+    def cp_prepare(self, iters, x0=None, alpha=0.0):
+        """Capture the CP graphs an `iters`-iteration cp_bench launches and, given x0, reset
+        the iterate for that run (outside timing); cp_bench(None, iters, alpha) follows."""
+        x0p = None if x0 is None else _ptr(self._vec(x0, self._packed.nx))
+        self._check(self._lib.raocp_cp_prepare(self._h, x0p, int(iters), float(alpha)))
 
     def cp_bench(self, x0, iters, alpha):
+        """Exactly `iters` CP iterations (tol = 0); x0=None: the run cp_prepare(iters, x0)
+        set up. Returns device ms."""
         self._require_l()
-        x0 = self._vec(x0, self._packed.nx)
+        x0p = None if x0 is None else _ptr(self._vec(x0, self._packed.nx))
         ms = ctypes.c_float()
-        self._check(self._lib.raocp_cp_bench(self._h, _ptr(x0), int(iters), float(alpha), ctypes.byref(ms)))
+        self._check(self._lib.raocp_cp_bench(self._h, x0p, int(iters), float(alpha), ctypes.byref(ms)))
         return ms.value
 
     def debug_dyn_stamps(self, cap=128):
