@@ -342,8 +342,11 @@ class OracleProblem:
         Ab = np.array([self.Abar[self.iAbar[j]] if j > 0 else np.zeros((self.nx, self.nx)) for j in range(self.n)])
         return P, K, Ab
 
-    def project_on_dynamics(self, z, x0):
-        """cache.py:259-288: backward sweep over stages N-1..0, forward sweep 0..N-1."""
+    def project_on_dynamics(self, z, x0, exchange=None):
+        """cache.py:259-288: backward sweep over stages N-1..0, forward sweep 0..N-1.
+        exchange (test infrastructure for subtree sharding, SURVEY.md 8(e)): (stage S, fn);
+        once the backward sweep has finished stage S, q of the stage-S nodes is replaced by
+        fn(q_S) (a shard gathers every shard's roots, the X2 exchange)."""
         self.offline()
         n, m, nx, nu = self.n, self.m, self.nx, self.nu
         out = np.array(z, dtype=float, copy=True)
@@ -370,6 +373,8 @@ class OracleProblem:
             np.add.at(sum_q, par, at)
             kt = _grouped_matvec(self.KcT, ci, d[nodes] - U[nodes])
             q[nodes] = -X[nodes] + kt + sum_q[nodes]
+            if exchange is not None and t == exchange[0]:
+                q[nodes] = exchange[1](q[nodes])
         X[0] = np.asarray(x0, dtype=float).reshape(-1)
         for t in range(0, self.N):
             nodes = np.flatnonzero((self.stage == t) & (np.arange(n) < m))
@@ -387,7 +392,7 @@ class OracleProblem:
         out = np.empty_like(rhs)
         for c in np.unique(ci):
             sel = np.flatnonzero(ci == c)
-            out[sel] = scipy.linalg.cho_solve(self.choc[c], rhs[sel].T).T
+            out[sel] = scipy.linalg.cho_solve(self.choc[c], rhs[sel].T, check_finite=False).T
         return out
 
     def project_on_kernel(self, z):

@@ -617,14 +617,17 @@ void shard_unpack_x2(raocp_ctx* c) {
     raocp::k_scatter_rows<<<std::max(1, std::min(256, cdiv(tot, kBlock))), kBlock, 0, c->stream>>>(
         c->x2_recv, c->q, c->d_slc, c->sh_R, c->x_max, c->KP);
 }
+// X1 carries the roots' (eta+, xi2) eta2 entries and the previous iteration's residual record
+int x1_len(const raocp_ctx* c) { return 2 * c->x_max + 16; }
 void shard_pack_x1(raocp_ctx* c) {
-    if (c->own_cnt)
-        raocp::k_pack2<<<std::max(1, cdiv(c->own_cnt, kBlock)), kBlock, 0, c->stream>>>(
-            c->x1_send, c->bufs.e1 + c->dev.E2 + c->own_first, c->XI2 + c->dev.E2 + c->own_first, c->own_cnt);
+    raocp::k_pack_x1<<<std::max(1, cdiv(c->own_cnt, kBlock)), kBlock, 0, c->stream>>>(
+        c->x1_send, c->bufs.e1 + c->dev.E2 + c->own_first, c->XI2 + c->dev.E2 + c->own_first, c->own_cnt, c->x_max,
+        c->red8);
 }
 void shard_unpack_x1(raocp_ctx* c) {
-    raocp::k_unpack2<<<std::max(1, cdiv(c->sh_R * c->x_max, kBlock)), kBlock, 0, c->stream>>>(
+    raocp::k_unpack_x1<<<std::max(1, cdiv(c->sh_R * c->x_max, kBlock)), kBlock, 0, c->stream>>>(
         c->x1_recv, c->bufs.e1 + c->dev.E2, c->XI2 + c->dev.E2, c->d_slc, c->sh_R, c->x_max);
+    raocp::k_cp_check_gather<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->x1_recv, c->sh_R, c->x_max);
 }
 int rccl_check(ncclResult_t r, const char* what) {
     if (r != ncclSuccess)
@@ -645,16 +648,25 @@ int enqueue_shard_iteration(raocp_ctx* c) {
     launch_dynamics(c, c->bufs, 1, c->ctl, 2);
     launch_cpd(c);
     shard_pack_x1(c);
-    if ((rc = rccl_check(g_rccl.all_gather(c->x1_send, c->x1_recv, (size_t)2 * c->x_max, ncclFloat64, comm, c->stream),
-                         "ncclAllGather(eta2)")))
+    if ((rc = rccl_check(g_rccl.all_gather(c->x1_send, c->x1_recv, (size_t)x1_len(c), ncclFloat64, comm, c->stream),
+                         "ncclAllGather(eta2, residuals)")))
         return rc;
-    shard_unpack_x1(c);
+    shard_unpack_x1(c);  // + the previous iteration's stopping test
     launch_cpp(c);
     raocp::k_cp_reduce<<<1, kBlock, 0, c->stream>>>(c->ctl, c->redpart, c->cp_rows, c->red8);
-    if ((rc = rccl_check(g_rccl.all_reduce(c->red8, c->red8, 16, ncclFloat64, ncclMax, comm, c->stream),
-                         "ncclAllReduce(max)")))
+    return RAOCP_OK;
+}
+
+// the last iteration's stopping test (its record has no next iteration to ride on): the
+// X1 all-gather with only the residual record meaningful
+int enqueue_shard_tail(raocp_ctx* c) {
+    shard_pack_x1(c);
+    int rc;
+    if ((rc = rccl_check(g_rccl.all_gather(c->x1_send, c->x1_recv, (size_t)x1_len(c), ncclFloat64, (ncclComm_t)c->comm,
+                                           c->stream),
+                         "ncclAllGather(residuals)")))
         return rc;
-    raocp::k_cp_check_red<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->red8);
+    raocp::k_cp_check_gather<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->x1_recv, c->sh_R, c->x_max);
     return RAOCP_OK;
 }
 
@@ -719,6 +731,7 @@ int cp_init(raocp_ctx* c, const double* x0, int max_iters, double tol, double al
         HIPCHK(hipMemsetAsync(c->Z[0], 0, c->P * sizeof(double), c->stream));
         HIPCHK(hipMemsetAsync(c->E[0], 0, c->D * sizeof(double), c->stream));
     }
+    if (c->red8) HIPCHK(hipMemsetAsync(c->red8, 0, 16 * sizeof(double), c->stream));  // no previous record
     for (int b = 1; b < 3; ++b) HIPCHK(hipMemsetAsync(c->Z[b], 0, c->P * sizeof(double), c->stream));
     HIPCHK(hipMemsetAsync(c->E[1], 0, c->D * sizeof(double), c->stream));
     HIPCHK(hipMemsetAsync(c->XI2, 0, c->D * sizeof(double), c->stream));
@@ -2189,7 +2202,7 @@ int raocp_cp_prepare(raocp_ctx* c, const double* x0, int iters, double alpha) {
 int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, float* ms) {
     DevGuard dg_(c);
     if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 CP loop unavailable: no fp32 dynamics plan");
-    if (!c || !x0 || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
+    if (!c || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
     int rc;
     if ((rc = ensure_hist(c, (size_t)iters + 1))) return rc;
     const int batch = kGraphBatch, full = iters / batch, rem = iters % batch;
@@ -2208,10 +2221,12 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (x0) HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventRecord(e0, c->stream));
-    // exactly `iters` iterations' kernels: whole batches, then the remainder batch
+    // exactly `iters` iterations' kernels: whole batches, then the remainder batch (an RCCL
+    // shard then runs the last iteration's deferred stopping test)
     for (int b = 0; b < full; ++b)
         if ((rc = launch_batch(c, batch))) return rc;
     if (rem && (rc = launch_batch(c, rem))) return rc;
+    if (c->comm && (rc = enqueue_shard_tail(c))) return rc;
     HIPCHK(hipEventRecord(e1, c->stream));
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
@@ -2311,7 +2326,7 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     int rc;
     if ((rc = build_cp_blocks(c, pr_, lr_))) return rc;
     if ((rc = c->alloc(&c->x2_send, (size_t)xmax * c->KP)) || (rc = c->alloc(&c->x2_recv, (size_t)nranks * xmax * c->KP)) ||
-        (rc = c->alloc(&c->x1_send, (size_t)2 * xmax)) || (rc = c->alloc(&c->x1_recv, (size_t)2 * nranks * xmax)) ||
+        (rc = c->alloc(&c->x1_send, (size_t)2 * xmax + 16)) || (rc = c->alloc(&c->x1_recv, (size_t)nranks * (2 * xmax + 16))) ||
         (rc = c->alloc(&c->red8, 16)) || (rc = c->upload_vec(&c->d_slc, slc)))
         return rc;
     drop_graphs(c);
@@ -2374,7 +2389,10 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
         for (int r = 0; r < R; ++r) HIPCHK(hipStreamSynchronize(cs[r]->stream));
         return RAOCP_OK;
     };
-    std::vector<double> red(16 * R);
+    // the RCCL iteration's protocol with device copies as the transport: X2 after the tiers'
+    // backward sweeps, X1 (roots' eta2 entries + the previous iteration's residual record,
+    // whose stopping test runs on arrival) after k_cpd; the loop ends once the (deferred)
+    // test has fired
     for (int k = 0;; ++k) {
         for (int r = 0; r < R; ++r) {
             raocp_ctx* c = cs[r];
@@ -2397,23 +2415,11 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
         for (int r = 0; r < R; ++r) {
             raocp_ctx* c = cs[r];
             for (int q = 0; q < R; ++q)
-                HIPCHK(hipMemcpyAsync(c->x1_recv + (size_t)2 * q * c->x_max, cs[q]->x1_send, (size_t)2 * c->x_max * sizeof(double),
+                HIPCHK(hipMemcpyAsync(c->x1_recv + (size_t)q * x1_len(c), cs[q]->x1_send, (size_t)x1_len(c) * sizeof(double),
                                       hipMemcpyDeviceToDevice, c->stream));
             shard_unpack_x1(c);
             launch_cpp(c);
             raocp::k_cp_reduce<<<1, kBlock, 0, c->stream>>>(c->ctl, c->redpart, c->cp_rows, c->red8);
-            HIPCHK(hipMemcpyAsync(red.data() + 16 * r, c->red8, 16 * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-        }
-        if ((rc = sync_all())) return rc;
-        double g[16];
-        for (int q = 0; q < 16; ++q) {
-            g[q] = red[q];
-            for (int r = 1; r < R; ++r) g[q] = std::max(g[q], red[16 * r + q]);
-        }
-        for (int r = 0; r < R; ++r) {
-            raocp_ctx* c = cs[r];
-            HIPCHK(hipMemcpyAsync(c->red8, g, 16 * sizeof(double), hipMemcpyHostToDevice, c->stream));
-            raocp::k_cp_check_red<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->red8);
             HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
         }
         if ((rc = sync_all())) return rc;

@@ -928,20 +928,26 @@ __global__ void k_scatter_rows(const double* __restrict__ recv, double* __restri
         if (i < slc[2 * r + 1]) dst[(size_t)(slc[2 * r] + i) * w + k] = recv[e];
     }
 }
-// pack (a[i], b[i]) pairs of the owned slice; unpack every rank's pairs into a, b
-__global__ void k_pack2(double* __restrict__ send, const double* __restrict__ a, const double* __restrict__ b, int cnt) {
+// X1 record of a shard (stride 2 maxc + 16 doubles): the (a[i], b[i]) pairs of its owned
+// roots, then the 16-double residual record of its PREVIOUS iteration (k_cp_reduce; the
+// stopping test runs one iteration late, so the residual all-reduce rides on this
+// all-gather: two collectives per iteration)
+__global__ void k_pack_x1(double* __restrict__ send, const double* __restrict__ a, const double* __restrict__ b, int cnt,
+                          int maxc, const double* __restrict__ red16) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
         send[2 * i] = a[i];
         send[2 * i + 1] = b[i];
     }
+    if (blockIdx.x == 0 && threadIdx.x < 16) send[2 * maxc + threadIdx.x] = red16[threadIdx.x];
 }
-__global__ void k_unpack2(const double* __restrict__ recv, double* __restrict__ a, double* __restrict__ b,
-                          const int* __restrict__ slc, int R, int maxc) {
+__global__ void k_unpack_x1(const double* __restrict__ recv, double* __restrict__ a, double* __restrict__ b,
+                            const int* __restrict__ slc, int R, int maxc) {
+    const int stride = 2 * maxc + 16;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < R * maxc; e += gridDim.x * blockDim.x) {
         const int r = e / maxc, i = e - r * maxc;
         if (i < slc[2 * r + 1]) {
-            a[slc[2 * r] + i] = recv[2 * e];
-            b[slc[2 * r] + i] = recv[2 * e + 1];
+            a[slc[2 * r] + i] = recv[(size_t)r * stride + 2 * i];
+            b[slc[2 * r] + i] = recv[(size_t)r * stride + 2 * i + 1];
         }
     }
 }
@@ -964,10 +970,38 @@ __global__ void __launch_bounds__(kBlock) k_cp_reduce(const Ctl* ctl, const doub
     if (threadIdx.x < 6) red6[threadIdx.x] = s_m[threadIdx.x][0];
     if (threadIdx.x == 6) red6[6] = (ctl->flags & 1) ? 1.0 : 0.0;  // NaN-in-box flag, all-reduced too
     if (threadIdx.x == 7) red6[7] = 0.0;
-    // a NaN maximum is flagged in slots 8..13 (RCCL's max need not propagate NaN)
+    // a NaN maximum is flagged in slots 8..13 (RCCL's max need not propagate NaN); slot 15
+    // marks the record valid (cp_init zeroes it: iteration 0 has no previous record)
     if (threadIdx.x >= 8 && threadIdx.x < 16)
-        red6[threadIdx.x] = (threadIdx.x < 14 && s_m[threadIdx.x - 8][0] != s_m[threadIdx.x - 8][0]) ? 1.0 : 0.0;
+        red6[threadIdx.x] = threadIdx.x == 15 ? 1.0
+                            : (threadIdx.x < 14 && s_m[threadIdx.x - 8][0] != s_m[threadIdx.x - 8][0]) ? 1.0 : 0.0;
 }
+// history + stopping test of the previous iteration from the R records gathered with X1
+// (max over the shards; the same decision on every shard)
+__global__ void k_cp_check_gather(Ctl* ctl, double* hist, const double* __restrict__ recv, int R, int maxc) {
+    if (threadIdx.x != 0 || ctl->done) return;
+    const int stride = 2 * maxc + 16;
+    const double* r0 = recv + 2 * maxc;
+    if (r0[15] == 0.0) return;  // no previous iteration yet
+    double M[16];
+    for (int q = 0; q < 16; ++q) M[q] = r0[q];
+    for (int r = 1; r < R; ++r)
+        for (int q = 0; q < 16; ++q) M[q] = nmax(M[q], recv[(size_t)r * stride + 2 * maxc + q]);
+    const int k = ctl->k;
+    for (int q = 0; q < 6; ++q) {
+        if (M[8 + q] > 0.0) M[q] = __builtin_nan("");
+        hist[(size_t)k * 6 + q] = M[q];
+    }
+    const double err = nmax(nmax(M[0], M[1]), M[2]);
+    if (M[6] > 0.0) ctl->flags |= 1;
+    if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
+        ctl->done = 1;
+        ctl->final_k = k;
+    } else {
+        ctl->k = k + 1;
+    }
+}
+
 // history + stopping test on the all-reduced maxima (same decision on every shard)
 __global__ void k_cp_check_red(Ctl* ctl, double* hist, const double* __restrict__ red6) {
     if (threadIdx.x != 0 || ctl->done) return;

@@ -257,6 +257,26 @@ def test_c2_operators_vs_oracle(c2):
     assert rel_err(cache.get_dual_flat(), orc.prox_gconj(ee, 0.3)) <= 1e-12
 
 
+def test_c2_bench_runs_the_requested_iterations(c2):
+    """bench.py's timed call: raocp_cp_prepare(x0, K) then raocp_cp_bench(NULL, K) runs
+    exactly K iterations from x0 (a whole graph batch plus a remainder) and leaves the same
+    iterate as raocp_cp_bench(x0, K) and as a K-iteration cp_run."""
+    r, prob, cache, orc = c2
+    nat = cache.native
+    alpha = 0.999 / nat.step_size()
+    K = 29
+    nat.cp_run(r["x0"], K - 1, 0.0, alpha)
+    z_run, e_run = nat.get_primal(), nat.get_dual()
+    nat.cp_bench(r["x0"], K, alpha)
+    assert np.array_equal(nat.get_primal(), z_run) and np.array_equal(nat.get_dual(), e_run)
+    nat.cp_prepare(K, r["x0"], alpha)
+    ms = nat.cp_bench(None, K, alpha)
+    assert ms > 0
+    assert np.array_equal(nat.get_primal(), z_run) and np.array_equal(nat.get_dual(), e_run)
+    with pytest.raises(Exception, match="raocp_cp_prepare"):
+        nat.cp_bench(None, K, alpha)  # a prepared run is consumed by one bench call
+
+
 def test_c2_cp_trace_vs_oracle(c2):
     r, prob, cache, orc = c2
     lam = cache.native.step_size()
