@@ -141,6 +141,7 @@ struct raocp_ctx {
     std::vector<double> h_x0;
     unsigned* ticket = nullptr;  // k_cpp blocks done (fused stopping test)
     bool no_fuse_check = true;   // RAOCP_FUSE_CHECK=1: the stopping test inside k_cpp's last block
+    bool no_defer_check = false; // RAOCP_DEFER_CHECK=0: k_cp_check after every iteration (defer_check)
                                  // (measured slower than its own launch: DESIGN.md)
     // captured CP iterations
     hipGraphExec_t graph = nullptr;      // kGraphBatch iterations (raocp_cp_run, raocp_cp_bench)
@@ -371,7 +372,7 @@ struct DynOp {
     // part: 0 whole projection; 1 the tiers' backward sweeps only; 2 the top and the
     // tiers' forward sweeps (a shard exchanges the roots' q rows in between)
     template <int NX, int NU>
-    void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part) {
+    void run(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part, const raocp::ChkArg* ck) {
         const int s = c->cut;
         const int B = c->dyn_block;
         // diagnostics: each launch stamps into its own 64-slot region
@@ -397,9 +398,16 @@ struct DynOp {
                     const int p0 = c->pair_ptr[c0], p1 = c->pair_ptr[c1];
                     auto kb = tp.fold ? raocp::k_dyn_bottom_back<NX, NU, true> : raocp::k_dyn_bottom_back<NX, NU, false>;
                     allow_lds(kb, tp.lds_b);
+                    // the deepest tier (launched first) carries the deferred stopping test
+                    raocp::ChkArg cka{};
+                    raocp::TierArg ta = tier_arg(k);
+                    if (ck && k == (int)c->tiers.size() - 1) {
+                        cka = *ck;
+                        ta.boff -= 1;
+                    }
                     if (tier_blocks(k) > 0)
-                        kb<<<tier_blocks(k), B, tp.lds_b, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->d, tp.s0, tp.s1,
-                                                                      tp.maxch, c0, c1, p0, p1, tp.lv, tier_arg(k));
+                        kb<<<tier_blocks(k) + cka.on, B, tp.lds_b, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->d, tp.s0,
+                                                                               tp.s1, tp.maxch, c0, c1, p0, p1, tp.lv, ta, cka);
                 }
             if (part == 1) return;
             {
@@ -445,14 +453,17 @@ struct DynOp {
     }
 };
 // dynamics projection on z = Z[(k + zsel) % 3] (k from ctl when ctl != null, else 0)
-void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part = 0) {
+// ck: the previous CP iteration's stopping test, run by an extra workgroup of the first
+// launch (only where defer_check(c) holds)
+void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part = 0,
+                     const raocp::ChkArg* ck = nullptr) {
     if (c->dyn2) {
         double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
         if (c->f32) dispatch_rt(c->nx, c->nu, Dyn2Op<float>{}, c, z, ctl);
         else dispatch_rt(c->nx, c->nu, Dyn2Op<double>{}, c, z, ctl);
         return;
     }
-    dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl, part);
+    dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl, part, ck);
 }
 
 // role: 0 all blocks; 1 nonleaf blocks only; 2 leaf blocks only (op_bench timing)
@@ -571,6 +582,18 @@ void launch_first_half(raocp_ctx* c) {
 }
 // RAOCP_FUSE_CHECK=1: the unsharded CP iteration runs its stopping test inside k_cpp
 bool fuse_check(const raocp_ctx* c) { return !c->comm && c->sh_R == 1 && !c->no_fuse_check; }
+// Deferred stopping test (default for the tiered dynamics; RAOCP_DEFER_CHECK=0 disables):
+// iteration k's test runs in an extra workgroup of iteration k + 1's first dynamics launch
+// instead of its own k_cp_check launch after k_cpp, and a batch ends with one k_cp_check
+// for its last iteration. Iteration k + 1's kernels that start before the test fires only
+// write the next iterate's buffers (Z[(k + 1) % 3] projected in place, nothing of
+// z+_k = Z[k % 3] or eta+_k = E[k % 2]), and every later kernel exits on ctl->done, so the
+// result and the history are those of the eager test.
+bool defer_check(const raocp_ctx* c) {
+    if (c->comm || c->sh_R != 1 || fuse_check(c) || c->dyn2 || c->cut <= 0 || c->tiers.empty() || c->no_defer_check)
+        return false;
+    return c->tiers.back().nsub > 0;
+}
 
 // ---- RCCL, loaded on demand (dlopen) so single-GPU users never load it
 struct Rccl {
@@ -679,13 +702,19 @@ int enqueue_cp_iteration(raocp_ctx* c, int it) {
         c->bufs = keep;
         return rc;
     }
-    launch_dynamics(c, c->bufs, 1, c->ctl);
+    const bool defer = defer_check(c);
+    const raocp::ChkArg ck{c->ctl, c->hist, c->redpart, c->cp_rows, 1};
+    launch_dynamics(c, c->bufs, 1, c->ctl, 0, defer && it > 0 ? &ck : nullptr);
     launch_cpd(c);
     const bool fuse = fuse_check(c);
     launch_cpp(c, fuse);
     c->bufs = keep;
-    if (!fuse) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
+    if (!fuse && !defer) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
     return RAOCP_OK;
+}
+// the end of a batch: the deferred test of its last iteration
+void enqueue_batch_tail(raocp_ctx* c) {
+    if (defer_check(c)) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
 }
 
 
@@ -776,6 +805,7 @@ int ensure_graph(raocp_ctx* c, int iters) {
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     int rc_enq = RAOCP_OK;
     for (int it = 0; it < iters && rc_enq == RAOCP_OK; ++it) rc_enq = enqueue_cp_iteration(c, it);
+    if (rc_enq == RAOCP_OK) enqueue_batch_tail(c);
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (rc_enq != RAOCP_OK) {
         if (g) (void)hipGraphDestroy(g);
@@ -810,6 +840,7 @@ int launch_batch(raocp_ctx* c, int iters) {
             const int rc = enqueue_cp_iteration(c, it);
             if (rc) return rc;
         }
+        enqueue_batch_tail(c);
         HIPCHK(hipGetLastError());
         return RAOCP_OK;
     }
@@ -1793,6 +1824,10 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
     c->dev.dyn_regtab = 0;  // RAOCP_DYN_REGTAB=1: dynamics tables by vector loads instead of LDS-DMA
     if (const char* e = getenv("RAOCP_DYN_REGTAB")) c->dev.dyn_regtab = atoi(e) != 0;
+    c->dev.dyn_rot = 1;  // RAOCP_DYN_ROT=0: every staged range starts at wave 0
+    if (const char* e = getenv("RAOCP_DYN_ROT")) c->dev.dyn_rot = atoi(e) != 0;
+    c->dev.cp_pack = 1;  // RAOCP_CP_PACK=0: one LDS-DMA pass per staged region in k_cpd / k_cpp
+    if (const char* e = getenv("RAOCP_CP_PACK")) c->dev.cp_pack = atoi(e) != 0;
     {
         // L by streaming wave tasks (raocp_ell3.hip): compile-time sizes, and one sqrtQ / sqrtR
         // table over all children and one sqrtPf over all leaves (the waves keep them in registers)
@@ -1816,6 +1851,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     if ((rc = c->alloc(&c->ticket, 64))) return bail(rc);
     if (hipMemset(c->ticket, 0, 64 * sizeof(unsigned)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
     if (const char* e = getenv("RAOCP_FUSE_CHECK")) c->no_fuse_check = atoi(e) == 0;
+    if (const char* e = getenv("RAOCP_DEFER_CHECK")) c->no_defer_check = atoi(e) == 0;
     *out = c;
     return RAOCP_OK;
 }

@@ -40,7 +40,14 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
     glbd* eo = (glbd*)bf.e1;               // eta+
     glbd* xi2 = (glbd*)xi2_;
     const int bid = blockIdx.x;
+    __shared__ unsigned long long s_tsrc[kStgMaxR];
+    __shared__ int s_tc0[kStgMaxR];
+    __shared__ unsigned char s_regof[kStgMaxChunks];
     Stg st{(ldsd*)smem_, 0};
+    st.pack = p.cp_pack;
+    st.tsrc = (__attribute__((address_space(3))) unsigned long long*)s_tsrc;
+    st.tc0 = (__attribute__((address_space(3))) int*)s_tc0;
+    st.regof = (__attribute__((address_space(3))) unsigned char*)s_regof;
     double m2 = 0.0, m5 = 0.0;
     auto finish = [&](int e, double dv, double v, double pv, double b) {
         const double ep = alpha * (v - pv);
@@ -81,6 +88,7 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
         const ldsd* SR = st.dbl((const glbd*)p.SR, nR);
         const ldsd* BL = st.dbl((const glbd*)p.blo_nl, nBx);
         const ldsd* BH = st.dbl((const glbd*)p.bhi_nl, nBx);
+        st.issue();
         done = ctl->done;
         alpha = ctl->alpha;
         dma_wait();
@@ -215,6 +223,7 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
         const ldsd* SP = st.dbl((const glbd*)p.SP, nP);
         const ldsd* BL = st.dbl((const glbd*)p.blo_l, nBx);
         const ldsd* BH = st.dbl((const glbd*)p.bhi_l, nBx);
+        st.issue();
         done = ctl->done;
         alpha = ctl->alpha;
         dma_wait();
@@ -344,7 +353,14 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
     const glbd* dA = (const glbd*)bf.e1;   // eta+
     const glbd* xg = (const glbd*)xi2_;
     const int bid = blockIdx.x;
+    __shared__ unsigned long long s_tsrc[kStgMaxR];
+    __shared__ int s_tc0[kStgMaxR];
+    __shared__ unsigned char s_regof[kStgMaxChunks];
     Stg st{(ldsd*)smem_, 0};
+    st.pack = p.cp_pack;
+    st.tsrc = (__attribute__((address_space(3))) unsigned long long*)s_tsrc;
+    st.tc0 = (__attribute__((address_space(3))) int*)s_tc0;
+    st.regof = (__attribute__((address_space(3))) unsigned char*)s_regof;
     double m0 = 0.0, m1 = 0.0, m3 = 0.0, m4 = 0.0;
     stamp(p, 0);
     // residual terms of one primal entry: pp = p, zz = z+, w = L^T(d - eta+), lc = L^T xi2
@@ -394,6 +410,7 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
         const ldsd* SQ = st.dbl((const glbd*)p.SQ, nQ);
         const ldsd* SR = st.dbl((const glbd*)p.SR, nR);
         stamp(p, 1);
+        st.issue();
         done = ctl->done;
         alpha = ctl->alpha;
         dma_wait();
@@ -558,6 +575,7 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
         const ldsrec* LR = st.rec(p.lrec + (l0 - p.m), Lc);
         const int nP = p.nSP * nx * nx;
         const ldsd* SP = st.dbl((const glbd*)p.SP, nP);
+        st.issue();
         done = ctl->done;
         alpha = ctl->alpha;
         dma_wait();

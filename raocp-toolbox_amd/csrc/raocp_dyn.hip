@@ -606,6 +606,27 @@ __device__ __forceinline__ void rows_in(bool dmaok, ldsd* dst, int w, const doub
     if (dmaok) dma_rows(dst, w, src, sstride, cols, rows, zp);
     else copy_rows_reg(dst, w, src, sstride, cols, rows, tid, nthr);
 }
+// The same copies with a rotating first wave (Dev::dyn_rot): a prologue of many small
+// ranges would otherwise put the first (often only) instruction of every range on wave 0,
+// which then issues them one after another. rot < 0: rotation off (every range starts at
+// wave 0); else the next range starts where the previous one ended.
+__device__ __forceinline__ void dma_r(ldsd* dst, const double* src, int n, int& rot) {
+    const int g = dma_gen(dst, n >> 1, [=](int ch) { return src + 2 * ch; }, rot < 0 ? 0 : rot);
+    if (rot >= 0) rot += g;
+}
+__device__ __forceinline__ void rows_in_r(bool dmaok, ldsd* dst, int w, const double* src, int sstride, int cols,
+                                          int rows, const double* zp, int tid, int nthr, int& rot) {
+    if (!dmaok) {
+        copy_rows_reg(dst, w, src, sstride, cols, rows, tid, nthr);
+        return;
+    }
+    const int cpr = w >> 1, cc = cols >> 1;
+    const int g = dma_gen(dst, rows * cpr, [=](int ch) {
+        const int r = ch / cpr, c = ch - r * cpr;
+        return c < cc ? src + (size_t)r * sstride + 2 * c : zp;
+    }, rot < 0 ? 0 : rot);
+    if (rot >= 0) rot += g;
+}
 
 // level ranges of a tier's subtree: from the kernel argument when the tier is regular
 // (every subtree the same shape, ids consecutive), else from the host table
@@ -654,9 +675,15 @@ template <int NXc, int NUc, bool FOLD>
 __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
                                                                 double* qbuf_, double* dbuf_, int s, int s1, int maxch,
                                                                 int c0, int c1, int p0, int p1,
-                                                                const Rec* __restrict__ sub_lv, TierArg ta) {
+                                                                const Rec* __restrict__ sub_lv, TierArg ta, ChkArg ck) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
+    // block 0 of a launch with ck.on: the previous CP iteration's stopping test (the host
+    // shifts ta.boff by one, so the subtrees stay blocks 1..)
+    if (ck.on && blockIdx.x == 0) {
+        if (threadIdx.x < 64) cp_check_wave(ck);
+        return;
+    }
     tstamp(p, pl, 0);
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
@@ -669,9 +696,10 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     const int oW = 0, oRG = oW + nW, oXQ = oRG + (c1 - c0) * ts.RG1;
     const double* srcW = FOLD ? p.dWT + (size_t)p0 * ts.W1 : p.dW;
     const double* srcRG = p.dRG + (size_t)c0 * ts.RG1;
+    int rot = p.dyn_rot ? 0 : -1;
     if (!p.dyn_regtab) {
-        dma(smem + oW, srcW, nW);
-        dma(smem + oRG, srcRG, (c1 - c0) * ts.RG1);
+        dma_r(smem + oW, srcW, nW, rot);
+        dma_r(smem + oRG, srcRG, (c1 - c0) * ts.RG1, rot);
     }
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
@@ -686,16 +714,16 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     for (int l = 0; l <= L; ++l) {
         const int cnt = pl.hi[l] - pl.lo[l];
         if (l < L || leaves)
-            rows_in(dmaok, XQ + (size_t)pl.off[l] * g.KP, g.KP, (const double*)z + p.X0 + (size_t)pl.lo[l] * g.nx,
-                    g.nx, g.nx, cnt, p.zpage, tid, nthr);
+            rows_in_r(dmaok, XQ + (size_t)pl.off[l] * g.KP, g.KP, (const double*)z + p.X0 + (size_t)pl.lo[l] * g.nx,
+                      g.nx, g.nx, cnt, p.zpage, tid, nthr, rot);
         else  // q rows of the next tier's roots, already padded
-            dma(XQ + (size_t)pl.off[l] * g.KP, qbuf_ + (size_t)pl.lo[l] * g.KP, cnt * g.KP);
+            dma_r(XQ + (size_t)pl.off[l] * g.KP, qbuf_ + (size_t)pl.lo[l] * g.KP, cnt * g.KP, rot);
         if (l < L) {
-            rows_in(dmaok, U + (size_t)pl.off[l] * g.NUP, g.NUP, (const double*)z + p.U0 + (size_t)pl.lo[l] * g.nu,
-                    g.nu, g.nu, cnt, p.zpage, tid, nthr);
-            dma(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt);
+            rows_in_r(dmaok, U + (size_t)pl.off[l] * g.NUP, g.NUP, (const double*)z + p.U0 + (size_t)pl.lo[l] * g.nu,
+                      g.nu, g.nu, cnt, p.zpage, tid, nthr, rot);
+            dma_r(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt, rot);
         }
-        if (l > 0) dma(CHd + 2 * (pl.off[l] - 1), (const double*)(p.cinfo + pl.lo[l]), 2 * cnt);
+        if (l > 0) dma_r(CHd + 2 * (pl.off[l] - 1), (const double*)(p.cinfo + pl.lo[l]), 2 * cnt, rot);
     }
     if (!FOLD) zero_fill(PB, maxch * g.PS, tid, nthr);
     if (p.dyn_regtab) {
@@ -765,9 +793,10 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     ldsd* smem = (ldsd*)smem_;
     const int L = s1 - s;
     const int oKM = 0, oF = oKM + (c1 - c0) * ts.KM1, oXD = oF + (FL ? (p1 - p0) * ts.F1 : 0);
+    int rot = p.dyn_rot ? 0 : -1;
     if (!p.dyn_regtab) {
-        dma(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1);
-        if (FL) dma(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
+        dma_r(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1, rot);
+        if (FL) dma_r(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1, rot);
     }
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
@@ -787,12 +816,13 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
         if (dmaok) {
             const int cpr = g.KF >> 1, cx = g.nx >> 1, cd = (g.nx + g.nu) >> 1;
             const bool first = l == 0;
-            dma_gen(xd, cnt * cpr, [=](int ch) {
+            const int gx = dma_gen(xd, cnt * cpr, [=](int ch) {
                 const int r = ch / cpr, c = ch - r * cpr;
                 if (c < cx) return (first && r == 0) ? xroot + 2 * c : zp;
                 if (c < cd) return dl + (size_t)r * g.nu + 2 * (c - cx);
                 return zp;
-            });
+            }, rot < 0 ? 0 : rot);
+            if (rot >= 0) rot += gx;
         } else {
             for (int e = tid; e < cnt * g.KF; e += nthr) {
                 const int r = e / g.KF, c = e - r * g.KF;
@@ -802,9 +832,9 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
                 xd[e] = v;
             }
         }
-        dma(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt);
+        dma_r(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt, rot);
         const int cc = pl.hi[l + 1] - pl.lo[l + 1];
-        dma(CHd + 2 * (pl.off[l + 1] - 1), (const double*)(p.cinfo + pl.lo[l + 1]), 2 * cc);
+        dma_r(CHd + 2 * (pl.off[l + 1] - 1), (const double*)(p.cinfo + pl.lo[l + 1]), 2 * cc, rot);
     }
     if (p.dyn_regtab) {
         TabCopy tc;
@@ -859,22 +889,24 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl
     const int oW = 0, oRG = oW + nW, oKM = oRG + c1 * ts.RG1, oF = oKM + c1 * ts.KM1;
     const int oXQ = oF + (FL ? p1 * ts.F1 : 0), oQB = oXQ + T * g.KP, oU = oQB + nb * g.KP, oXD = oU + T * g.NUP;
     const int oP = oXD + T * g.KF, oNL = oP + (FOLD ? 0 : rup(maxch * g.PS, 2)), oCH = oNL + 2 * T;
+    int rot = p.dyn_rot ? 0 : -1;
     if (!p.dyn_regtab) {
-        dma(smem + oW, FOLD ? p.dWT : p.dW, nW);
-        dma(smem + oRG, p.dRG, c1 * ts.RG1);
-        dma(smem + oKM, p.dKM, c1 * ts.KM1);
-        if (FL) dma(smem + oF, p.dF, p1 * ts.F1);
+        dma_r(smem + oW, FOLD ? p.dWT : p.dW, nW, rot);
+        dma_r(smem + oRG, p.dRG, c1 * ts.RG1, rot);
+        dma_r(smem + oKM, p.dKM, c1 * ts.KM1, rot);
+        if (FL) dma_r(smem + oF, p.dF, p1 * ts.F1, rot);
     }
-    dma(smem + oNL, (const double*)p.ninfo, 2 * T);
-    dma(smem + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1));
+    dma_r(smem + oNL, (const double*)p.ninfo, 2 * T, rot);
+    dma_r(smem + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1), rot);
     if (tid <= s + 1) pl.sp[tid] = p.stage_ptr[tid];
     glbd* z = dyn_z(bf, zsel, ctl);
-    rows_in(dmaok, smem + oXQ, g.KP, (const double*)z + p.X0, g.nx, g.nx, T, p.zpage, tid, nthr);
+    rows_in_r(dmaok, smem + oXQ, g.KP, (const double*)z + p.X0, g.nx, g.nx, T, p.zpage, tid, nthr, rot);
     if (leaves)
-        rows_in(dmaok, smem + oQB, g.KP, (const double*)z + p.X0 + (size_t)T * g.nx, g.nx, g.nx, nb, p.zpage, tid, nthr);
+        rows_in_r(dmaok, smem + oQB, g.KP, (const double*)z + p.X0 + (size_t)T * g.nx, g.nx, g.nx, nb, p.zpage, tid,
+                  nthr, rot);
     else
-        dma(smem + oQB, qbuf_ + (size_t)T * g.KP, nb * g.KP);
-    rows_in(dmaok, smem + oU, g.NUP, (const double*)z + p.U0, g.nu, g.nu, T, p.zpage, tid, nthr);
+        dma_r(smem + oQB, qbuf_ + (size_t)T * g.KP, nb * g.KP, rot);
+    rows_in_r(dmaok, smem + oU, g.NUP, (const double*)z + p.U0, g.nu, g.nu, T, p.zpage, tid, nthr, rot);
     zero_fill(smem + oXD, T * g.KF, tid, nthr);
     if (!FOLD) zero_fill(smem + oP, maxch * g.PS, tid, nthr);
     if (p.dyn_regtab) {

@@ -88,31 +88,81 @@ struct Gather {
     }
 };
 
-// sequential LDS regions filled by LDS-DMA, one DMA pass per region (CP kernels)
+// sequential LDS regions filled by LDS-DMA (CP kernels). Region r occupies F_r 16-B chunk
+// slots from chunk offset o / 2 (F_r = its bytes rounded up plus one pad chunk, the
+// footprint the host's LDS plan counts).
+//   unpacked: one DMA pass per region (at least one wave instruction per region, however
+//             small: a family block of k_cpp has ~50 regions);
+//   packed (Dev::cp_pack): regions are only recorded (source, first slot; a slot -> region
+//             map in LDS), and issue() sends all slots of the block 64 per wave
+//             instruction, so several short regions share one instruction (each slot reads
+//             16 B of its region's source; pad slots read up to 31 B past a range, inside
+//             the allocation or its 64-B slack).
+constexpr int kStgMaxR = 64, kStgMaxChunks = 4096;
 struct Stg {
     ldsd* base;
     int o;        // next free offset (doubles), kept even
-    int rot = 0;  // wave that issues the next region's first DMA group
+    int rot = 0;  // wave that issues the next region's first DMA group (unpacked)
+    bool pack = false;
+    __attribute__((address_space(3))) unsigned long long* tsrc = nullptr;  // per region: 16-B aligned source of its first slot
+    __attribute__((address_space(3))) int* tc0 = nullptr;                 // per region: first slot
+    __attribute__((address_space(3))) unsigned char* regof = nullptr;
+    int nr = 0;
+    // a region of F slots whose first slot reads s16 (16-B aligned); `bytes` from s16 are data
+    // not inlined: ~50 call sites in k_cpp would otherwise unroll into ~10 KB of straight-
+    // line code, fetched through the instruction cache on every launch
+    __device__ __attribute__((noinline)) ldsd* region(const char* s16, int bytes, int F) {
+        ldsd* dst = base + o;
+        const int c0 = o >> 1;
+        if (pack && nr < kStgMaxR && c0 + F <= kStgMaxChunks) {
+            if (threadIdx.x == 0) {
+                tsrc[nr] = (unsigned long long)(uintptr_t)s16;
+                tc0[nr] = c0;
+            }
+            for (int c = threadIdx.x; c < F; c += blockDim.x) regof[c0 + c] = (unsigned char)nr;
+            ++nr;
+        } else {
+            const int chunks = (bytes + 15) >> 4;
+            const int g = dma_gen(dst, chunks, [=](int ch) { return (const double*)(s16 + 16 * ch); }, rot);
+            rot += g;
+            if (pack)  // slots issued here: issue() skips them
+                for (int c = threadIdx.x; c < F && c0 + c < kStgMaxChunks; c += blockDim.x)
+                    regof[c0 + c] = (unsigned char)kStgMaxR;
+        }
+        o += 2 * F;
+        return dst;
+    }
     template <class PT>
     __device__ __forceinline__ const ldsd* dbl(PT src, int count) {  // count doubles
-        ldsd* dst = base + o;
-        const int sh = dma_any(dst, src, count * 8, &rot);
-        o += rup(count, 2) + 2;
-        return dst + sh;
+        const uintptr_t a = (uintptr_t)src;
+        const int sh = (int)(a & 15);
+        return region((const char*)(a - sh), sh + 8 * count, (rup(count, 2) + 2) >> 1) + (sh >> 3);
     }
     __device__ __forceinline__ const ldsrec* rec(const Rec* src, int count) {  // 16-B records
-        ldsd* dst = base + o;
-        dma_any(dst, (const glbd*)src, count * 16, &rot);
-        o += 2 * count + 2;
-        return (const ldsrec*)dst;
+        return (const ldsrec*)region((const char*)src, 16 * count, count + 1);
     }
     __device__ __forceinline__ const __attribute__((address_space(3))) int* ints(const int* src, int count) {
-        ldsd* dst = base + o;
         const uintptr_t a = (uintptr_t)src;
         const int shb = (int)(a & 15);
-        dma_any(dst, (const glbd*)(a - shb), count * 4 + shb, &rot);
-        o += rup((count * 4 + shb + 7) / 8, 2) + 2;
+        ldsd* dst = region((const char*)(a - shb), count * 4 + shb, (rup((count * 4 + shb + 7) / 8, 2) + 2) >> 1);
         return (const __attribute__((address_space(3))) int*)((__attribute__((address_space(3))) char*)dst + shb);
+    }
+    // packed: send every recorded slot (call once, after the last region, by the whole block)
+    __device__ __forceinline__ void issue() const {
+        if (!pack || nr == 0) return;
+        __syncthreads();  // tab / regof written
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+        const int total = min(o >> 1, kStgMaxChunks);
+        for (int c0 = wave * 64; c0 < total; c0 += nw * 64) {
+            const int ch = c0 + lane;
+            if (ch < total) {
+                const unsigned r = regof[ch];
+                if (r < (unsigned)nr) {
+                    const char* src = (const char*)(uintptr_t)tsrc[r];
+                    __builtin_amdgcn_global_load_lds((const glbd*)(src + 16 * (ch - tc0[r])), base + 2 * c0, 16, 0, 0);
+                }
+            }
+        }
     }
 };
 

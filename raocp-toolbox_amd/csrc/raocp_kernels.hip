@@ -34,6 +34,16 @@ struct Ctl {
     double tol;
 };
 
+// the stopping test of the previous CP iteration run by an extra workgroup (block 0) of the
+// next iteration's first dynamics launch (raocp_capi.hip, defer_check): on = 0 disables it
+struct ChkArg {
+    Ctl* ctl;
+    double* hist;
+    const double* part;
+    int rows;
+    int on;
+};
+
 // explicit address spaces: loads through these types are ds_read / global_load, never flat
 typedef __attribute__((address_space(3))) double ldsd;
 typedef __attribute__((address_space(1))) double glbd;
@@ -94,6 +104,8 @@ struct Dev {
     unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)
     int regstage;          // staging by vector loads + LDS stores instead of LDS-DMA (RAOCP_REGSTAGE)
     int dyn_regtab;        // dynamics kernels stage their matrix tables by vector loads (RAOCP_DYN_REGTAB)
+    int dyn_rot;           // tier kernels rotate the first wave of each staged range (RAOCP_DYN_ROT)
+    int cp_pack;           // k_cpd / k_cpp pack their staged regions into shared DMA instructions (RAOCP_CP_PACK)
     int cp_dbg;            // timing diagnostics only (RAOCP_CP2_DBG bits): skip phases of k_cpd2 / k_cpp2
 };
 
@@ -129,6 +141,29 @@ __device__ __forceinline__ u64 dbits(double v) { return (u64)__double_as_longlon
 // takes its inf-norms with numpy, which propagates NaN, so a NaN residual fails the
 // stopping test `max(error) <= tol` there (solver.py:137-161) and must fail it here too.
 __device__ __forceinline__ double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
+
+// k_cp_check by one wave (the deferred test's extra workgroup): lanes take rows, then a
+// butterfly of NaN-propagating maxima; the same record, history row and decision
+__device__ __forceinline__ void cp_check_wave(const ChkArg& ck) {
+    Ctl* ctl = ck.ctl;
+    if (ctl->done) return;
+    const int lane = threadIdx.x & 63;
+    double m[6] = {0, 0, 0, 0, 0, 0};
+    for (int r = lane; r < ck.rows; r += 64)
+        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], ck.part[(size_t)r * 6 + q]);
+    _Pragma("unroll") for (int off = 32; off > 0; off >>= 1)
+        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], __shfl_xor(m[q], off));
+    if (lane != 0) return;
+    const int k = ctl->k;
+    for (int q = 0; q < 6; ++q) ck.hist[(size_t)k * 6 + q] = m[q];
+    const double err = nmax(nmax(m[0], m[1]), m[2]);
+    if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
+        ctl->done = 1;
+        ctl->final_k = k;
+    } else {
+        ctl->k = k + 1;
+    }
+}
 
 // ---- batched dot products ----------------------------------------------------------
 // All loads of a chunk are issued before its FMAs (a sched_barrier keeps hipcc from
@@ -915,7 +950,6 @@ __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, con
         ctl->k = k + 1;
     }
 }
-
 
 // ---- subtree sharding (raocp_capi.hip, raocp_shard_setup): exchange packing and the
 // residual reduction split around the all-reduce

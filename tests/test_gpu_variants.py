@@ -1,7 +1,10 @@
 """GPU parity of the opt-in kernel variants (measured slower on MI355X than the defaults,
 kept correct): the CP stopping test fused into k_cpp's last block (RAOCP_FUSE_CHECK=1);
-and the default per-parent L^T tiles against the LDS-staged path
-(RAOCP_ELLT_PARENT_TILES=0).
+the eager stopping test after every iteration (RAOCP_DEFER_CHECK=0) against the default
+deferred one; the staging switches (RAOCP_CP_PACK=0: one LDS-DMA pass per staged region
+in k_cpd / k_cpp; RAOCP_DYN_ROT=0: every staged range of the dynamics kernels starts at
+wave 0), which must not change a bit; and the default per-parent L^T tiles against the
+LDS-staged path (RAOCP_ELLT_PARENT_TILES=0).
 
 Tolerances as in test_gpu_parity.py.
 """
@@ -55,6 +58,52 @@ def test_fused_stopping_test_main_py(golden):
     assert status == 0 and solver.error_cache.shape == (937, 3)
     assert trace_rel_err(solver.error_cache, z["main/cp_error"]) <= 1e-8
     assert rel_err(solver.cache.get_primal_flat(), z["main/cp_z"]) <= 1e-9
+
+
+@pytest.mark.parametrize("iters,stop", [(0, None), (1, None), (23, None), (24, None), (30, None), (60, 37), (60, 24)])
+def test_deferred_stopping_test_matches_eager(iters, stop):
+    """The default deferred stopping test (iteration k's test in an extra workgroup of
+    iteration k + 1's first dynamics launch, one k_cp_check per graph batch) against
+    k_cp_check after every iteration: same status, iteration count, history and final
+    iterate, bit for bit, at batch boundaries (24 iterations per graph) and on early stops."""
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    dfr = core.Cache(prob)
+    eag = _with_env({"RAOCP_DEFER_CHECK": "0"}, lambda: core.Cache(prob))
+    alpha = 0.999 / dfr.native.step_size()
+    tol = 0.0
+    if stop is not None:  # a tolerance the run meets at iteration `stop` (or before)
+        _, err, _ = eag.native.cp_run(r["x0"], iters, 0.0, alpha)
+        tol = float(err[stop].max())
+    out = []
+    for cache in (dfr, eag):
+        status, err, derr = cache.native.cp_run(r["x0"], iters, tol, alpha)
+        out.append((status, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
+    (s1, e1, d1, z1, y1), (s2, e2, d2, z2, y2) = out
+    assert s1 == s2 and e1.shape == e2.shape
+    assert np.array_equal(e1, e2) and np.array_equal(d1, d2)
+    assert np.array_equal(z1, z2) and np.array_equal(y1, y2)
+    if stop is not None:
+        assert s1 == 0 and e1.shape[0] <= stop + 1  # stopped early
+
+
+@pytest.mark.parametrize("env", [{"RAOCP_CP_PACK": "0"}, {"RAOCP_DYN_ROT": "0"}], ids=["cp_pack0", "dyn_rot0"])
+@pytest.mark.parametrize("cfg", [1, 2])
+def test_staging_switches_bit_identical(env, cfg):
+    """Staging only moves bytes: the CP loop with a staging switch flipped reproduces the
+    default run bit for bit (config 1: the generic-size kernels; config 2: the benchmark)."""
+    from raocp.problems import recipe_main
+    r = recipe_main() if cfg == 1 else recipe_config(2)
+    tree, prob = build_problem(r)
+    a = core.Cache(prob)
+    b = _with_env(env, lambda: core.Cache(prob))
+    alpha = 0.999 / a.native.step_size()
+    out = []
+    for cache in (a, b):
+        status, err, derr = cache.native.cp_run(r["x0"], 12, 0.0, alpha)
+        out.append((status, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
+    for u, v in zip(out[0], out[1]):
+        assert np.array_equal(u, v)
 
 
 @pytest.mark.parametrize("cfg", [2, 3, 4, "4-modes"])
