@@ -1826,7 +1826,10 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     if (const char* e = getenv("RAOCP_DYN_REGTAB")) c->dev.dyn_regtab = atoi(e) != 0;
     c->dev.dyn_rot = 1;  // RAOCP_DYN_ROT=0: every staged range starts at wave 0
     if (const char* e = getenv("RAOCP_DYN_ROT")) c->dev.dyn_rot = atoi(e) != 0;
-    c->dev.cp_pack = 1;  // RAOCP_CP_PACK=0: one LDS-DMA pass per staged region in k_cpd / k_cpp
+    // RAOCP_CP_PACK=1: the CP / L^T kernels pack their staged regions into shared LDS-DMA
+    // instructions (StgTable). Measured neutral at config 2 and 4-6 % slower at configs 3-5
+    // (the slot map costs two more barriers per block), so one pass per region is the default.
+    c->dev.cp_pack = 0;
     if (const char* e = getenv("RAOCP_CP_PACK")) c->dev.cp_pack = atoi(e) != 0;
     {
         // L by streaming wave tasks (raocp_ell3.hip): compile-time sizes, and one sqrtQ / sqrtR

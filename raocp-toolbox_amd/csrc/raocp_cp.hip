@@ -40,14 +40,7 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
     glbd* eo = (glbd*)bf.e1;               // eta+
     glbd* xi2 = (glbd*)xi2_;
     const int bid = blockIdx.x;
-    __shared__ unsigned long long s_tsrc[kStgMaxR];
-    __shared__ int s_tc0[kStgMaxR];
-    __shared__ unsigned char s_regof[kStgMaxChunks];
-    Stg st{(ldsd*)smem_, 0};
-    st.pack = p.cp_pack;
-    st.tsrc = (__attribute__((address_space(3))) unsigned long long*)s_tsrc;
-    st.tc0 = (__attribute__((address_space(3))) int*)s_tc0;
-    st.regof = (__attribute__((address_space(3))) unsigned char*)s_regof;
+    Stg st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
     double m2 = 0.0, m5 = 0.0;
     auto finish = [&](int e, double dv, double v, double pv, double b) {
         const double ep = alpha * (v - pv);
@@ -353,14 +346,7 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
     const glbd* dA = (const glbd*)bf.e1;   // eta+
     const glbd* xg = (const glbd*)xi2_;
     const int bid = blockIdx.x;
-    __shared__ unsigned long long s_tsrc[kStgMaxR];
-    __shared__ int s_tc0[kStgMaxR];
-    __shared__ unsigned char s_regof[kStgMaxChunks];
-    Stg st{(ldsd*)smem_, 0};
-    st.pack = p.cp_pack;
-    st.tsrc = (__attribute__((address_space(3))) unsigned long long*)s_tsrc;
-    st.tc0 = (__attribute__((address_space(3))) int*)s_tc0;
-    st.regof = (__attribute__((address_space(3))) unsigned char*)s_regof;
+    Stg st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
     double m0 = 0.0, m1 = 0.0, m3 = 0.0, m4 = 0.0;
     stamp(p, 0);
     // residual terms of one primal entry: pp = p, zz = z+, w = L^T(d - eta+), lc = L^T xi2

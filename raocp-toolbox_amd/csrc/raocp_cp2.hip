@@ -68,8 +68,8 @@ using cglbp = const __attribute__((address_space(1))) U*;
 // misalignment); host mirror: cp2_region_bytes in raocp_capi.hip.
 struct StgB {
     ldsd* base;
-    int o = 0;    // next free byte offset (multiple of 16)
-    int rot = 0;  // wave that issues the next region's first DMA group
+    int o = 0;  // next free byte offset (multiple of 16)
+    StgTable tab;
     template <class U>
     __device__ __forceinline__ ldsp<U> arr(const U* src, int count) {
         typedef __attribute__((address_space(3))) char lchar;
@@ -78,10 +78,12 @@ struct StgB {
         const int nb = count > 0 ? count * (int)sizeof(U) : 0;
         const int chunks = nb > 0 ? (sh + nb + 15) >> 4 : 0;
         lchar* dst = (lchar*)base + o;
-        if (chunks) rot += dma_gen((ldsd*)dst, chunks, [=](int ch) { return (const double*)(a - sh + 16 * ch); }, rot);
+        tab.record((const char*)(a - sh), chunks ? sh + nb : 0, o >> 4);
         o += 16 * chunks + 16;
         return (ldsp<U>)(dst + sh);
     }
+    // send the recorded regions (StgTable::issue: packed or one pass per region)
+    __device__ __forceinline__ void issue() const { tab.issue(base, o >> 4); }
 };
 
 // sum over the 16 lanes of a lane group (lanes h*16 .. h*16+15)
@@ -245,7 +247,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
     const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int lo = lane & 15, h = lane >> 4;
     const crec4* tab = (const crec4*)p.cp2_tab;
-    StgB st{(ldsd*)smem_};
+    StgB st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
     double m2 = 0.0, m5 = 0.0;
     T alpha = T(0), ra = T(0);  // alpha and 1 / alpha (products instead of divisions: 1 ulp)
     auto finish = [&](int e, T dv, T v, T pv, T b) {
@@ -284,6 +286,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
         const int nBx = p.nBnl * (nx + nu);
         const ldsp<T> BL = st.arr((const T*)p.blo_nl, nBx);
         const ldsp<T> BH = st.arr((const T*)p.bhi_nl, nBx);
+        st.issue();
         const int tq = t2.x, tr = t2.y;
         WFr<T, RTX> wq;
         WFr<T, RTU> wr;
@@ -435,6 +438,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
         const int nBx = p.nBl * nx;
         const ldsp<T> BL = st.arr((const T*)p.blo_l, nBx);
         const ldsp<T> BH = st.arr((const T*)p.bhi_l, nBx);
+        st.issue();
         const int tp = t1.x;
         WFr<T, RTX> wp;
         if (tp >= 0) wp.load((const T*)p.SP, tp, nx);
@@ -536,7 +540,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
     const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int lo = lane & 15, h = lane >> 4;
     const crec4* tab = (const crec4*)p.cp2_tab;
-    StgB st{(ldsd*)smem_};
+    StgB st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
     double m0 = 0.0, m1 = 0.0, m3 = 0.0, m4 = 0.0;
     T alpha = T(0), ra = T(0);
     // residual terms of one primal entry: pp = p, zz = z+, w = L^T(d - eta+), lc = L^T xi2
@@ -584,6 +588,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
         const ldsp<T> AR = st.arr((const T*)p.alpha_r + i0, P);
         const ldsp<Rec> FR = st.arr(p.frec + i0, P);  // {yrel, nch, ch_start, e7off}
         const ldsp<Rec> CR = st.arr(p.crec + cb, C);  // {anc, iSQ, iSR, 0}
+        st.issue();
         const int tq = t2.x, tr = t2.y, creg = t2.z;
         WFr<T, RTX> wq;
         WFr<T, RTU> wr;
@@ -829,6 +834,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
         const ldsp<T> Xz = st.arr(zp + p.X0 + (size_t)l0 * nx, Lc * nx);
         const ldsp<T> Xp = st.arr(pz + p.X0 + (size_t)l0 * nx, Lc * nx);
         const ldsp<Rec> LR = st.arr(p.lrec + (l0 - p.m), Lc);
+        st.issue();
         const int tp = t1.x;
         WFr<T, RTX> wp;
         if (tp >= 0) wp.load((const T*)p.SP, tp, nx);

@@ -90,45 +90,86 @@ struct Gather {
 
 // sequential LDS regions filled by LDS-DMA (CP kernels). Region r occupies F_r 16-B chunk
 // slots from chunk offset o / 2 (F_r = its bytes rounded up plus one pad chunk, the
-// footprint the host's LDS plan counts).
-//   unpacked: one DMA pass per region (at least one wave instruction per region, however
-//             small: a family block of k_cpp has ~50 regions);
-//   packed (Dev::cp_pack): regions are only recorded (source, first slot; a slot -> region
-//             map in LDS), and issue() sends all slots of the block 64 per wave
-//             instruction, so several short regions share one instruction (each slot reads
-//             16 B of its region's source; pad slots read up to 31 B past a range, inside
-//             the allocation or its 64-B slack).
+// footprint the host's LDS plan counts). The regions are only recorded (source, first
+// slot, slots: a table in LDS, a few instructions per region); issue() then sends them:
+//   packed (Dev::cp_pack): every slot of the block, 64 per wave instruction, through a
+//             slot -> region map, so several short regions share one instruction;
+//   unpacked: one DMA pass per region (at least one instruction per region, however small:
+//             a family block of k_cpp has ~50 regions).
+// Only a region's data chunks are loaded (its first chunk may start up to 8 B before the
+// range, its last end up to 15 B after it: inside the allocation or its 64-B slack).
+// (Recording instead of issuing per call keeps the kernels small: the inlined per-region
+// DMA loops made k_cpp 89 KB of code, more than the instruction cache.)
 constexpr int kStgMaxR = 64, kStgMaxChunks = 4096;
+// the recorded regions of one block (LDS tables: each kernel declares them, StgLds)
+struct StgTable {
+    __attribute__((address_space(3))) unsigned long long* tsrc = nullptr;  // per region: 16-B aligned source
+    __attribute__((address_space(3))) int* tc0 = nullptr;                 // per region: first slot
+    __attribute__((address_space(3))) int* tF = nullptr;                  // per region: chunks to load
+    __attribute__((address_space(3))) unsigned char* regof = nullptr;     // slot -> region (packed)
+    int nr = 0;
+    bool pack = false;
+    __device__ __forceinline__ void record(const char* s16, int bytes, int c0) {
+        if (threadIdx.x == 0 && nr < kStgMaxR) {
+            tsrc[nr] = (unsigned long long)(uintptr_t)s16;
+            tc0[nr] = c0;
+            tF[nr] = bytes > 0 ? (bytes + 15) >> 4 : 0;
+        }
+        ++nr;
+    }
+    // send every recorded region into slots from `base` (call once, after the last region,
+    // by the whole block); total = slots of the footprint
+    __device__ __forceinline__ void issue(ldsd* base, int total) const {
+        __syncthreads();  // the region table is written
+        const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
+        const int R = min(nr, kStgMaxR);
+        if (pack && total <= kStgMaxChunks) {
+            for (int c = tid; c < total; c += nt) regof[c] = (unsigned char)kStgMaxR;  // footprint slots not loaded
+            __syncthreads();
+            _Pragma("unroll 1") for (int r = 0; r < R; ++r) {
+                const int c0 = tc0[r], F = tF[r];
+                for (int c = tid; c < F; c += nt) regof[c0 + c] = (unsigned char)r;
+            }
+            __syncthreads();
+            for (int c0 = wave * 64; c0 < total; c0 += nw * 64) {
+                const int ch = c0 + lane;
+                const int r = ch < total ? regof[ch] : kStgMaxR;
+                if (r < kStgMaxR) {
+                    const char* src = (const char*)(uintptr_t)tsrc[r];
+                    __builtin_amdgcn_global_load_lds((const glbd*)(src + 16 * (ch - tc0[r])), base + 2 * c0, 16, 0, 0);
+                }
+            }
+        } else {
+            int rot = 0;
+            _Pragma("unroll 1") for (int r = 0; r < R; ++r) {
+                const char* src = (const char*)(uintptr_t)tsrc[r];
+                rot += dma_gen(base + 2 * tc0[r], tF[r], [=](int ch) { return (const double*)(src + 16 * ch); }, rot);
+            }
+        }
+    }
+};
+// the LDS tables of a StgTable, declared once per kernel (a __shared__ array in an inlined
+// device function is one allocation per kernel that uses it)
+__device__ __forceinline__ StgTable stg_table(bool pack) {
+    __shared__ unsigned long long s_tsrc[kStgMaxR];
+    __shared__ int s_tc0[kStgMaxR], s_tF[kStgMaxR];
+    __shared__ unsigned char s_regof[kStgMaxChunks];
+    StgTable t;
+    t.tsrc = (__attribute__((address_space(3))) unsigned long long*)s_tsrc;
+    t.tc0 = (__attribute__((address_space(3))) int*)s_tc0;
+    t.tF = (__attribute__((address_space(3))) int*)s_tF;
+    t.regof = (__attribute__((address_space(3))) unsigned char*)s_regof;
+    t.pack = pack;
+    return t;
+}
 struct Stg {
     ldsd* base;
-    int o;        // next free offset (doubles), kept even
-    int rot = 0;  // wave that issues the next region's first DMA group (unpacked)
-    bool pack = false;
-    __attribute__((address_space(3))) unsigned long long* tsrc = nullptr;  // per region: 16-B aligned source of its first slot
-    __attribute__((address_space(3))) int* tc0 = nullptr;                 // per region: first slot
-    __attribute__((address_space(3))) unsigned char* regof = nullptr;
-    int nr = 0;
-    // a region of F slots whose first slot reads s16 (16-B aligned); `bytes` from s16 are data
-    // not inlined: ~50 call sites in k_cpp would otherwise unroll into ~10 KB of straight-
-    // line code, fetched through the instruction cache on every launch
-    __device__ __attribute__((noinline)) ldsd* region(const char* s16, int bytes, int F) {
+    int o;  // next free offset (doubles), kept even
+    StgTable tab;
+    // a region of F slots whose first `bytes` from s16 (16-B aligned) are data
+    __device__ __forceinline__ ldsd* region(const char* s16, int bytes, int F) {
         ldsd* dst = base + o;
-        const int c0 = o >> 1;
-        if (pack && nr < kStgMaxR && c0 + F <= kStgMaxChunks) {
-            if (threadIdx.x == 0) {
-                tsrc[nr] = (unsigned long long)(uintptr_t)s16;
-                tc0[nr] = c0;
-            }
-            for (int c = threadIdx.x; c < F; c += blockDim.x) regof[c0 + c] = (unsigned char)nr;
-            ++nr;
-        } else {
-            const int chunks = (bytes + 15) >> 4;
-            const int g = dma_gen(dst, chunks, [=](int ch) { return (const double*)(s16 + 16 * ch); }, rot);
-            rot += g;
-            if (pack)  // slots issued here: issue() skips them
-                for (int c = threadIdx.x; c < F && c0 + c < kStgMaxChunks; c += blockDim.x)
-                    regof[c0 + c] = (unsigned char)kStgMaxR;
-        }
+        tab.record(s16, bytes, o >> 1);
         o += 2 * F;
         return dst;
     }
@@ -136,7 +177,7 @@ struct Stg {
     __device__ __forceinline__ const ldsd* dbl(PT src, int count) {  // count doubles
         const uintptr_t a = (uintptr_t)src;
         const int sh = (int)(a & 15);
-        return region((const char*)(a - sh), sh + 8 * count, (rup(count, 2) + 2) >> 1) + (sh >> 3);
+        return region((const char*)(a - sh), count > 0 ? sh + 8 * count : 0, (rup(count, 2) + 2) >> 1) + (sh >> 3);
     }
     __device__ __forceinline__ const ldsrec* rec(const Rec* src, int count) {  // 16-B records
         return (const ldsrec*)region((const char*)src, 16 * count, count + 1);
@@ -144,26 +185,11 @@ struct Stg {
     __device__ __forceinline__ const __attribute__((address_space(3))) int* ints(const int* src, int count) {
         const uintptr_t a = (uintptr_t)src;
         const int shb = (int)(a & 15);
-        ldsd* dst = region((const char*)(a - shb), count * 4 + shb, (rup((count * 4 + shb + 7) / 8, 2) + 2) >> 1);
+        ldsd* dst = region((const char*)(a - shb), count > 0 ? count * 4 + shb : 0,
+                           (rup((count * 4 + shb + 7) / 8, 2) + 2) >> 1);
         return (const __attribute__((address_space(3))) int*)((__attribute__((address_space(3))) char*)dst + shb);
     }
-    // packed: send every recorded slot (call once, after the last region, by the whole block)
-    __device__ __forceinline__ void issue() const {
-        if (!pack || nr == 0) return;
-        __syncthreads();  // tab / regof written
-        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-        const int total = min(o >> 1, kStgMaxChunks);
-        for (int c0 = wave * 64; c0 < total; c0 += nw * 64) {
-            const int ch = c0 + lane;
-            if (ch < total) {
-                const unsigned r = regof[ch];
-                if (r < (unsigned)nr) {
-                    const char* src = (const char*)(uintptr_t)tsrc[r];
-                    __builtin_amdgcn_global_load_lds((const glbd*)(src + 16 * (ch - tc0[r])), base + 2 * c0, 16, 0, 0);
-                }
-            }
-        }
-    }
+    __device__ __forceinline__ void issue() const { tab.issue(base, o >> 1); }
 };
 
 typedef __attribute__((address_space(4))) const Rec crec4;  // scalar (constant) loads

@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(256) k_ell2(Dev p, const double* __restrict__ 
     const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int lo = lane & 15, h = lane >> 4;
     const crec4* tab = (const crec4*)p.cp2_tab;
-    StgB st{(ldsd*)smem_};
+    StgB st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
     if (bid < nbF) {
         const Rec t0 = tab[kCpFamRecs * bid], t1 = tab[kCpFamRecs * bid + 1], t2 = tab[kCpFamRecs * bid + 2];
         const int i0 = t1.z, i1 = t1.w, P = i1 - i0;
@@ -39,6 +39,7 @@ __global__ void __launch_bounds__(256) k_ell2(Dev p, const double* __restrict__ 
         const ldsp<T> CD = st.arr((const T*)p.cond + cb, C);
         const ldsp<Rec> FR = st.arr(p.frec + i0, P);
         const ldsp<Rec> CR = st.arr(p.crec + cb, C);
+        st.issue();
         WFr<T, RTX> wq;
         WFr<T, RTU> wr;
         wq.load((const T*)p.SQ, t2.x, nx);
@@ -102,6 +103,7 @@ __global__ void __launch_bounds__(256) k_ell2(Dev p, const double* __restrict__ 
         const ldsp<T> X = st.arr(z + p.X0 + (size_t)l0 * nx, Lc * nx);
         const ldsp<T> S = st.arr(z + p.S0 + l0, Lc);
         const ldsp<Rec> LR = st.arr(p.lrec + (l0 - p.m), Lc);
+        st.issue();
         WFr<T, RTX> wp;
         wp.load((const T*)p.SP, t1.x, nx);
         dma_wait();
@@ -146,7 +148,7 @@ __global__ void __launch_bounds__(256) k_ellt2(Dev p, const double* __restrict__
     const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int lo = lane & 15, h = lane >> 4;
     const crec4* tab = (const crec4*)p.cp2_tab;
-    StgB st{(ldsd*)smem_};
+    StgB st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
     if (bid < nbF) {
         const Rec t0 = tab[kCpFamRecs * bid], t1 = tab[kCpFamRecs * bid + 1], t2 = tab[kCpFamRecs * bid + 2];
         const int i0 = t1.z, i1 = t1.w, P = i1 - i0;
@@ -160,6 +162,7 @@ __global__ void __launch_bounds__(256) k_ellt2(Dev p, const double* __restrict__
         const ldsp<T> D7 = st.arr(d + e7a, E7n);
         const ldsp<T> CD = st.arr((const T*)p.cond + cb, C);
         const ldsp<Rec> FR = st.arr(p.frec + i0, P);
+        st.issue();
         const int creg = t2.z;
         WFr<T, RTX> wq;
         WFr<T, RTU> wr;
@@ -273,6 +276,7 @@ __global__ void __launch_bounds__(256) k_ellt2(Dev p, const double* __restrict__
         const ldsp<T> D12 = st.arr(d + p.E12 + l0, Lc);
         const ldsp<T> D13 = st.arr(d + p.E13 + l0, Lc);
         const ldsp<Rec> LR = st.arr(p.lrec + (l0 - p.m), Lc);
+        st.issue();
         WFr<T, RTX> wp;
         wp.load((const T*)p.SP, t1.x, nx);
         dma_wait();

@@ -1,8 +1,8 @@
 """GPU parity of the opt-in kernel variants (measured slower on MI355X than the defaults,
 kept correct): the CP stopping test fused into k_cpp's last block (RAOCP_FUSE_CHECK=1);
 the eager stopping test after every iteration (RAOCP_DEFER_CHECK=0) against the default
-deferred one; the staging switches (RAOCP_CP_PACK=0: one LDS-DMA pass per staged region
-in k_cpd / k_cpp; RAOCP_DYN_ROT=0: every staged range of the dynamics kernels starts at
+deferred one; the staging switches (RAOCP_CP_PACK=1: the staged regions of k_cpd / k_cpp
+packed into shared LDS-DMA instructions; RAOCP_DYN_ROT=0: every staged range of the dynamics kernels starts at
 wave 0), which must not change a bit; and the default per-parent L^T tiles against the
 LDS-staged path (RAOCP_ELLT_PARENT_TILES=0).
 
@@ -87,7 +87,7 @@ def test_deferred_stopping_test_matches_eager(iters, stop):
         assert s1 == 0 and e1.shape[0] <= stop + 1  # stopped early
 
 
-@pytest.mark.parametrize("env", [{"RAOCP_CP_PACK": "0"}, {"RAOCP_DYN_ROT": "0"}], ids=["cp_pack0", "dyn_rot0"])
+@pytest.mark.parametrize("env", [{"RAOCP_CP_PACK": "1"}, {"RAOCP_DYN_ROT": "0"}], ids=["cp_pack1", "dyn_rot0"])
 @pytest.mark.parametrize("cfg", [1, 2])
 def test_staging_switches_bit_identical(env, cfg):
     """Staging only moves bytes: the CP loop with a staging switch flipped reproduces the
