@@ -30,11 +30,31 @@ struct WPerm {
     }
 };
 
+// 16-B vectors of T at 4- / 8-B alignment (rows and output tiles start wherever the
+// reference's flat layout puts them; gfx950 global memory takes unaligned vector accesses)
+template <class T>
+struct Vec16 {
+    static constexpr int V = 16 / (int)sizeof(T);
+    typedef T type __attribute__((ext_vector_type(16 / sizeof(T)), aligned(sizeof(T))));
+};
+
 // A values of a lane: a[s] = v[KC h + s] for k < K (v a global row pointer or null)
 template <class T, int K>
 __device__ __forceinline__ void load_arow(cglbp<T> v, T (&a)[(K + 3) / 4]) {
-    constexpr int KC = (K + 3) / 4;
+    constexpr int KC = (K + 3) / 4, V = Vec16<T>::V;
+    typedef typename Vec16<T>::type vt;
     const int h = (threadIdx.x & 63) >> 4;
+    if constexpr (K % 4 == 0 && KC % V == 0) {
+        if (v) {  // whole 16-B loads
+            _Pragma("unroll") for (int s = 0; s < KC; s += V) {
+                const vt w = *(const __attribute__((address_space(1))) vt*)(v + KC * h + s);
+                _Pragma("unroll") for (int u = 0; u < V; ++u) a[s + u] = w[u];
+            }
+        } else {
+            _Pragma("unroll") for (int s = 0; s < KC; ++s) a[s] = T(0);
+        }
+        return;
+    }
     if (v && (K % 4 == 0 || h < 3)) {
         _Pragma("unroll") for (int s = 0; s < KC; ++s) a[s] = v[KC * h + s];
     } else {
@@ -67,9 +87,22 @@ __device__ __forceinline__ void store_tile(__attribute__((address_space(3))) T* 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     const int tot = cnt * R;
-    for (int q = lane; q < tot; q += 64) {
-        const int a = q / R, r = q - a * R;
-        dst[q] = img[a * S + r];
+    constexpr int V = Vec16<T>::V;
+    if constexpr (R % V == 0) {
+        // 16 B per lane (a lane's V elements lie in one row): a quarter (fp32) / half (fp64)
+        // of the store instructions of one element per lane
+        typedef typename Vec16<T>::type vt;
+        for (int q = lane * V; q < tot; q += 64 * V) {
+            const int a = q / R, r = q - a * R;
+            vt w;
+            _Pragma("unroll") for (int u = 0; u < V; ++u) w[u] = img[a * S + r + u];
+            *(__attribute__((address_space(1))) vt*)(dst + q) = w;
+        }
+    } else {
+        for (int q = lane; q < tot; q += 64) {
+            const int a = q / R, r = q - a * R;
+            dst[q] = img[a * S + r];
+        }
     }
     __builtin_amdgcn_wave_barrier();
 }
