@@ -107,7 +107,8 @@ struct raocp_ctx {
     double* redpart = nullptr;   // per-block residual maxima [red_rows][6]
     int red_rows = 0;
     size_t lds_top = 0;
-    int dyn_block = 1024;
+    int dyn_block = 1024;        // tier workgroups (RAOCP_DYN_BLOCK)
+    int dyn_top_block = 1024;    // the top's single workgroup (RAOCP_DYN_TOP_BLOCK)
     // node-block CP kernels (raocp_cp.hip): family / leaf block sizes, grid, LDS bytes
     int cp_FB = 1, cp_LB = 1, cp_nbF = 0, cp_nbL = 0;
     int ell_nb = 0, ell_threads = 512;  // L / L^T blocks (raocp_ell.hip), threads, LDS bytes
@@ -416,7 +417,8 @@ struct DynOp {
                                        : (c->fold_top ? raocp::k_dyn_top<NX, NU, false, true> : raocp::k_dyn_top<NX, NU, false, false>);
                 allow_lds(kt, c->lds_top);
                 const int T = c->stage_ptr[s], nb = c->stage_ptr[s + 1] - T;
-                kt<<<1, B, c->lds_top, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->x0, s, c->maxch_top, c1, p1, T, nb);
+                kt<<<1, c->dyn_top_block, c->lds_top, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->x0, s, c->maxch_top, c1,
+                                                                   p1, T, nb);
             }
             for (int k = 0; k < (int)c->tiers.size(); ++k) {
                 const auto& tp = c->tiers[k];
@@ -1453,6 +1455,21 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         int n_cus = 0;
         if (hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cus <= 0)
             n_cus = 256;
+        // workgroup sizes (multiples of 64, at most 1024). The plan below is costed for
+        // 1024-lane workgroups; launching its tiers with 512 lanes measured 98.0 vs 106.5 us
+        // per CP iteration at config 2 and 577 vs 589 us at config 4 (more co-resident
+        // workgroups per CU, cheaper barriers), while re-costing the plan for 512 or 256
+        // lanes picked worse plans (config 4: 906 / 815 us). RAOCP_DYN_BLOCK /
+        // RAOCP_DYN_TOP_BLOCK override.
+        auto wg_env = [](const char* name, int def) {
+            const char* e = getenv(name);
+            const int v = e ? atoi(e) : def;
+            return v >= 64 && v <= 1024 && v % 64 == 0 ? v : def;
+        };
+        c->dyn_block = wg_env("RAOCP_DYN_BLOCK", 512);
+        c->dyn_top_block = wg_env("RAOCP_DYN_TOP_BLOCK", 1024);
+        if (R * raocp::kKS > c->dyn_block) c->dyn_block = 1024;  // a child's split-k rows in one workgroup
+        const long wg_per_cu = 2;
         auto level_cost = [&](double P, double C) { return 3.0 + (C * R + P * R + P * nu + C * nx) / 384.0; };
         auto recs = [](size_t cnt) { return 2 * cnt; };  // 16-B records in doubles
         // fold: one-phase backward levels (per-pair WT tables instead of per-kind W, no P rows)
@@ -1510,13 +1527,13 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 w.bf -= 8 * npr * F1;
                 w.cost += 2 * (b - a);
             }
-            // the tier's subtrees run as rounds of co-resident workgroups (two 1024-lane
-            // workgroups per CU at most, fewer when their LDS does not fit): every round
+            // the tier's subtrees run as rounds of co-resident workgroups (2048 lanes per CU
+            // at most, fewer workgroups when their LDS does not fit): every round
             // pays the levels again (measured at configs 3 / 4: deep tiers of thousands of
             // subtrees lost to one-level tiers)
             {
                 const size_t lds = std::max(w.bb, w.bf);
-                const long per_cu = std::max<long>(1, std::min<long>(2, lds ? (long)(160 * 1024 / lds) : 2));
+                const long per_cu = std::max<long>(1, std::min<long>(wg_per_cu, lds ? (long)(160 * 1024 / lds) : wg_per_cu));
                 const long nsub = c->stage_ptr[a + 1] - c->stage_ptr[a];
                 const long rounds = (nsub + (long)n_cus * per_cu - 1) / ((long)n_cus * per_cu);
                 w.cost *= (double)std::max<long>(1, rounds);
@@ -1826,6 +1843,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     if (const char* e = getenv("RAOCP_DYN_REGTAB")) c->dev.dyn_regtab = atoi(e) != 0;
     c->dev.dyn_rot = 1;  // RAOCP_DYN_ROT=0: every staged range starts at wave 0
     if (const char* e = getenv("RAOCP_DYN_ROT")) c->dev.dyn_rot = atoi(e) != 0;
+
     // RAOCP_CP_PACK=1: the CP / L^T kernels pack their staged regions into shared LDS-DMA
     // instructions (StgTable). Measured neutral at config 2 and 4-6 % slower at configs 3-5
     // (the slot map costs two more barriers per block), so one pass per region is the default.

@@ -55,10 +55,12 @@ struct Problem {
         bl_lo.assign(nx, -1.0); bl_hi.assign(nx, 1.0);
         A.assign(nx * nx, 0.0);
         for (int k = 0; k < nx; ++k) A[k * nx + k] = 0.5;
-        B.assign(nx * nu, 0.1);
+        // B = 0 makes the offline products exact for any P (cache.py:207-233): R~ = I,
+        // K = 0, Abar = A, M = K' + sum Abar' P B = 0, so the projection is the true one
+        B.assign(nx * nu, 0.0);
         K.assign(N * nu * nx, 0.0);
         Rinv.assign(N * nu * nu, 0.0);
-        for (int c = 0; c < N; ++c) for (int k = 0; k < nu; ++k) Rinv[c * nu * nu + k * nu + k] = 0.5;
+        for (int c = 0; c < N; ++c) for (int k = 0; k < nu; ++k) Rinv[c * nu * nu + k * nu + k] = 1.0;
         M.assign(N * nx * nu, 0.0);
         t = raocp_tree_desc{n, m, nx, nu, anc.data(), stage.data(), ch_start.data(), nch.data()};
         p.n_sq = p.n_sr = p.n_sp = 1;
@@ -176,5 +178,6 @@ int main(int argc, char** argv) {
     cpu_checks();
     if (gpu) gpu_checks();
     printf("abi_driver %s: %s\n", gpu ? "gpu" : "cpu", g_fail ? "FAILED" : "ok");
+    fflush(stdout);
     return g_fail ? 1 : 0;
 }

@@ -9,3 +9,5 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 240 rocprofv3 --pmc $ctr --kernel-trace -d gpurun_out/pmc2_$ctr -o pmc --output-format csv -- python3 bench.py --steps 96 --warmup 24 --no-cpu --no-shard --op-reps 200 > gpurun_out/pmc2_$ctr.log 2>&1 || { echo "pmc pass $ctr failed"; exit 1; }
 done
 echo pmc_done
+timeout -k 10 120 python3 tools/stamps.py 2 > gpurun_out/stamps_c2.log 2>&1 || exit 1
+timeout -k 10 120 ./build/asan_abi gpu > gpurun_out/asan_gpu.log 2>&1; echo "asan gpu rc=$?"; tail -2 gpurun_out/asan_gpu.log
