@@ -51,6 +51,9 @@ struct raocp_ctx {
     bool dyn32 = false;          // the per-stage T-templated dynamics (raocp_dyn2.hip) is planned
     bool ell3 = false;           // L by streaming wave tasks (raocp_ell3.hip)
     int ell3_grid = 0;
+    int unif_C = 0;              // uniform branching factor <= 4 with uniform tables (0 = not)
+    int ellt3_C = 0;             // L^T by streaming wave tasks: uniform branching factor (0 = off)
+    int ellt3_grid = 0;
     // per-stage MFMA dynamics (raocp_dyn2.hip): tables, node lists, tile lists per stage
     bool dyn2 = false;           // fp32 contexts always; fp64 opt-in RAOCP_DYN2=1
     const double *W2 = nullptr, *RG2 = nullptr, *KM2 = nullptr, *F2 = nullptr;
@@ -313,9 +316,9 @@ struct Ell2Op {
 template <class T>
 bool launch_ell3(raocp_ctx* c, const double* z, double* eta) {
     const int g = c->ell3_grid;
-    if (c->nx == 20 && c->nu == 8) raocp::k_ell3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, z, eta);
-    else if (c->nx == 32 && c->nu == 12) raocp::k_ell3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, z, eta);
-    else if (c->nx == 64 && c->nu == 16) raocp::k_ell3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, z, eta);
+    if (c->nx == 20 && c->nu == 8) raocp::k_ell3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C);
+    else if (c->nx == 32 && c->nu == 12) raocp::k_ell3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C);
+    else if (c->nx == 64 && c->nu == 16) raocp::k_ell3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C);
     else return false;
     return true;
 }
@@ -333,7 +336,18 @@ struct EllTOp {
         if (c->ell_nb) k<<<c->ell_nb, c->ell_threads, c->ellt_lds, c->stream>>>(c->dev, eta, z);
     }
 };
+// L^T as streaming wave tasks (raocp_ell3.hip): uniform tables and branching
+template <class T>
+bool launch_ellt3(raocp_ctx* c, const double* eta, double* z) {
+    const int g = c->ellt3_grid, C = c->ellt3_C;
+    if (c->nx == 20 && c->nu == 8) raocp::k_ellt3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C);
+    else if (c->nx == 32 && c->nu == 12) raocp::k_ellt3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C);
+    else if (c->nx == 64 && c->nu == 16) raocp::k_ellt3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C);
+    else return false;
+    return true;
+}
 void launch_ell_t(raocp_ctx* c, const double* eta, double* z) {
+    if (c->ellt3_C && (c->f32 ? launch_ellt3<float>(c, eta, z) : launch_ellt3<double>(c, eta, z))) return;
     if (c->f32) dispatch_rt(c->nx, c->nu, Ell2Op<float>{}, c, eta, z, true);
     else dispatch(c->nx, c->nu, EllTOp{}, c, eta, z);
 }
@@ -1864,6 +1878,22 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         const long tasks = (long)(n - 1 + 15) / 16 + (n - m + 15) / 16 + ((long)m * (nx + nu) + (c->dev.T0 - c->dev.Y0) + m + 63) / 64;
         c->ell3_grid = (int)std::max(1L, std::min((tasks + 3) / 4, 4096L));
         if (const char* e = getenv("RAOCP_ELL3_GRID")) c->ell3_grid = std::max(1, atoi(e));
+        // L^T by streaming wave tasks: additionally one branching factor C <= 4 over all
+        // nonleaf nodes (children 1 + C i .., y_i at (2C + 1) i); RAOCP_ELLT3=0 keeps k_ell_t
+        int C = m > 0 ? t->nch[0] : 0;
+        bool reg = uni && C >= 1 && C <= 4;
+        for (int i = 0; i < m && reg; ++i)
+            if (t->nch[i] != C || t->ch_start[i] != 1 + C * i) reg = false;
+        c->unif_C = reg ? C : 0;
+        if (const char* e = getenv("RAOCP_ELLT3")) reg = reg && atoi(e) != 0;
+        c->ellt3_C = reg ? C : 0;
+        const long tasks_t = (long)(m + 4 * (4 / std::max(C, 1)) - 1) / (4 * (4 / std::max(C, 1))) + (n - m + 15) / 16 +
+                             ((long)(c->dev.T0 - c->dev.Y0) + 2L * n - 1 + 63) / 64;
+        // grid sweep (profiles/r02_v2/ab_ellt3.log): fp64 config 4 best at 4,096 blocks
+        // (27.8 us vs 31.9 at 1,024), fp32 config 5 at 1,024 (163 vs 184 us at 4,096: each
+        // wave loads a 16-KB sqrtQ fragment, so fewer waves with more tiles each win there)
+        c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, c->f32 ? 1024L : 4096L));
+        if (const char* e = getenv("RAOCP_ELLT3_GRID")) c->ellt3_grid = std::max(1, atoi(e));
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels
     if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = atoi(e);

@@ -108,7 +108,7 @@ __device__ __forceinline__ void store_tile(__attribute__((address_space(3))) T* 
 }
 
 template <class T, int NX, int NU>
-__global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ z_, double* __restrict__ eta_) {
+__global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ z_, double* __restrict__ eta_, int C) {
     typedef typename MF<T>::v4 v4;
     constexpr int nx = NX, nu = NU, RTX = (NX + 15) / 16, RTU = (NU + 15) / 16;
     const int n = p.n, m = p.m;
@@ -119,7 +119,8 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
     const int Tc = (n - 1 + 15) >> 4, Tl = (n - m + 15) >> 4;
     const int y1 = p.T0 - p.Y0;  // eta1 = y over the whole y segment
     const int nrow = m * (nx + nu) + y1 + m;
-    const int Tp = (nrow + 63) >> 6;
+    const int fbeg = C ? m * (nx + nu) : 0;  // eta7 rows: written by the child tiles when C > 0
+    const int Tp = (nrow - fbeg + 63) >> 6;
     WPerm<T, NX, NX> wq;  // sqrtQ for child tiles, sqrtPf for leaf tiles
     WPerm<T, NU, NU> wr;
     // per-wave LDS image of one output tile (16 nodes x (nx + 1))
@@ -132,7 +133,11 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
         auto fetch = [&](int tk, Rec& cr, T (&ax)[(NX + 3) / 4], T (&au)[(NU + 3) / 4]) {
             const int ja = 1 + 16 * tk + lo;
             const bool la = tk < Tc && ja < n;
-            cr = la ? p.crec[ja] : Rec{0, -1, -1, 0};
+            // uniform branching C (host-checked BFS): the ancestor without a dependent record
+            // load, and w = the parent's eta7 offset on its first child (-1: none / C = 0)
+            if (!la) cr = Rec{0, -1, -1, -1};
+            else if (C) cr = Rec{(ja - 1) / C, 0, 0, (ja - 1) % C == 0 ? p.e7off[(ja - 1) / C] : -1};
+            else { cr = p.crec[ja]; cr.w = -1; }
             load_arow<T, NX>(la ? z + p.X0 + (size_t)cr.x * nx : nullptr, ax);
             load_arow<T, NU>(la ? z + p.U0 + (size_t)cr.x * nu : nullptr, au);
         };
@@ -140,7 +145,8 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
         T ax[(NX + 3) / 4], au[(NU + 3) / 4];
         if (task < Tc) {
             fetch(task, cr, ax, au);
-            const int tq = __builtin_amdgcn_readfirstlane(cr.y), tr = __builtin_amdgcn_readfirstlane(cr.z);
+            const int tq = C ? p.crec[1].y : __builtin_amdgcn_readfirstlane(cr.y);
+            const int tr = C ? p.crec[1].z : __builtin_amdgcn_readfirstlane(cr.z);
             wq.load((const T*)p.SQ, tq);  // one table over the tiles (host check)
             wr.load((const T*)p.SR, tr);
         }
@@ -161,6 +167,15 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
             if (lane < 2 * cnt) {
                 const int j = j0 + (lane >> 1);
                 eg[((lane & 1) ? p.E6 : p.E5) + j] = T(0.5) * z[p.T0 + j];
+            }
+            if (cr.w >= 0) {
+                // eta7_i = [x_i; u_i] of a boxed parent, from its first child's A registers
+                // (lane (lo, h) holds entries KC h .. KC h + KC of the row)
+                constexpr int KX = (NX + 3) / 4, KU = (NU + 3) / 4;
+                _Pragma("unroll") for (int k = 0; k < KX; ++k)
+                    if (KX * h + k < nx) eg[cr.w + KX * h + k] = ax[k];
+                _Pragma("unroll") for (int k = 0; k < KU; ++k)
+                    if (KU * h + k < nu) eg[cr.w + nx + KU * h + k] = au[k];
             }
             cr = cr2;
             _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];
@@ -206,7 +221,7 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
     for (int task = ((Tc + Tl - gw + nwv - 1) / nwv) * nwv + gw; task < Tc + Tl + Tp; task += nwv) {
         {
             // 64 flat rows: eta7 (nonleaf [x; u] on boxed nodes) | eta1 = y | eta2 = s - b'y
-            const int q = 64 * (task - Tc - Tl) + lane;
+            const int q = fbeg + 64 * (task - Tc - Tl) + lane;
             const int nD = m * (nx + nu), nF = nD + y1;
             if (q < nD) {
                 const int i = q / (nx + nu), rr = q - i * (nx + nu);
@@ -224,6 +239,137 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
                 by += z[p.Y0 + yo + 2 * c];
                 eg[p.E2 + i] = z[p.S0 + i] - by;
             }
+        }
+    }
+}
+
+// L^T (operators.py:55-94) as streaming wave tasks, for trees with one sqrtQ / sqrtR table over
+// all children, one sqrtPf over all leaves and a uniform branching factor C <= 4 (BFS: the
+// children of parent i are 1 + C i .. C i + C, y_i starts at (2C + 1) i; host-checked).
+//
+// Tasks (from the task index, no table):
+//   [0, Tq)        parent tiles of PT = 4 Q parents (Q = 4 / C): A row lo is child
+//                  kA = e_of(lo) % C of parent h_of(lo) + 4 (e_of(lo) / C), so the C children
+//                  of one parent land in one lane's accumulator slots and are summed there in
+//                  the reference's order: x_i = C7' eta7_i + sum_j sqrtQ eta3_j (same for u)
+//   [Tq, + Tl)     leaf tiles of 16 leaves: x_l = sqrtPf eta11_l (+ eta14_l on boxed leaves)
+//   [.., + Tf)     flat chunks of 64 rows of [y | s | tau_1..]: y_i = eta1_i - b_i eta2_i,
+//                  s_i = eta2_i (nonleaf), s_l = (eta12_l + eta13_l) / 2, tau_j = (eta5_j + eta6_j) / 2
+template <class T, int NX, int NU>
+__global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C) {
+    typedef typename MF<T>::v4 v4;
+    constexpr int nx = NX, nu = NU, RTX = (NX + 15) / 16, RTU = (NU + 15) / 16;
+    const int n = p.n, m = p.m;
+    cglbp<T> d = (cglbp<T>)eta_;
+    glbp<T> zg = (glbp<T>)z_;
+    const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4;
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwv = gridDim.x * (blockDim.x >> 6);
+    const int Q = 4 / C, PT = 4 * Q;
+    const int Tq = (m + PT - 1) / PT, Tl = (n - m + 15) >> 4;
+    const int ny = p.T0 - p.Y0, nrow = ny + n + (n - 1);
+    const int Tf = (nrow + 63) >> 6;
+    const int hA = MF<T>::h_of(lo), eA = MF<T>::e_of(lo);
+    const int pA = hA + 4 * (eA / C), kA = eA % C;
+    const bool slotA = eA < Q * C;
+    WPerm<T, NX, NX> wq;  // sqrtQ for parent tiles, sqrtPf for leaf tiles
+    WPerm<T, NU, NU> wr;
+    {
+        int task = gw;
+        auto fetch = [&](int tk, T (&ax)[(NX + 3) / 4], T (&au)[(NU + 3) / 4]) {
+            const int q = PT * tk + pA;
+            const bool la = tk < Tq && slotA && q < m;
+            const int j = 1 + C * q + kA;
+            load_arow<T, NX>(la ? d + e3(p, j) : nullptr, ax);
+            load_arow<T, NU>(la ? d + e4(p, j) : nullptr, au);
+        };
+        T ax[(NX + 3) / 4], au[(NU + 3) / 4];
+        if (task < Tq) {
+            fetch(task, ax, au);
+            wq.load((const T*)p.SQ, p.crec[1].y);  // one table over the children (host check)
+            wr.load((const T*)p.SR, p.crec[1].z);
+        }
+        for (; task < Tq; task += nwv) {
+            T ax2[(NX + 3) / 4], au2[(NU + 3) / 4];
+            fetch(task + nwv, ax2, au2);
+            v4 cx[RTX], cu[RTU];
+            _Pragma("unroll") for (int r = 0; r < RTX; ++r) cx[r] = v4{0, 0, 0, 0};
+            _Pragma("unroll") for (int r = 0; r < RTU; ++r) cu[r] = v4{0, 0, 0, 0};
+            mma_perm<T, NX, NX>(wq, ax, cx);
+            mma_perm<T, NU, NU>(wr, au, cu);
+            const int pb = PT * task;
+            _Pragma("unroll") for (int sl = 0; sl < 4; ++sl) {
+                const int q = pb + h + 4 * sl;
+                if (sl >= Q || q >= m) continue;
+                const int o7 = p.e7off[q];
+                _Pragma("unroll") for (int rt = 0; rt < RTX; ++rt) {
+                    const int r = 16 * rt + lo;
+                    if (r >= nx) continue;
+                    T v = o7 >= 0 ? d[o7 + r] : T(0);
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                        if (e / C == sl && e < Q * C) v += cx[rt][e];
+                    zg[p.X0 + (size_t)q * nx + r] = v;
+                }
+                _Pragma("unroll") for (int rt = 0; rt < RTU; ++rt) {
+                    const int r = 16 * rt + lo;
+                    if (r >= nu) continue;
+                    T v = o7 >= 0 ? d[o7 + nx + r] : T(0);
+                    _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                        if (e / C == sl && e < Q * C) v += cu[rt][e];
+                    zg[p.U0 + (size_t)q * nu + r] = v;
+                }
+            }
+            _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];
+            _Pragma("unroll") for (int k = 0; k < (NU + 3) / 4; ++k) au[k] = au2[k];
+        }
+    }
+    {
+        const int first = ((Tq - gw + nwv - 1) / nwv) * nwv + gw;  // this wave's first task >= Tq
+        int task = first;
+        auto fetch = [&](int tk, T (&ax)[(NX + 3) / 4]) {
+            const int la_ = m + 16 * (tk - Tq) + lo;
+            const bool la = tk < Tq + Tl && la_ < n;
+            load_arow<T, NX>(la ? d + e11(p, la_) : nullptr, ax);
+        };
+        T ax[(NX + 3) / 4];
+        if (task < Tq + Tl) {
+            fetch(task, ax);
+            wq.load((const T*)p.SP, p.lrec[0].x);
+        }
+        for (; task < Tq + Tl; task += nwv) {
+            T ax2[(NX + 3) / 4];
+            fetch(task + nwv, ax2);
+            const int l0 = m + 16 * (task - Tq);
+            v4 cx[RTX];
+            _Pragma("unroll") for (int r = 0; r < RTX; ++r) cx[r] = v4{0, 0, 0, 0};
+            mma_perm<T, NX, NX>(wq, ax, cx);
+            _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                const int l = l0 + MF<T>::row(h, e);
+                if (l >= n) continue;
+                const int o14 = p.lrec[l - m].z;
+                _Pragma("unroll") for (int rt = 0; rt < RTX; ++rt) {
+                    const int r = 16 * rt + lo;
+                    if (r >= nx) continue;
+                    T v = cx[rt][e];
+                    if (o14 >= 0) v += d[o14 + r];
+                    zg[p.X0 + (size_t)l * nx + r] = v;
+                }
+            }
+            _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];
+        }
+    }
+    const int G = 2 * C + 1;
+    for (int task = ((Tq + Tl - gw + nwv - 1) / nwv) * nwv + gw; task < Tq + Tl + Tf; task += nwv) {
+        const int q = 64 * (task - Tq - Tl) + lane;
+        if (q < ny) {
+            const int i = q / G, k = q - i * G;
+            const T b = k < C ? ((cglbp<T>)p.cond)[1 + C * i + k] : (k < 2 * C ? T(0) : T(1));
+            zg[p.Y0 + q] = d[p.E1 + q] - b * d[p.E2 + i];
+        } else if (q < ny + n) {
+            const int i = q - ny;
+            zg[p.S0 + i] = i < m ? d[p.E2 + i] : T(0.5) * (d[p.E12 + i] + d[p.E13 + i]);
+        } else if (q < nrow) {
+            const int j = q - ny - n + 1;
+            zg[p.T0 + j] = T(0.5) * (d[p.E5 + j] + d[p.E6 + j]);
         }
     }
 }

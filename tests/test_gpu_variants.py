@@ -4,7 +4,8 @@ the eager stopping test after every iteration (RAOCP_DEFER_CHECK=0) against the 
 deferred one; the staging switches (RAOCP_CP_PACK=1: the staged regions of k_cpd / k_cpp
 packed into shared LDS-DMA instructions; RAOCP_DYN_ROT=0: every staged range of the dynamics kernels starts at
 wave 0), which must not change a bit; and the default per-parent L^T tiles against the
-LDS-staged path (RAOCP_ELLT_PARENT_TILES=0).
+LDS-staged path (RAOCP_ELLT_PARENT_TILES=0); the streaming L^T (k_ellt3, default on
+uniform trees) against the block kernel (RAOCP_ELLT3=0) and the oracle.
 
 Tolerances as in test_gpu_parity.py.
 """
@@ -117,10 +118,45 @@ def test_ell_t_parent_tiles_bit_identical_to_staged(cfg):
     if cfg == "4-modes":
         r["Q"] = np.array([(1.0 + k) * q for k, q in enumerate(r["Q"])])
     tree, prob = build_problem(r)
-    tiles = core.Cache(prob)
-    staged = _with_env({"RAOCP_ELLT_PARENT_TILES": "0"}, lambda: core.Cache(prob))
+    tiles = _with_env({"RAOCP_ELLT3": "0"}, lambda: core.Cache(prob))
+    staged = _with_env({"RAOCP_ELLT3": "0", "RAOCP_ELLT_PARENT_TILES": "0"}, lambda: core.Cache(prob))
     rng = np.random.default_rng(11)
     ee = rng.standard_normal(tiles.dual_size)
     a, b = tiles.native.ell_t(ee), staged.native.ell_t(ee)
     assert np.array_equal(a, b)
     assert rel_err(a, OracleProblem(prob).ell_t(ee)) <= 1e-12
+
+
+@pytest.mark.parametrize("cfg", ["chain", 2, "2-nobox", 4, "4-c2"])
+def test_ell_t_streaming_vs_block_and_oracle(cfg):
+    """k_ellt3 (streaming wave tasks, uniform tables and branching C <= 4; raocp_ell3.hip)
+    against k_ell_t (RAOCP_ELLT3=0) and the oracle (operators.py:55-94) on random duals:
+    a chain (C = 1), config 2 (C = 2) with and without boxes (eta7 / eta14 terms), config 4
+    (C = 3, nx = 32) and a binary tree at nx = 32."""
+    from oracle.raocp_oracle import OracleProblem
+    from raocp.problems import recipe_synthetic
+    if cfg == "chain":
+        r = recipe_synthetic(np.ones((1, 1)), np.ones(1), 40, 40, 20, 8, seed=3)
+    elif cfg == "4-c2":
+        r = recipe_synthetic(np.full((2, 2), .5), np.full(2, .5), 9, 9, 32, 12, seed=4)
+    else:
+        r = recipe_config(2 if cfg == "2-nobox" else cfg)
+    if cfg == "2-nobox":
+        r["nl_min"] = r["nl_max"] = r["l_min"] = r["l_max"] = None
+    tree, prob = build_problem(r)
+    stream = core.Cache(prob)
+    block = _with_env({"RAOCP_ELLT3": "0"}, lambda: core.Cache(prob))
+    rng = np.random.default_rng(12)
+    ee = rng.standard_normal(stream.dual_size)
+    a, b = stream.native.ell_t(ee), block.native.ell_t(ee)
+    ref = OracleProblem(prob).ell_t(ee)
+    assert rel_err(a, ref) <= 1e-12 and rel_err(a, b) <= 1e-12
+    # tau_0 is never written (operators.py:55-94 writes tau_j for children only)
+    tmpl = rng.standard_normal(stream.primal_size)
+    a2 = stream.native.ell_t(ee, template=tmpl)
+    pk = stream.packed
+    t0 = pk.n * pk.nx + pk.m * pk.nu + int(np.sum(2 * pk.nch[:pk.m] + 1))  # flat index of tau_0
+    assert a2[t0] == tmpl[t0]
+    keep = np.ones(a2.size, bool)
+    keep[t0] = False
+    assert np.array_equal(a2[keep], a[keep])
