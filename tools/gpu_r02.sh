@@ -10,4 +10,4 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
 done
 echo pmc_done
 timeout -k 10 120 python3 tools/stamps.py 2 > gpurun_out/stamps_c2.log 2>&1 || exit 1
-timeout -k 10 120 ./build/asan_abi gpu > gpurun_out/asan_gpu.log 2>&1; echo "asan gpu rc=$?"; tail -2 gpurun_out/asan_gpu.log
+LSAN_OPTIONS=suppressions=tests/asan/lsan.supp timeout -k 10 120 ./build/asan_abi gpu > gpurun_out/asan_gpu.log 2>&1; echo "asan gpu rc=$?"; tail -2 gpurun_out/asan_gpu.log
