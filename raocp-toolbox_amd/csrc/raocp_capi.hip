@@ -51,6 +51,7 @@ struct raocp_ctx {
     bool dyn32 = false;          // the per-stage T-templated dynamics (raocp_dyn2.hip) is planned
     bool ell3 = false;           // L by streaming wave tasks (raocp_ell3.hip)
     int ell3_grid = 0;
+    int box_mode = 0;            // k_ell3 / k_ellt3: bits 0-1 nonleaf, 2-3 leaf boxes (1 all, 2 none, 0 mixed)
     int unif_C = 0;              // uniform branching factor <= 4 with uniform tables (0 = not)
     int ellt3_C = 0;             // L^T by streaming wave tasks: uniform branching factor (0 = off)
     int ellt3_grid = 0;
@@ -316,9 +317,9 @@ struct Ell2Op {
 template <class T>
 bool launch_ell3(raocp_ctx* c, const double* z, double* eta) {
     const int g = c->ell3_grid;
-    if (c->nx == 20 && c->nu == 8) raocp::k_ell3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C);
-    else if (c->nx == 32 && c->nu == 12) raocp::k_ell3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C);
-    else if (c->nx == 64 && c->nu == 16) raocp::k_ell3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C);
+    if (c->nx == 20 && c->nu == 8) raocp::k_ell3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C, c->box_mode);
+    else if (c->nx == 32 && c->nu == 12) raocp::k_ell3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C, c->box_mode);
+    else if (c->nx == 64 && c->nu == 16) raocp::k_ell3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, z, eta, c->unif_C, c->box_mode);
     else return false;
     return true;
 }
@@ -340,9 +341,9 @@ struct EllTOp {
 template <class T>
 bool launch_ellt3(raocp_ctx* c, const double* eta, double* z) {
     const int g = c->ellt3_grid, C = c->ellt3_C;
-    if (c->nx == 20 && c->nu == 8) raocp::k_ellt3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C);
-    else if (c->nx == 32 && c->nu == 12) raocp::k_ellt3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C);
-    else if (c->nx == 64 && c->nu == 16) raocp::k_ellt3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C);
+    if (c->nx == 20 && c->nu == 8) raocp::k_ellt3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
+    else if (c->nx == 32 && c->nu == 12) raocp::k_ellt3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
+    else if (c->nx == 64 && c->nu == 16) raocp::k_ellt3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
     else return false;
     return true;
 }
@@ -1876,7 +1877,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         c->ell3 = uni;
         if (const char* e = getenv("RAOCP_ELL3")) c->ell3 = uni && atoi(e) != 0;
         const long tasks = (long)(n - 1 + 15) / 16 + (n - m + 15) / 16 + ((long)m * (nx + nu) + (c->dev.T0 - c->dev.Y0) + m + 63) / 64;
-        c->ell3_grid = (int)std::max(1L, std::min((tasks + 3) / 4, 4096L));
+        // grid sweep (profiles/r02_v2/ab_order.log): config 4 fp64 best at 2,048 blocks (25.3 us
+        // vs 26.7 at 4,096), config 5 fp32 at 1,024 (116 vs 137 us at 4,096)
+        c->ell3_grid = (int)std::max(1L, std::min((tasks + 3) / 4, c->f32 ? 1024L : 2048L));
         if (const char* e = getenv("RAOCP_ELL3_GRID")) c->ell3_grid = std::max(1, atoi(e));
         // L^T by streaming wave tasks: additionally one branching factor C <= 4 over all
         // nonleaf nodes (children 1 + C i .., y_i at (2C + 1) i); RAOCP_ELLT3=0 keeps k_ell_t
@@ -1885,14 +1888,20 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         for (int i = 0; i < m && reg; ++i)
             if (t->nch[i] != C || t->ch_start[i] != 1 + C * i) reg = false;
         c->unif_C = reg ? C : 0;
+        {
+            int nb = 0, lb = 0;
+            for (int i = 0; i < m; ++i) nb += pr->i_box_nl[i] >= 0;
+            for (int l = m; l < n; ++l) lb += pr->i_box_l[l] >= 0;
+            c->box_mode = (nb == m ? 1 : nb == 0 ? 2 : 0) | ((lb == n - m ? 1 : lb == 0 ? 2 : 0) << 2);
+            if (const char* e = getenv("RAOCP_BOX_MODE")) c->box_mode = atoi(e);  // 0: always the tables
+        }
         if (const char* e = getenv("RAOCP_ELLT3")) reg = reg && atoi(e) != 0;
         c->ellt3_C = reg ? C : 0;
         const long tasks_t = (long)(m + 4 * (4 / std::max(C, 1)) - 1) / (4 * (4 / std::max(C, 1))) + (n - m + 15) / 16 +
                              ((long)(c->dev.T0 - c->dev.Y0) + 2L * n - 1 + 63) / 64;
-        // grid sweep (profiles/r02_v2/ab_ellt3.log): fp64 config 4 best at 4,096 blocks
-        // (27.8 us vs 31.9 at 1,024), fp32 config 5 at 1,024 (163 vs 184 us at 4,096: each
-        // wave loads a 16-KB sqrtQ fragment, so fewer waves with more tiles each win there)
-        c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, c->f32 ? 1024L : 4096L));
+        // grid sweep (profiles/r02_v2/ab_order.log): 1,024 blocks best at config 4 fp64
+        // (28.7 us vs 32.3 at 4,096) and config 5 fp32 (116 vs 136 us)
+        c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, 1024L));
         if (const char* e = getenv("RAOCP_ELLT3_GRID")) c->ellt3_grid = std::max(1, atoi(e));
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels

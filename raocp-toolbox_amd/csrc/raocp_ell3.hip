@@ -107,8 +107,24 @@ __device__ __forceinline__ void store_tile(__attribute__((address_space(3))) T* 
     __builtin_amdgcn_wave_barrier();
 }
 
+// eta7 / eta14 offsets of a node. bx (host-built): bits 0-1 nonleaf boxes, bits 2-3 leaf
+// boxes; 1 = every node boxed (offsets computed, no record load), 2 = none, 0 = mixed (table)
+template <int NX, int NU>
+__device__ __forceinline__ int o7_of(const Dev& p, int i, int bx) {
+    const int md = bx & 3;
+    return md == 1 ? p.E7 + i * (NX + NU) : md == 2 ? -1 : p.e7off[i];
+}
+template <int NX>
+__device__ __forceinline__ int o14_of(const Dev& p, int l, int bx) {
+    const int md = (bx >> 2) & 3;
+    return md == 1 ? p.E14 + p.m + (l - p.m) * NX : md == 2 ? -1 : p.lrec[l - p.m].z;
+}
+
+// Loop order of the streaming kernels: a tile's epilogue operands are loaded first, then the
+// wave's next tile, then the MFMAs and stores: vmcnt is in order, so an operand loaded after
+// the prefetch would make the epilogue wait for the prefetched tile too.
 template <class T, int NX, int NU>
-__global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ z_, double* __restrict__ eta_, int C) {
+__global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ z_, double* __restrict__ eta_, int C, int bx) {
     typedef typename MF<T>::v4 v4;
     constexpr int nx = NX, nu = NU, RTX = (NX + 15) / 16, RTU = (NU + 15) / 16;
     const int n = p.n, m = p.m;
@@ -136,7 +152,7 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
             // uniform branching C (host-checked BFS): the ancestor without a dependent record
             // load, and w = the parent's eta7 offset on its first child (-1: none / C = 0)
             if (!la) cr = Rec{0, -1, -1, -1};
-            else if (C) cr = Rec{(ja - 1) / C, 0, 0, (ja - 1) % C == 0 ? p.e7off[(ja - 1) / C] : -1};
+            else if (C) cr = Rec{(ja - 1) / C, 0, 0, (ja - 1) % C == 0 ? o7_of<NX, NU>(p, (ja - 1) / C, bx) : -1};
             else { cr = p.crec[ja]; cr.w = -1; }
             load_arow<T, NX>(la ? z + p.X0 + (size_t)cr.x * nx : nullptr, ax);
             load_arow<T, NU>(la ? z + p.U0 + (size_t)cr.x * nu : nullptr, au);
@@ -151,22 +167,23 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
             wr.load((const T*)p.SR, tr);
         }
         for (; task < Tc; task += nwv) {
+            const int j0 = 1 + 16 * task;
+            const int cnt = min(16, n - j0);
+            const T tv = lane < 2 * cnt ? z[p.T0 + j0 + (lane >> 1)] : T(0);
             Rec cr2;
             T ax2[(NX + 3) / 4], au2[(NU + 3) / 4];
             fetch(task + nwv, cr2, ax2, au2);
-            const int j0 = 1 + 16 * task;
             v4 cx[RTX], cu[RTU];
             _Pragma("unroll") for (int r = 0; r < RTX; ++r) cx[r] = v4{0, 0, 0, 0};
             _Pragma("unroll") for (int r = 0; r < RTU; ++r) cu[r] = v4{0, 0, 0, 0};
             mma_perm<T, NX, NX>(wq, ax, cx);
             mma_perm<T, NU, NU>(wr, au, cu);
-            const int cnt = min(16, n - j0);
             // eta3 / eta4 of consecutive children are contiguous blocks
             store_tile<T, NX>(img, cx, cnt, eg + e3(p, j0));
             store_tile<T, NU>(img, cu, cnt, eg + e4(p, j0));
             if (lane < 2 * cnt) {
                 const int j = j0 + (lane >> 1);
-                eg[((lane & 1) ? p.E6 : p.E5) + j] = T(0.5) * z[p.T0 + j];
+                eg[((lane & 1) ? p.E6 : p.E5) + j] = T(0.5) * tv;
             }
             if (cr.w >= 0) {
                 // eta7_i = [x_i; u_i] of a boxed parent, from its first child's A registers
@@ -186,35 +203,39 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
     {
         const int first = ((Tc - gw + nwv - 1) / nwv) * nwv + gw;  // this wave's first task >= Tc
         int task = first;
-        auto fetch = [&](int tk, T (&ax)[(NX + 3) / 4]) {
+        // o14: eta14 offset of leaf lo of the tile (-1: unboxed / no leaf)
+        auto fetch = [&](int tk, int& o14, T (&ax)[(NX + 3) / 4]) {
             const int la_ = m + 16 * (tk - Tc) + lo;
             const bool la = tk < Tc + Tl && la_ < n;
+            o14 = la ? o14_of<NX>(p, la_, bx) : -1;
             load_arow<T, NX>(la ? z + p.X0 + (size_t)la_ * nx : nullptr, ax);
         };
+        int o14;
         T ax[(NX + 3) / 4];
         if (task < Tc + Tl) {
-            fetch(task, ax);
+            fetch(task, o14, ax);
             wq.load((const T*)p.SP, p.lrec[m + 16 * (task - Tc) - m].x);
         }
         for (; task < Tc + Tl; task += nwv) {
-            T ax2[(NX + 3) / 4];
-            fetch(task + nwv, ax2);
             const int l0 = m + 16 * (task - Tc);
+            const int cnt = min(16, n - l0);
+            const T sv = lane < 2 * cnt ? z[p.S0 + l0 + (lane >> 1)] : T(0);
+            int o14b;
+            T ax2[(NX + 3) / 4];
+            fetch(task + nwv, o14b, ax2);
             v4 cx[RTX];
             _Pragma("unroll") for (int r = 0; r < RTX; ++r) cx[r] = v4{0, 0, 0, 0};
             mma_perm<T, NX, NX>(wq, ax, cx);
-            const int cnt = min(16, n - l0);
             store_tile<T, NX>(img, cx, cnt, eg + e11(p, l0));
-            // eta14 = x (boxed leaves; a leaf's eta14 block is its x row), eta12 = eta13 = s / 2
-            for (int q = lane; q < cnt * nx; q += 64) {
-                const int a = q / nx, r = q - a * nx;
-                const int o14 = p.lrec[l0 + a - m].z;
-                if (o14 >= 0) eg[o14 + r] = z[p.X0 + (size_t)l0 * nx + q];
+            // eta14 = x (boxed leaves; a leaf's eta14 block is its x row), from the A registers
+            if (o14 >= 0) {
+                constexpr int KX = (NX + 3) / 4;
+                _Pragma("unroll") for (int k = 0; k < KX; ++k)
+                    if (KX * h + k < nx) eg[o14 + KX * h + k] = ax[k];
             }
-            if (lane < 2 * cnt) {
-                const int l = l0 + (lane >> 1);
-                eg[((lane & 1) ? p.E13 : p.E12) + l] = T(0.5) * z[p.S0 + l];
-            }
+            // eta12 = eta13 = s / 2
+            if (lane < 2 * cnt) eg[((lane & 1) ? p.E13 : p.E12) + l0 + (lane >> 1)] = T(0.5) * sv;
+            o14 = o14b;
             _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];
         }
     }
@@ -225,7 +246,7 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
             const int nD = m * (nx + nu), nF = nD + y1;
             if (q < nD) {
                 const int i = q / (nx + nu), rr = q - i * (nx + nu);
-                const int o7 = p.e7off[i];
+                const int o7 = o7_of<NX, NU>(p, i, bx);
                 if (o7 >= 0) eg[o7 + rr] = rr < nx ? z[p.X0 + (size_t)i * nx + rr] : z[p.U0 + (size_t)i * nu + rr - nx];
             } else if (q < nF) {
                 const int e = q - nD;
@@ -256,7 +277,7 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
 //   [.., + Tf)     flat chunks of 64 rows of [y | s | tau_1..]: y_i = eta1_i - b_i eta2_i,
 //                  s_i = eta2_i (nonleaf), s_l = (eta12_l + eta13_l) / 2, tau_j = (eta5_j + eta6_j) / 2
 template <class T, int NX, int NU>
-__global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C) {
+__global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C, int bx) {
     typedef typename MF<T>::v4 v4;
     constexpr int nx = NX, nu = NU, RTX = (NX + 15) / 16, RTU = (NU + 15) / 16;
     const int n = p.n, m = p.m;
@@ -289,6 +310,17 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
             wr.load((const T*)p.SR, p.crec[1].z);
         }
         for (; task < Tq; task += nwv) {
+            const int pb = PT * task;
+            // C7' eta7 of this tile's parents (lane: parent h + 4 sl, rows 16 rt + lo)
+            T e7x[4][RTX], e7u[4][RTU];
+            _Pragma("unroll") for (int sl = 0; sl < 4; ++sl) {
+                const int q = pb + h + 4 * sl;
+                const int o7 = sl < Q && q < m ? o7_of<NX, NU>(p, q, bx) : -1;
+                _Pragma("unroll") for (int rt = 0; rt < RTX; ++rt)
+                    e7x[sl][rt] = o7 >= 0 && 16 * rt + lo < nx ? d[o7 + 16 * rt + lo] : T(0);
+                _Pragma("unroll") for (int rt = 0; rt < RTU; ++rt)
+                    e7u[sl][rt] = o7 >= 0 && 16 * rt + lo < nu ? d[o7 + nx + 16 * rt + lo] : T(0);
+            }
             T ax2[(NX + 3) / 4], au2[(NU + 3) / 4];
             fetch(task + nwv, ax2, au2);
             v4 cx[RTX], cu[RTU];
@@ -296,15 +328,13 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
             _Pragma("unroll") for (int r = 0; r < RTU; ++r) cu[r] = v4{0, 0, 0, 0};
             mma_perm<T, NX, NX>(wq, ax, cx);
             mma_perm<T, NU, NU>(wr, au, cu);
-            const int pb = PT * task;
             _Pragma("unroll") for (int sl = 0; sl < 4; ++sl) {
                 const int q = pb + h + 4 * sl;
                 if (sl >= Q || q >= m) continue;
-                const int o7 = p.e7off[q];
                 _Pragma("unroll") for (int rt = 0; rt < RTX; ++rt) {
                     const int r = 16 * rt + lo;
                     if (r >= nx) continue;
-                    T v = o7 >= 0 ? d[o7 + r] : T(0);
+                    T v = e7x[sl][rt];  // the reference starts from C7' eta7 or 0 (operators.py:73-78)
                     _Pragma("unroll") for (int e = 0; e < 4; ++e)
                         if (e / C == sl && e < Q * C) v += cx[rt][e];
                     zg[p.X0 + (size_t)q * nx + r] = v;
@@ -312,7 +342,7 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
                 _Pragma("unroll") for (int rt = 0; rt < RTU; ++rt) {
                     const int r = 16 * rt + lo;
                     if (r >= nu) continue;
-                    T v = o7 >= 0 ? d[o7 + nx + r] : T(0);
+                    T v = e7u[sl][rt];
                     _Pragma("unroll") for (int e = 0; e < 4; ++e)
                         if (e / C == sl && e < Q * C) v += cu[rt][e];
                     zg[p.U0 + (size_t)q * nu + r] = v;
@@ -336,21 +366,30 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
             wq.load((const T*)p.SP, p.lrec[0].x);
         }
         for (; task < Tq + Tl; task += nwv) {
+            const int l0 = m + 16 * (task - Tq);
+            // C14' eta14 of this tile's leaves (lane: leaf row(h, e), rows 16 rt + lo)
+            T e14[4][RTX];
+            bool b14[4];
+            _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                const int l = l0 + MF<T>::row(h, e);
+                const int o14 = l < n ? o14_of<NX>(p, l, bx) : -1;
+                b14[e] = o14 >= 0;
+                _Pragma("unroll") for (int rt = 0; rt < RTX; ++rt)
+                    e14[e][rt] = o14 >= 0 && 16 * rt + lo < nx ? d[o14 + 16 * rt + lo] : T(0);
+            }
             T ax2[(NX + 3) / 4];
             fetch(task + nwv, ax2);
-            const int l0 = m + 16 * (task - Tq);
             v4 cx[RTX];
             _Pragma("unroll") for (int r = 0; r < RTX; ++r) cx[r] = v4{0, 0, 0, 0};
             mma_perm<T, NX, NX>(wq, ax, cx);
             _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 const int l = l0 + MF<T>::row(h, e);
                 if (l >= n) continue;
-                const int o14 = p.lrec[l - m].z;
                 _Pragma("unroll") for (int rt = 0; rt < RTX; ++rt) {
                     const int r = 16 * rt + lo;
                     if (r >= nx) continue;
                     T v = cx[rt][e];
-                    if (o14 >= 0) v += d[o14 + r];
+                    if (b14[e]) v += e14[e][rt];
                     zg[p.X0 + (size_t)l * nx + r] = v;
                 }
             }

@@ -127,22 +127,27 @@ def test_ell_t_parent_tiles_bit_identical_to_staged(cfg):
     assert rel_err(a, OracleProblem(prob).ell_t(ee)) <= 1e-12
 
 
-@pytest.mark.parametrize("cfg", ["chain", 2, "2-nobox", 4, "4-c2"])
+@pytest.mark.parametrize("cfg", ["chain", 2, "2-nobox", "2-leafbox", 4, "4-c2"])
 def test_ell_t_streaming_vs_block_and_oracle(cfg):
     """k_ellt3 (streaming wave tasks, uniform tables and branching C <= 4; raocp_ell3.hip)
     against k_ell_t (RAOCP_ELLT3=0) and the oracle (operators.py:55-94) on random duals:
-    a chain (C = 1), config 2 (C = 2) with and without boxes (eta7 / eta14 terms), config 4
-    (C = 3, nx = 32) and a binary tree at nx = 32."""
+    a chain (C = 1), config 2 (C = 2) with all, no and leaf-only boxes (eta7 / eta14 terms),
+    config 4 (C = 3, nx = 32) and a binary tree at nx = 32. The same for L (k_ell3 against
+    k_ell, operators.py:19-53), and both with the eta7 / eta14 offsets read from the tables
+    (RAOCP_BOX_MODE=0) instead of computed from the all / none box patterns."""
     from oracle.raocp_oracle import OracleProblem
     from raocp.problems import recipe_synthetic
     if cfg == "chain":
         r = recipe_synthetic(np.ones((1, 1)), np.ones(1), 40, 40, 20, 8, seed=3)
     elif cfg == "4-c2":
         r = recipe_synthetic(np.full((2, 2), .5), np.full(2, .5), 9, 9, 32, 12, seed=4)
+    elif cfg in ("2-nobox", "2-leafbox"):
+        r = recipe_config(2)
+        r["nl_min"] = r["nl_max"] = None
+        if cfg == "2-nobox":
+            r["l_min"] = r["l_max"] = None
     else:
-        r = recipe_config(2 if cfg == "2-nobox" else cfg)
-    if cfg == "2-nobox":
-        r["nl_min"] = r["nl_max"] = r["l_min"] = r["l_max"] = None
+        r = recipe_config(cfg)
     tree, prob = build_problem(r)
     stream = core.Cache(prob)
     block = _with_env({"RAOCP_ELLT3": "0"}, lambda: core.Cache(prob))
@@ -160,3 +165,11 @@ def test_ell_t_streaming_vs_block_and_oracle(cfg):
     keep = np.ones(a2.size, bool)
     keep[t0] = False
     assert np.array_equal(a2[keep], a[keep])
+    tabs = _with_env({"RAOCP_BOX_MODE": "0"}, lambda: core.Cache(prob))
+    assert np.array_equal(tabs.native.ell_t(ee), a)
+    zz = rng.standard_normal(stream.primal_size)
+    lz = stream.native.ell(zz)
+    assert rel_err(lz, OracleProblem(prob).ell(zz)) <= 1e-12
+    assert np.array_equal(tabs.native.ell(zz), lz)
+    blk = _with_env({"RAOCP_ELL3": "0"}, lambda: core.Cache(prob))
+    assert rel_err(blk.native.ell(zz), lz) <= 1e-12
