@@ -338,14 +338,21 @@ struct EllTOp {
     }
 };
 // L^T as streaming wave tasks (raocp_ell3.hip): uniform tables and branching
-template <class T>
-bool launch_ellt3(raocp_ctx* c, const double* eta, double* z) {
+template <class T, int QM>
+bool launch_ellt3q(raocp_ctx* c, const double* eta, double* z) {
     const int g = c->ellt3_grid, C = c->ellt3_C;
-    if (c->nx == 20 && c->nu == 8) raocp::k_ellt3<T, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
-    else if (c->nx == 32 && c->nu == 12) raocp::k_ellt3<T, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
-    else if (c->nx == 64 && c->nu == 16) raocp::k_ellt3<T, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
+    if (c->nx == 20 && c->nu == 8) raocp::k_ellt3<T, 20, 8, QM><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
+    else if (c->nx == 32 && c->nu == 12) raocp::k_ellt3<T, 32, 12, QM><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
+    else if (c->nx == 64 && c->nu == 16) raocp::k_ellt3<T, 64, 16, QM><<<g, 256, 0, c->stream>>>(c->dev, eta, z, C, c->box_mode);
     else return false;
     return true;
+}
+template <class T>
+bool launch_ellt3(raocp_ctx* c, const double* eta, double* z) {
+    const int C = c->ellt3_C;
+    if (C == 1) return launch_ellt3q<T, 4>(c, eta, z);
+    if (C == 2) return launch_ellt3q<T, 2>(c, eta, z);
+    return launch_ellt3q<T, 1>(c, eta, z);
 }
 void launch_ell_t(raocp_ctx* c, const double* eta, double* z) {
     if (c->ellt3_C && (c->f32 ? launch_ellt3<float>(c, eta, z) : launch_ellt3<double>(c, eta, z))) return;
@@ -1899,9 +1906,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         c->ellt3_C = reg ? C : 0;
         const long tasks_t = (long)(m + 4 * (4 / std::max(C, 1)) - 1) / (4 * (4 / std::max(C, 1))) + (n - m + 15) / 16 +
                              ((long)(c->dev.T0 - c->dev.Y0) + 2L * n - 1 + 63) / 64;
-        // grid sweep (profiles/r02_v2/ab_order.log): 1,024 blocks best at config 4 fp64
-        // (28.7 us vs 32.3 at 4,096) and config 5 fp32 (116 vs 136 us)
-        c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, 1024L));
+        // grid sweep (profiles/r02_v3/ab_q.log): config 4 fp64 best at 4,096 blocks (25.5 us
+        // vs 26.2 at 2,048), config 5 fp32 at 2,048 (115 vs 121 us at 4,096, 141 at 1,024)
+        c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, c->f32 ? 2048L : 4096L));
         if (const char* e = getenv("RAOCP_ELLT3_GRID")) c->ellt3_grid = std::max(1, atoi(e));
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels

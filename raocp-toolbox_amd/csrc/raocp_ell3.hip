@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
 //   [Tq, + Tl)     leaf tiles of 16 leaves: x_l = sqrtPf eta11_l (+ eta14_l on boxed leaves)
 //   [.., + Tf)     flat chunks of 64 rows of [y | s | tau_1..]: y_i = eta1_i - b_i eta2_i,
 //                  s_i = eta2_i (nonleaf), s_l = (eta12_l + eta13_l) / 2, tau_j = (eta5_j + eta6_j) / 2
-template <class T, int NX, int NU>
+template <class T, int NX, int NU, int QM>  // QM = 4 / C parents per lane (compile time: register arrays)
 __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C, int bx) {
     typedef typename MF<T>::v4 v4;
     constexpr int nx = NX, nu = NU, RTX = (NX + 15) / 16, RTU = (NU + 15) / 16;
@@ -285,7 +285,8 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
     glbp<T> zg = (glbp<T>)z_;
     const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4;
     const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwv = gridDim.x * (blockDim.x >> 6);
-    const int Q = 4 / C, PT = 4 * Q;
+    constexpr int Q = QM;
+    const int PT = 4 * Q;
     const int Tq = (m + PT - 1) / PT, Tl = (n - m + 15) >> 4;
     const int ny = p.T0 - p.Y0, nrow = ny + n + (n - 1);
     const int Tf = (nrow + 63) >> 6;
@@ -312,10 +313,10 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
         for (; task < Tq; task += nwv) {
             const int pb = PT * task;
             // C7' eta7 of this tile's parents (lane: parent h + 4 sl, rows 16 rt + lo)
-            T e7x[4][RTX], e7u[4][RTU];
-            _Pragma("unroll") for (int sl = 0; sl < 4; ++sl) {
+            T e7x[Q][RTX], e7u[Q][RTU];
+            _Pragma("unroll") for (int sl = 0; sl < Q; ++sl) {
                 const int q = pb + h + 4 * sl;
-                const int o7 = sl < Q && q < m ? o7_of<NX, NU>(p, q, bx) : -1;
+                const int o7 = q < m ? o7_of<NX, NU>(p, q, bx) : -1;
                 _Pragma("unroll") for (int rt = 0; rt < RTX; ++rt)
                     e7x[sl][rt] = o7 >= 0 && 16 * rt + lo < nx ? d[o7 + 16 * rt + lo] : T(0);
                 _Pragma("unroll") for (int rt = 0; rt < RTU; ++rt)
@@ -328,9 +329,9 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
             _Pragma("unroll") for (int r = 0; r < RTU; ++r) cu[r] = v4{0, 0, 0, 0};
             mma_perm<T, NX, NX>(wq, ax, cx);
             mma_perm<T, NU, NU>(wr, au, cu);
-            _Pragma("unroll") for (int sl = 0; sl < 4; ++sl) {
+            _Pragma("unroll") for (int sl = 0; sl < Q; ++sl) {
                 const int q = pb + h + 4 * sl;
-                if (sl >= Q || q >= m) continue;
+                if (q >= m) continue;
                 _Pragma("unroll") for (int rt = 0; rt < RTX; ++rt) {
                     const int r = 16 * rt + lo;
                     if (r >= nx) continue;
