@@ -107,6 +107,11 @@ __device__ __forceinline__ void store_tile(__attribute__((address_space(3))) T* 
     __builtin_amdgcn_wave_barrier();
 }
 
+// rows per flat task: L^T 256 (4 per lane, branch-free loads: config 5 L^T 115 -> 111 us),
+// L 64 (its eta2 rows walk the children; 256 measured slower: config 5 L 116 -> 135 us,
+// profiles/r02_v3/ab_flat.log)
+constexpr int kFlatRows = 256, kFlatRowsL = 64;
+
 // eta7 / eta14 offsets of a node. bx (host-built): bits 0-1 nonleaf boxes, bits 2-3 leaf
 // boxes; 1 = every node boxed (offsets computed, no record load), 2 = none, 0 = mixed (table)
 template <int NX, int NU>
@@ -136,7 +141,7 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
     const int y1 = p.T0 - p.Y0;  // eta1 = y over the whole y segment
     const int nrow = m * (nx + nu) + y1 + m;
     const int fbeg = C ? m * (nx + nu) : 0;  // eta7 rows: written by the child tiles when C > 0
-    const int Tp = (nrow - fbeg + 63) >> 6;
+    const int Tp = (nrow - fbeg + kFlatRowsL - 1) / kFlatRowsL;
     WPerm<T, NX, NX> wq;  // sqrtQ for child tiles, sqrtPf for leaf tiles
     WPerm<T, NU, NU> wr;
     // per-wave LDS image of one output tile (16 nodes x (nx + 1))
@@ -240,17 +245,21 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
         }
     }
     for (int task = ((Tc + Tl - gw + nwv - 1) / nwv) * nwv + gw; task < Tc + Tl + Tp; task += nwv) {
-        {
-            // 64 flat rows: eta7 (nonleaf [x; u] on boxed nodes) | eta1 = y | eta2 = s - b'y
-            const int q = fbeg + 64 * (task - Tc - Tl) + lane;
-            const int nD = m * (nx + nu), nF = nD + y1;
-            if (q < nD) {
+        // kFlatRowsL flat rows: eta7 (nonleaf [x; u] on boxed nodes) | eta1 = y | eta2 = s - b'y
+        const int nD = m * (nx + nu), nF = nD + y1;
+        T a1[kFlatRowsL / 64];
+        _Pragma("unroll") for (int k = 0; k < kFlatRowsL / 64; ++k) {
+            const int q = fbeg + kFlatRowsL * (task - Tc - Tl) + 64 * k + lane;
+            a1[k] = z[p.Y0 + (q >= nD && q < nF ? q - nD : 0)];
+        }
+        _Pragma("unroll") for (int k = 0; k < kFlatRowsL / 64; ++k) {
+            const int q = fbeg + kFlatRowsL * (task - Tc - Tl) + 64 * k + lane;
+            if (q >= nD && q < nF) {
+                eg[p.E1 + q - nD] = a1[k];
+            } else if (q < nD) {
                 const int i = q / (nx + nu), rr = q - i * (nx + nu);
                 const int o7 = o7_of<NX, NU>(p, i, bx);
                 if (o7 >= 0) eg[o7 + rr] = rr < nx ? z[p.X0 + (size_t)i * nx + rr] : z[p.U0 + (size_t)i * nu + rr - nx];
-            } else if (q < nF) {
-                const int e = q - nD;
-                eg[p.E1 + e] = z[p.Y0 + e];
             } else if (q < nrow) {
                 const int i = q - nF;
                 const int c = p.nch[i], yo = p.yrel[i], cs = p.ch_start[i];
@@ -289,7 +298,7 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
     const int PT = 4 * Q;
     const int Tq = (m + PT - 1) / PT, Tl = (n - m + 15) >> 4;
     const int ny = p.T0 - p.Y0, nrow = ny + n + (n - 1);
-    const int Tf = (nrow + 63) >> 6;
+    const int Tf = (nrow + kFlatRows - 1) / kFlatRows;
     const int hA = MF<T>::h_of(lo), eA = MF<T>::e_of(lo);
     const int pA = hA + 4 * (eA / C), kA = eA % C;
     const bool slotA = eA < Q * C;
@@ -398,18 +407,41 @@ __global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__
         }
     }
     const int G = 2 * C + 1;
+    // kFlatRows flat rows per task, branch-free loads (every lane loads from valid indices,
+    // the row kind selects the formula afterwards) so all rows of a lane are in flight at once
     for (int task = ((Tq + Tl - gw + nwv - 1) / nwv) * nwv + gw; task < Tq + Tl + Tf; task += nwv) {
-        const int q = 64 * (task - Tq - Tl) + lane;
-        if (q < ny) {
-            const int i = q / G, k = q - i * G;
-            const T b = k < C ? ((cglbp<T>)p.cond)[1 + C * i + k] : (k < 2 * C ? T(0) : T(1));
-            zg[p.Y0 + q] = d[p.E1 + q] - b * d[p.E2 + i];
-        } else if (q < ny + n) {
-            const int i = q - ny;
-            zg[p.S0 + i] = i < m ? d[p.E2 + i] : T(0.5) * (d[p.E12 + i] + d[p.E13 + i]);
-        } else if (q < nrow) {
-            const int j = q - ny - n + 1;
-            zg[p.T0 + j] = T(0.5) * (d[p.E5 + j] + d[p.E6 + j]);
+        constexpr int KR = kFlatRows / 64;
+        T va[KR], vb[KR], vc[KR];
+        int kind[KR];
+        _Pragma("unroll") for (int k = 0; k < KR; ++k) {
+            const int q = kFlatRows * (task - Tq - Tl) + 64 * k + lane;
+            int ia = 0, ib = 0, ic = 0;
+            kind[k] = -1;
+            if (q < ny) {  // y_i[k] = eta1 - b_k eta2_i
+                const int i = q / G, kk = q - i * G;
+                ia = p.E1 + q; ib = p.E2 + i; ic = kk < C ? 1 + C * i + kk : 0;
+                kind[k] = kk < C ? 0 : kk < 2 * C ? 1 : 2;
+            } else if (q < ny + n) {  // s_i = eta2_i | s_l = (eta12 + eta13) / 2
+                const int i = q - ny;
+                ia = i < m ? p.E2 + i : p.E12 + i; ib = p.E13 + i;
+                kind[k] = i < m ? 3 : 4;
+            } else if (q < nrow) {  // tau_j = (eta5 + eta6) / 2
+                const int j = q - ny - n + 1;
+                ia = p.E5 + j; ib = p.E6 + j;
+                kind[k] = 4;
+            }
+            va[k] = d[ia];
+            vb[k] = d[ib];
+            vc[k] = ((cglbp<T>)p.cond)[ic];
+        }
+        _Pragma("unroll") for (int k = 0; k < KR; ++k) {
+            const int q = kFlatRows * (task - Tq - Tl) + 64 * k + lane;
+            const int kd = kind[k];
+            if (kd < 0) continue;
+            const T b = kd == 0 ? vc[k] : kd == 1 ? T(0) : T(1);
+            const T v = kd <= 2 ? va[k] - b * vb[k] : kd == 3 ? va[k] : T(0.5) * (va[k] + vb[k]);
+            const int o = q < ny ? p.Y0 + q : q < ny + n ? p.S0 + (q - ny) : p.T0 + (q - ny - n + 1);
+            zg[o] = v;
         }
     }
 }
