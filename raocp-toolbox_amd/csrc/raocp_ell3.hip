@@ -71,10 +71,11 @@ __device__ __forceinline__ void mma_perm(const WPerm<T, R, K>& w, const T (&a)[(
 
 // store a 16-node x R-row tile (accumulators of RT row tiles) to rows dst + node * R + r of
 // a contiguous block, through a per-wave LDS image (row stride R + 1: conflict-free writes)
-// so every store instruction writes 64 consecutive elements
+// so every store instruction writes 64 consecutive elements. rep > 1: every image row is
+// stored rep times to consecutive destination rows (cnt image rows -> cnt rep rows)
 template <class T, int R>
 __device__ __forceinline__ void store_tile(__attribute__((address_space(3))) T* img, const typename MF<T>::v4 (&acc)[(R + 15) / 16],
-                                           int cnt, glbp<T> dst) {
+                                           int cnt, glbp<T> dst, int rep = 1) {
     constexpr int RT = (R + 15) / 16, S = R + 1;
     const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4;
     _Pragma("unroll") for (int e = 0; e < 4; ++e) {
@@ -86,22 +87,22 @@ __device__ __forceinline__ void store_tile(__attribute__((address_space(3))) T* 
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-    const int tot = cnt * R;
+    const int tot = cnt * rep * R;
     constexpr int V = Vec16<T>::V;
     if constexpr (R % V == 0) {
         // 16 B per lane (a lane's V elements lie in one row): a quarter (fp32) / half (fp64)
         // of the store instructions of one element per lane
         typedef typename Vec16<T>::type vt;
         for (int q = lane * V; q < tot; q += 64 * V) {
-            const int a = q / R, r = q - a * R;
+            const int a = q / R, r = q - a * R, ia = rep == 1 ? a : a / rep;
             vt w;
-            _Pragma("unroll") for (int u = 0; u < V; ++u) w[u] = img[a * S + r + u];
+            _Pragma("unroll") for (int u = 0; u < V; ++u) w[u] = img[ia * S + r + u];
             *(__attribute__((address_space(1))) vt*)(dst + q) = w;
         }
     } else {
         for (int q = lane; q < tot; q += 64) {
-            const int a = q / R, r = q - a * R;
-            dst[q] = img[a * S + r];
+            const int a = q / R, r = q - a * R, ia = rep == 1 ? a : a / rep;
+            dst[q] = img[ia * S + r];
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -137,7 +138,10 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
     glbp<T> eg = (glbp<T>)eta_;
     const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4;
     const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nwv = gridDim.x * (blockDim.x >> 6);
-    const int Tc = (n - 1 + 15) >> 4, Tl = (n - m + 15) >> 4;
+    // C > 0 (uniform branching): parent tiles of 16 parents, each product sqrtQ x_i / sqrtR u_i
+    // computed once and stored to the C children's eta3 / eta4 rows (one table over the
+    // children); C == 0: child tiles of 16 children reading their ancestors' rows
+    const int Tc = C ? (m + 15) >> 4 : (n - 1 + 15) >> 4, Tl = (n - m + 15) >> 4;
     const int y1 = p.T0 - p.Y0;  // eta1 = y over the whole y segment
     const int nrow = m * (nx + nu) + y1 + m;
     const int fbeg = C ? m * (nx + nu) : 0;  // eta7 rows: written by the child tiles when C > 0
@@ -147,9 +151,57 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
     // per-wave LDS image of one output tile (16 nodes x (nx + 1))
     __shared__ T simg[4][16 * (NX + 1)];
     __attribute__((address_space(3))) T* img = (__attribute__((address_space(3))) T*)simg[threadIdx.x >> 6];
+    if (C) {
+        int task = gw;
+        // cr.w: eta7 offset of parent lo of the tile (-1: unboxed / none)
+        auto fetch = [&](int tk, int& o7, T (&ax)[(NX + 3) / 4], T (&au)[(NU + 3) / 4]) {
+            const int i = 16 * tk + lo;
+            const bool la = tk < Tc && i < m;
+            o7 = la ? o7_of<NX, NU>(p, i, bx) : -1;
+            load_arow<T, NX>(la ? z + p.X0 + (size_t)i * nx : nullptr, ax);
+            load_arow<T, NU>(la ? z + p.U0 + (size_t)i * nu : nullptr, au);
+        };
+        int o7;
+        T ax[(NX + 3) / 4], au[(NU + 3) / 4];
+        if (task < Tc) {
+            fetch(task, o7, ax, au);
+            wq.load((const T*)p.SQ, p.crec[1].y);  // one table over the children (host check)
+            wr.load((const T*)p.SR, p.crec[1].z);
+        }
+        for (; task < Tc; task += nwv) {
+            const int i0 = 16 * task, cnt = min(16, m - i0);
+            const int j0 = 1 + C * i0, cc = C * cnt;  // the tile's children j0 .. j0 + cc
+            // eta5 = eta6 = tau_j / 2 of the cc <= 64 children: lane -> child j0 + lane
+            const T tv = lane < cc ? z[p.T0 + j0 + lane] : T(0);
+            int o7b;
+            T ax2[(NX + 3) / 4], au2[(NU + 3) / 4];
+            fetch(task + nwv, o7b, ax2, au2);
+            v4 cx[RTX], cu[RTU];
+            _Pragma("unroll") for (int r = 0; r < RTX; ++r) cx[r] = v4{0, 0, 0, 0};
+            _Pragma("unroll") for (int r = 0; r < RTU; ++r) cu[r] = v4{0, 0, 0, 0};
+            mma_perm(wq, ax, cx);
+            mma_perm(wr, au, cu);
+            store_tile<T, NX>(img, cx, cnt, eg + e3(p, j0), C);
+            store_tile<T, NU>(img, cu, cnt, eg + e4(p, j0), C);
+            if (lane < cc) {
+                eg[p.E5 + j0 + lane] = T(0.5) * tv;
+                eg[p.E6 + j0 + lane] = T(0.5) * tv;
+            }
+            if (o7 >= 0) {
+                // eta7_i = [x_i; u_i] of a boxed parent from the A registers
+                constexpr int KX = (NX + 3) / 4, KU = (NU + 3) / 4;
+                _Pragma("unroll") for (int k = 0; k < KX; ++k)
+                    if (KX * h + k < nx) eg[o7 + KX * h + k] = ax[k];
+                _Pragma("unroll") for (int k = 0; k < KU; ++k)
+                    if (KU * h + k < nu) eg[o7 + nx + KU * h + k] = au[k];
+            }
+            o7 = o7b;
+            _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];
+            _Pragma("unroll") for (int k = 0; k < (NU + 3) / 4; ++k) au[k] = au2[k];
+        }
+    } else {
     // child tiles: loads of the wave's next tile are issued before the current tile's MFMAs
     // and stores (vmcnt is in order: loads issued after a store would wait for it)
-    {
         int task = gw;
         auto fetch = [&](int tk, Rec& cr, T (&ax)[(NX + 3) / 4], T (&au)[(NU + 3) / 4]) {
             const int ja = 1 + 16 * tk + lo;
