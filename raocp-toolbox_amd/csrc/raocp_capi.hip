@@ -1906,9 +1906,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         c->ellt3_C = reg ? C : 0;
         const long tasks_t = (long)(m + 4 * (4 / std::max(C, 1)) - 1) / (4 * (4 / std::max(C, 1))) + (n - m + 15) / 16 +
                              ((long)(c->dev.T0 - c->dev.Y0) + 2L * n - 1 + 63) / 64;
-        // grid sweep (profiles/r02_v3/ab_q.log): config 4 fp64 best at 4,096 blocks (25.5 us
-        // vs 26.2 at 2,048), config 5 fp32 at 2,048 (115 vs 121 us at 4,096, 141 at 1,024)
-        c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, c->f32 ? 2048L : 4096L));
+        // grid sweep (profiles/r02_v4/ab_grid.log): 1,536 blocks best at config 4 fp64 (24.0 us
+        // vs 24.9 at 4,096, 28.0 at 1,024) and config 5 fp32 (109.4 vs 111.1 at 2,048)
+        c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, 1536L));
         if (const char* e = getenv("RAOCP_ELLT3_GRID")) c->ellt3_grid = std::max(1, atoi(e));
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels
