@@ -413,7 +413,10 @@ def main():
 
     # HBM regime: the L / L^T kernels at config 4 (88,573 nodes, nx = 32,
     # nu = 12: 104.6 MB per application, past L2)
-    l_sweep = {"config2": {"L": kernels["k_ell"], "L_transpose": kernels["k_ell_t"]}}
+    # the kernels the default selection launches on these uniform trees (the
+    # rocprofv3 names in profiles/<latest>/prof_kernel_stats.csv)
+    l_sweep = {"config2": {"L": dict(kernels["k_ell"], kernel="k_ell3<double, 20, 8>"),
+                           "L_transpose": dict(kernels["k_ell_t"], kernel="k_ellt3<double, 20, 8, 2>")}}
     if not args.no_hbm:
         r4 = recipe_config(4, seed=0)
         c4 = core.Cache(build_problem(r4)[1])
@@ -421,9 +424,11 @@ def main():
         m4l, m4t = c4.native.op_bench(0, 200), c4.native.op_bench(1, 200)
         bb = b4P + b4D
         l_sweep["config4"] = {"config": "SURVEY.md 8(d) config 4: 88,573 nodes, nx=32, nu=12", "bytes_per_launch": bb,
-                              "L": {"us_per_launch": m4l * 1e3, "achieved": bb / (m4l * 1e-3) / 1e9,
+                              "L": {"kernel": "k_ell3<double, 32, 12>", "us_per_launch": m4l * 1e3,
+                                    "achieved": bb / (m4l * 1e-3) / 1e9,
                                     "frac": bb / (m4l * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                              "L_transpose": {"us_per_launch": m4t * 1e3, "achieved": bb / (m4t * 1e-3) / 1e9,
+                              "L_transpose": {"kernel": "k_ellt3<double, 32, 12, 1>", "us_per_launch": m4t * 1e3,
+                                              "achieved": bb / (m4t * 1e-3) / 1e9,
                                               "frac": bb / (m4t * 1e-3) / 1e9 / HBM_PEAK_GBS},
                               "unit": "GB/s", "peak": HBM_PEAK_GBS}
         del c4
@@ -441,9 +446,10 @@ def main():
         fp32 = {"config": "SURVEY.md 8(d) config 5 (BASELINE configs[4]): branching 4, N=9, 349,525 nodes, nx=64, "
                           "nu=16, fp32 iterate / tables / products (MFMA f32 tiles)", "dtype": "f32",
                 "bytes_per_launch": b5,
-                "L": {"us_per_launch": m5l * 1e3, "achieved": b5 / (m5l * 1e-3) / 1e9,
+                "L": {"kernel": "k_ell3<float, 64, 16>", "us_per_launch": m5l * 1e3, "achieved": b5 / (m5l * 1e-3) / 1e9,
                       "frac": b5 / (m5l * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                "L_transpose": {"us_per_launch": m5t * 1e3, "achieved": b5 / (m5t * 1e-3) / 1e9,
+                "L_transpose": {"kernel": "k_ellt3<float, 64, 16, 1>", "us_per_launch": m5t * 1e3,
+                                "achieved": b5 / (m5t * 1e-3) / 1e9,
                                 "frac": b5 / (m5t * 1e-3) / 1e9 / HBM_PEAK_GBS},
                 "cp": {"value": args.fp32_steps / w5, "unit": "it/s", "steps": args.fp32_steps,
                        "ms_per_step": 1e3 * w5 / args.fp32_steps},
