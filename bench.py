@@ -29,15 +29,17 @@ as the /opt/rocm one libraocp_hip.so links, and RCCL (dlopen'ed by the library) 
 initialise next to it. Barriers and the max-over-ranks go through a socket group.
 
 The JSON line also carries
-  roofline: the dominant kernel of the timed CP iteration (largest device time per
-            iteration), timed with HIP events on the context's stream over a graph of
-            back-to-back launches on a valid control block; algorithmic bytes per launch
-            over active entries; peak 8 TB/s HBM3E (cache-resident at this
-            size);
-  kernels:  the same figure for every kernel of the iteration;
-  l_sweep:  L and L^T at config 2, at config 4 (104.6 MB per launch, the HBM regime) and in
-            fp32 at config 5 (383.4 MB per launch);
-  fp32_config5: BASELINE configs[4] (fp32, 349,525 nodes, nx = 64): L / L^T and CP it/s;
+  roofline: the part of the timed CP iteration with the larger device time (the kernel after
+            the dynamics sweep -- the fused k_cp3 on the benchmark trees -- or the dynamics
+            projection), timed with HIP events on the context's stream over a graph of
+            back-to-back launches on a valid control block; algorithmic bytes per launch over
+            active entries (DESIGN.md 4); peak 8 TB/s HBM3E (cache-resident at this size);
+            its share of the step and the other part's figure next to it;
+  kernels:  both parts of the iteration, named by the library's own selection;
+  l_sweep:  L and L^T at config 2 (cache-resident), at config 4 and in fp32 at config 5 over
+            rotating buffer sets larger than the 256 MiB Infinity Cache (the HBM regime);
+  config4 / fp32_config5: BASELINE configs[3] (fp64, 88,573 nodes, nx = 32) and configs[4]
+            (fp32, 349,525 nodes, nx = 64) on one GPU: CP it/s, kernels, roofline, L / L^T;
   cpu_baseline: the oracle (vectorised NumPy restatement, oracle/raocp_oracle.py)
             timed on this host on a bounded sample of the same workload, next to the
             reference's own CPU figure measured in the build container.
@@ -82,19 +84,16 @@ def algorithmic_bytes(cache):
     return 8 * P, 8 * D
 
 
-def kernel_bytes(cache):
-    """Algorithmic bytes per launch of each kernel of the CP iteration:
-    every input vector read once, every output written once, tables excluded."""
+def kernel_bytes(cache, w=8):
+    """Algorithmic bytes per launch: every input vector read once, every
+    output written once, tables excluded. The CP iteration after the dynamics sweep:
+    the fused k_cp3 reads p, z+, d and writes eta+ and the next half step (3|P| + 2|D|);
+    the two-launch k_cpd* + k_cpp* also write and re-read xi2 and re-read p, z+, d
+    (5|P| + 6|D|). The dynamics projection reads and writes x, u."""
     P, D = active_sizes(cache)
     pk = cache.packed
-    dyn = 2 * (pk.n * pk.nx + pk.m * pk.nu)
-    return {
-        "k_ell": 8 * (P + D),                # z -> L z
-        "k_ell_t": 8 * (P + D),              # eta -> L^T eta
-        "k_cpd": 8 * (2 * P + 3 * D),        # p, z+, d -> eta+, xi2
-        "k_cpp": 8 * (3 * P + 3 * D),        # p, z+, d, eta+, xi2 -> next half step
-        "dynamics": 8 * dyn,                 # x, u in and out (all tier launches of one projection)
-    }
+    return {"cp_fused": w * (3 * P + 2 * D), "cp_two": w * (5 * P + 6 * D),
+            "dynamics": w * 2 * (pk.n * pk.nx + pk.m * pk.nu), "L": w * (P + D)}
 
 
 def pmc_traffic(kernel):
@@ -331,8 +330,82 @@ def sharded_entry(args, world):
     desc.update({"value": r["its"], "ms_per_step": 1e3 * r["wall_s"] / r["steps"], "nodes": r["nodes"],
                  "device_ms_per_step": r["device_ms"] / r["steps"],
                  "exchanges": "per iteration: all-gather of the boundary roots' q rows (dynamics), all-gather of "
-                              "their eta2 entries, all-reduce (max) of the residual maxima" if world > 1 else None})
+                              "their eta+ / xi2 eta2 entries together with the previous iteration's residual record "
+                              "(the stopping test runs one iteration late, so the residual reduction rides on it)"
+                              if world > 1 else None})
     return desc
+
+
+def _rate(b, us):
+    gbs = b / (us * 1e-6) / 1e9
+    return {"us_per_launch": us, "bytes_per_launch": b, "achieved": gbs, "frac": gbs / HBM_PEAK_GBS}
+
+
+def iteration_kernels(nat, cache, w, reps, dev_ms_per_step):
+    """HIP-event times (graph of back-to-back launches on the context's stream, valid control
+    block) of the two parts of a CP iteration: the dynamics projection (op 9: a chain of tier
+    launches, reported as a whole) and the kernel(s) after it (op 10: the fused k_cp3, or
+    k_cpd* + k_cpp*); kernel names from the library's own selection (raocp_kernel_info).
+    The roofline names the part with the larger device time per iteration."""
+    kb = kernel_bytes(cache, w)
+    name_cp, name_dyn = nat.kernel_info(10), nat.kernel_info(9)
+    fused = name_cp.startswith("k_cp3")
+    t_cp = 1e3 * nat.op_bench(10, reps)
+    t_dyn = 1e3 * nat.op_bench(9, max(1, reps // 4))
+    kernels = {"cp": dict(_rate(kb["cp_fused" if fused else "cp_two"], t_cp), kernel=name_cp, in_cp_iteration=True),
+               "dynamics": dict(_rate(kb["dynamics"], t_dyn), kernel=name_dyn, in_cp_iteration=True)}
+    dev_us = 1e3 * dev_ms_per_step
+    for k in kernels.values():
+        k["share_of_step"] = k["us_per_launch"] / dev_us if dev_us > 0 else None
+    dom = max(kernels, key=lambda k: kernels[k]["us_per_launch"])
+    traffic, src = pmc_traffic(kernels[dom]["kernel"]) if dom == "cp" else (None, None)
+    roofline = {"bound": "hbm", "kernel": kernels[dom]["kernel"], "part": dom, "achieved": kernels[dom]["achieved"],
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kernels[dom]["frac"], "traffic": traffic,
+                "traffic_source": src, "bytes_per_launch": kernels[dom]["bytes_per_launch"],
+                "us_per_launch": kernels[dom]["us_per_launch"], "share_of_step": kernels[dom]["share_of_step"],
+                "other_part": {k: kernels[k]["kernel"] + f": {kernels[k]['us_per_launch']:.1f} us, frac "
+                                                         f"{kernels[k]['frac']:.3f}" for k in kernels if k != dom}}
+    return kernels, roofline
+
+
+def op_pair(nat, cache, w, reps, nsets):
+    """L / L^T (standalone operators): HIP events over a graph of back-to-back launches;
+    nsets > 1 cycles over that many input / output buffer pairs (beyond the 256 MiB
+    Infinity Cache for configs 4 and 5: every launch reads HBM)."""
+    P, D = active_sizes(cache)
+    b = w * (P + D)
+    res = {}
+    for op, key in ((0, "L"), (1, "L_transpose")):
+        ms = nat.op_bench_rot(op, reps, nsets) if nsets > 1 else nat.op_bench(op, reps)
+        res[key] = dict(_rate(b, 1e3 * ms), kernel=nat.kernel_info(op))
+    res.update({"buffer_sets": nsets, "bytes_per_set": w * (P + D),
+                "regime": "HBM (buffer sets beyond the 256 MiB Infinity Cache)" if nsets * b > 256 * 2 ** 20
+                else "cache-resident"})
+    return res
+
+
+def config_leg(cfg, dtype, steps, warmup, reps, nsets):
+    """One BASELINE config on this GPU: CP it/s of the timed loop, its kernels and roofline,
+    L / L^T over rotating buffer sets."""
+    import raocp.core as core
+    from raocp.problems import build_problem, recipe_config
+    r = recipe_config(cfg, seed=0)
+    c = core.Cache(build_problem(r)[1], dtype=dtype)
+    nat = c.native
+    w = 4 if dtype == "float32" else 8
+    alpha = 0.999 / nat.step_size(rtol=1e-7 if w == 4 else 1e-14)
+    wall, dev_ms = timed_cp(nat, r["x0"], alpha, steps, warmup, None)
+    kernels, roofline = iteration_kernels(nat, c, w, reps, dev_ms / steps)
+    pk = c.packed
+    leg = {"config": f"SURVEY.md 8(d) config {cfg} (BASELINE configs[{cfg - 1}]): {pk.n} nodes, nx={pk.nx}, nu={pk.nu}",
+           "dtype": "f32" if w == 4 else "f64", "nodes": pk.n,
+           "cp": {"value": steps / wall, "unit": "it/s", "steps": steps, "ms_per_step": 1e3 * wall / steps,
+                  "device_ms_per_step": dev_ms / steps},
+           "kernels": kernels, "roofline": roofline}
+    if nsets:
+        leg["l_sweep"] = op_pair(nat, c, w, max(10, reps // 2), nsets)
+    del c
+    return leg
 
 
 def main():
@@ -352,6 +425,8 @@ def main():
     ap.add_argument("--shard-steps", type=int, default=200)
     ap.add_argument("--shard-warmup", type=int, default=20)
     ap.add_argument("--shard-timeout", type=float, default=240.0)
+    ap.add_argument("--rank-timeout", type=float, default=1500.0,
+                    help="time limit of the rank processes bench.py --gpus N starts itself")
     ap.add_argument("--shard-leg", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -359,7 +434,7 @@ def main():
         return shard_leg(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # start the N rank processes (no GPU has been touched in this one)
-        out, rcs = spawn(args.gpus, sys.argv[1:])
+        out, rcs = spawn(args.gpus, sys.argv[1:], timeout=args.rank_timeout)
         sys.stdout.write(out)
         sys.stdout.flush()
         return rcs[0] if rcs[0] else max(abs(rc) for rc in rcs)
@@ -389,73 +464,17 @@ def main():
         group.barrier()  # rank 0 measures the rest; the sharded leg uses every GPU
         return 0
 
-    # per-kernel HIP-event timings of the CP iteration's kernels (graph of back-to-back
-    # launches on a valid control block, the context's stream), algorithmic bytes / time
-    kb = kernel_bytes(cache)
-    reps = args.op_reps
-    ms = {"k_cpd": nat.op_bench(2, reps), "k_cpp": nat.op_bench(6, reps), "dynamics": nat.op_bench(9, max(1, reps // 4)),
-          "k_ell": nat.op_bench(0, reps), "k_ell_t": nat.op_bench(1, reps)}
-    kernels = {}
-    for k, t in ms.items():
-        gbs = kb[k] / (t * 1e-3) / 1e9
-        kernels[k] = {"us_per_launch": t * 1e3, "bytes_per_launch": kb[k], "achieved": gbs, "frac": gbs / HBM_PEAK_GBS,
-                      "in_cp_iteration": k in ("k_cpd", "k_cpp", "dynamics")}
-    # the dominant single kernel of the timed iteration (the dynamics projection is a chain of
-    # launches, one per tier, reported under kernels["dynamics"] as a whole)
-    dom = max(("k_cpd", "k_cpp"), key=lambda k: ms[k])
-    tname = {"k_cpd": f"k_cpd<{cache.packed.nx}, {cache.packed.nu}>", "k_cpp": f"k_cpp<{cache.packed.nx}, {cache.packed.nu}>"}
-    traffic, traffic_src = pmc_traffic(tname.get(dom, dom))
-    roofline = {"bound": "hbm", "kernel": dom, "achieved": kernels[dom]["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": kernels[dom]["frac"], "traffic": traffic, "traffic_source": traffic_src,
-                "bytes_per_launch": kb[dom], "us_per_launch": kernels[dom]["us_per_launch"],
-                "note": "dominant kernel of the timed CP iteration; working set L2/MALL-resident at this size "
-                        "(SURVEY.md 8(d)), so the HBM fraction is an effective cache-resident bandwidth"}
-
-    # HBM regime: the L / L^T kernels at config 4 (88,573 nodes, nx = 32,
-    # nu = 12: 104.6 MB per application, past L2)
-    # the kernels the default selection launches on these uniform trees (the
-    # rocprofv3 names in profiles/<latest>/prof_kernel_stats.csv)
-    l_sweep = {"config2": {"L": dict(kernels["k_ell"], kernel="k_ell3<double, 20, 8>"),
-                           "L_transpose": dict(kernels["k_ell_t"], kernel="k_ellt3<double, 20, 8, 2>")}}
+    kernels, roofline = iteration_kernels(nat, cache, 8, args.op_reps, dev_ms / args.steps)
+    # L / L^T at config 2 (standalone operators, not launched by the CP iteration)
+    l_sweep = {"config2": op_pair(nat, cache, 8, args.op_reps, 1)}
+    legs = {}
     if not args.no_hbm:
-        r4 = recipe_config(4, seed=0)
-        c4 = core.Cache(build_problem(r4)[1])
-        b4P, b4D = algorithmic_bytes(c4)
-        m4l, m4t = c4.native.op_bench(0, 200), c4.native.op_bench(1, 200)
-        bb = b4P + b4D
-        l_sweep["config4"] = {"config": "SURVEY.md 8(d) config 4: 88,573 nodes, nx=32, nu=12", "bytes_per_launch": bb,
-                              "L": {"kernel": "k_ell3<double, 32, 12>", "us_per_launch": m4l * 1e3,
-                                    "achieved": bb / (m4l * 1e-3) / 1e9,
-                                    "frac": bb / (m4l * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                              "L_transpose": {"kernel": "k_ellt3<double, 32, 12, 1>", "us_per_launch": m4t * 1e3,
-                                              "achieved": bb / (m4t * 1e-3) / 1e9,
-                                              "frac": bb / (m4t * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                              "unit": "GB/s", "peak": HBM_PEAK_GBS}
-        del c4
-    # BASELINE configs[4]: fp32, 349,525 nodes, nx = 64, nu = 16 (383.4 MB per L): L / L^T and
-    # the CP loop of an fp32 context
+        legs["config4"] = config_leg(4, "float64", args.shard_steps, args.shard_warmup, 200, 3)
+        l_sweep["config4"] = legs["config4"]["l_sweep"]
     fp32 = None
     if not args.no_fp32:
-        r5 = recipe_config(5, seed=0)
-        c5 = core.Cache(build_problem(r5)[1], dtype="float32")
-        P5, D5 = active_sizes(c5)
-        b5 = 4 * (P5 + D5)
-        m5l, m5t = c5.native.op_bench(0, 100), c5.native.op_bench(1, 100)
-        a5 = 0.999 / c5.native.step_size(rtol=1e-7)
-        w5, d5 = timed_cp(c5.native, r5["x0"], a5, args.fp32_steps, 2, None)
-        fp32 = {"config": "SURVEY.md 8(d) config 5 (BASELINE configs[4]): branching 4, N=9, 349,525 nodes, nx=64, "
-                          "nu=16, fp32 iterate / tables / products (MFMA f32 tiles)", "dtype": "f32",
-                "bytes_per_launch": b5,
-                "L": {"kernel": "k_ell3<float, 64, 16>", "us_per_launch": m5l * 1e3, "achieved": b5 / (m5l * 1e-3) / 1e9,
-                      "frac": b5 / (m5l * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                "L_transpose": {"kernel": "k_ellt3<float, 64, 16, 1>", "us_per_launch": m5t * 1e3,
-                                "achieved": b5 / (m5t * 1e-3) / 1e9,
-                                "frac": b5 / (m5t * 1e-3) / 1e9 / HBM_PEAK_GBS},
-                "cp": {"value": args.fp32_steps / w5, "unit": "it/s", "steps": args.fp32_steps,
-                       "ms_per_step": 1e3 * w5 / args.fp32_steps},
-                "unit": "GB/s", "peak": HBM_PEAK_GBS}
-        l_sweep["config5_fp32"] = {k: fp32[k] for k in ("config", "bytes_per_launch", "L", "L_transpose", "unit", "peak")}
-        del c5
+        legs["config5_fp32"] = fp32 = config_leg(5, "float32", args.fp32_steps, 2, 40, 2)
+        l_sweep["config5_fp32"] = fp32["l_sweep"]
 
     out = {
         "metric": METRIC, "value": its, "unit": "it/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -470,6 +489,7 @@ def main():
         "roofline": roofline,
         "kernels": kernels,
         "l_sweep": l_sweep,
+        "config4": legs.get("config4"),
         "fp32_config5": fp32,
     }
     if not args.no_shard:
@@ -478,15 +498,12 @@ def main():
         out["cpu_baseline"] = cpu_baseline(recipe, args.cpu_seconds)
     if world == 1 and not args.no_shard:
         # N = 1 point of the strong-scaling leg: the same config-4 tree unsharded in this process
-        r4 = recipe_config(args.shard_config, seed=0)
-        c4 = core.Cache(build_problem(r4)[1])
-        a4 = 0.999 / c4.native.step_size()
-        w4, d4 = timed_cp(c4.native, r4["x0"], a4, args.shard_steps, args.shard_warmup, None)
+        c4 = (legs.get("config4") if args.shard_config == 4 else None) or config_leg(args.shard_config, "float64", args.shard_steps, args.shard_warmup, 200, 0)
         out["sharded"] = {"config": f"SURVEY.md 8(d) config {args.shard_config} (BASELINE configs[{args.shard_config - 1}]): "
                                     "ONE tree, unsharded on 1 GPU (the N = 1 point of the strong-scaling leg)",
                           "n_gpus": 1, "steps": args.shard_steps, "unit": "it/s", "scaling": "strong",
-                          "value": args.shard_steps / w4, "ms_per_step": 1e3 * w4 / args.shard_steps,
-                          "device_ms_per_step": d4 / args.shard_steps, "nodes": c4.packed.n}
+                          "value": c4["cp"]["value"], "ms_per_step": c4["cp"]["ms_per_step"],
+                          "device_ms_per_step": c4["cp"]["device_ms_per_step"], "nodes": c4["nodes"]}
     print(json.dumps(out), flush=True)
     if group:
         group.barrier()

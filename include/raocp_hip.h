@@ -125,6 +125,13 @@ int raocp_set_dual(raocp_ctx* ctx, const double* eta, int flags);
 int raocp_get_dual(raocp_ctx* ctx, double* eta, int flags);
 /* Cache.cache_initial_state (cache.py:79-82): x0 has nx entries. */
 int raocp_set_initial_state(raocp_ctx* ctx, const double* x0);
+/* Zero the current primal and dual on the device: the iterate of a fresh Cache
+ * (cache.py:126-170 zero templates), without a host upload (cold-started chock). */
+int raocp_reset_iterate(raocp_ctx* ctx);
+/* Name of the kernel the context's default selection launches for `op` (raocp_op_bench
+ * numbering: 0 L, 1 L^T, 2 dual CP kernel, 6 primal CP kernel, 9 dynamics projection,
+ * 10 fused CP iteration), as rocprofv3 reports it; written NUL-terminated to buf. */
+int raocp_kernel_info(raocp_ctx* ctx, int op, char* buf, int cap);
 
 /* prox of f on the current primal (Cache.proximal_of_f, cache.py:248-257) and its steps */
 int raocp_prox_f(raocp_ctx* ctx, double alpha);
@@ -172,14 +179,20 @@ int raocp_cp_bench(raocp_ctx* ctx, const double* x0, int iters, double alpha, fl
 /* Time `reps` back-to-back launches of L (op=0) or L^T (op=1) on device-resident
  * vectors with HIP events on the context's stream; returns average ms per launch. */
 int raocp_op_bench(raocp_ctx* ctx, int op, int reps, float* ms_per_launch);
+/* The same for L (op 0) / L^T (op 1) with the launches cycling over `nsets` (<= 16) freshly
+ * allocated input / output buffer pairs, so that a working set beyond the 256 MiB Infinity
+ * Cache is read from HBM on every launch. */
+int raocp_op_bench_rot(raocp_ctx* ctx, int op, int reps, int nsets, float* ms_per_launch);
 /* Diagnostics: one dynamics projection with in-kernel s_memrealtime stamps (100 MHz). */
 int raocp_debug_dyn_stamps(raocp_ctx* ctx, unsigned long long* stamps, int cap);
 
 /* Subtree sharding across GPUs (north_star "scenarios shard naturally
  * by subtree"). Shard `rank` of `nranks` owns a contiguous block of the subtrees rooted
  * at the boundary stage of the replicated top of the tree; the CP iteration then runs on
- * the owned nodes only, with three exchanges per iteration (q rows of the roots, the
- * roots' eta2 / xi2 entries, and an all-reduce of the residual maxima).
+ * the owned nodes only, with two all-gathers per iteration: the q rows of the roots
+ * (dynamics backward sweep), and the roots' eta2 / xi2 entries together with the previous
+ * iteration's residual record (the stopping test runs one iteration late, so the residual
+ * reduction needs no collective of its own).
  * raocp_shard_setup restricts this context to its shard; raocp_comm_init binds an RCCL
  * communicator (one process per GPU; the 128-byte id comes from raocp_comm_unique_id on
  * one rank); raocp_cp_run / raocp_cp_bench then run the sharded iteration.

@@ -53,8 +53,12 @@ struct raocp_ctx {
     int ell3_grid = 0;
     int box_mode = 0;            // k_ell3 / k_ellt3: bits 0-1 nonleaf, 2-3 leaf boxes (1 all, 2 none, 0 mixed)
     int unif_C = 0;              // uniform branching factor <= 4 with uniform tables (0 = not)
+    int unif_branch = 0;         // uniform branching factor <= 4 (children 1 + C i ..), any tables (dyn3)
     int ellt3_C = 0;             // L^T by streaming wave tasks: uniform branching factor (0 = off)
     int ellt3_grid = 0;
+    bool cp3 = false;            // the CP iteration after the dynamics as one streaming kernel (raocp_cp3.hip)
+    int cp3_grid = 0;
+    int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
     // per-stage MFMA dynamics (raocp_dyn2.hip): tables, node lists, tile lists per stage
     bool dyn2 = false;           // fp32 contexts always; fp64 opt-in RAOCP_DYN2=1
     const double *W2 = nullptr, *RG2 = nullptr, *KM2 = nullptr, *F2 = nullptr;
@@ -62,6 +66,10 @@ struct raocp_ctx {
     const raocp::DynTile* d2_tiles = nullptr;
     std::vector<int> d2_off;     // per stage t: [prod, node, fwdU, fwdX] tile offsets, 5 entries
     double *Q2 = nullptr, *PA2 = nullptr, *Dd2 = nullptr;
+    // per-stage streaming dynamics (raocp_dyn3.hip): uniform branching, per-slot kinds and one
+    // class per stage; fp32 contexts by default, fp64 opt-in RAOCP_DYN3=1
+    bool dyn3 = false;
+    std::vector<raocp::Dy3Stage> d3st;
     int wsz = 8;                 // bytes per scalar of the iterate
     hipStream_t stream = nullptr;
     Dev dev{};
@@ -391,6 +399,46 @@ struct Dyn2Op {
     }
 };
 
+// the per-stage streaming sweep (raocp_dyn3.hip) on z; ck: the previous iteration's stopping
+// test in an extra workgroup of the first launch (defer_check)
+template <class T, int NX, int NU>
+void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck) {
+    typedef raocp::Dy3Lds<T, NX, NU> L;
+    const int C = c->unif_branch;
+    const size_t lb = (size_t)L::back_n(C) * sizeof(T), lf = (size_t)L::fwd_n(C) * sizeof(T);
+    const int thr = std::max(lb, lf) > 64 * 1024 ? 512 : 256, wpb = thr / 64;
+    auto kb = raocp::k_dy3_back<T, NX, NU>;
+    auto kf = raocp::k_dy3_fwd<T, NX, NU>;
+    allow_lds(kb, lb);
+    allow_lds(kf, lf);
+    auto grid = [&](const raocp::Dy3Stage& st) {
+        const int tiles = (st.i1 - st.i0 + 15) / 16;
+        return std::max(1, std::min(512, (tiles + wpb - 1) / wpb));
+    };
+    const int N = c->N;
+    for (int t = N - 1; t >= 0; --t) {
+        const raocp::Dy3Stage& st = c->d3st[t];
+        raocp::ChkArg ca{};
+        if (ck && t == N - 1) ca = *ck;
+        kb<<<grid(st) + ca.on, thr, lb, c->stream>>>(c->dev, ctl, ca, z, c->Q2, c->Dd2, st, C, c->W2, c->RG2);
+    }
+    for (int t = 0; t < N; ++t) {
+        const raocp::Dy3Stage& st = c->d3st[t];
+        kf<<<grid(st), thr, lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, st, C, c->KM2, c->F2);
+    }
+}
+void launch_dyn3(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck) {
+    if (c->f32) {
+        if (c->nx == 20) launch_dyn3t<float, 20, 8>(c, z, ctl, ck);
+        else if (c->nx == 32) launch_dyn3t<float, 32, 12>(c, z, ctl, ck);
+        else launch_dyn3t<float, 64, 16>(c, z, ctl, ck);
+    } else {
+        if (c->nx == 20) launch_dyn3t<double, 20, 8>(c, z, ctl, ck);
+        else if (c->nx == 32) launch_dyn3t<double, 32, 12>(c, z, ctl, ck);
+        else launch_dyn3t<double, 64, 16>(c, z, ctl, ck);
+    }
+}
+
 struct DynOp {
     // part: 0 whole projection; 1 the tiers' backward sweeps only; 2 the top and the
     // tiers' forward sweeps (a shard exchanges the roots' q rows in between)
@@ -481,6 +529,11 @@ struct DynOp {
 // launch (only where defer_check(c) holds)
 void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part = 0,
                      const raocp::ChkArg* ck = nullptr) {
+    if (c->dyn3 && c->sh_S == 0) {
+        double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
+        launch_dyn3(c, z, ctl, ck);
+        return;
+    }
     if (c->dyn2) {
         double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
         if (c->f32) dispatch_rt(c->nx, c->nu, Dyn2Op<float>{}, c, z, ctl);
@@ -591,6 +644,22 @@ void launch_cpp(raocp_ctx* c, bool fuse = false) {
     else if (c->cp_v1 || fuse) dispatch(c->nx, c->nu, CppOp{}, c, fuse);
     else dispatch_rt(c->nx, c->nu, Cpp2Op<double>{}, c);
 }
+// the fused CP iteration (raocp_cp3.hip): compile-time sizes of the benchmark configs
+// instantiated for the fp64 sizes of configs 2 and 4 and the fp32 sizes of configs 2, 4, 5
+bool cp3_sizes(bool f32, int nx, int nu) {
+    return (nx == 20 && nu == 8) || (nx == 32 && nu == 12) || (f32 && nx == 64 && nu == 16);
+}
+void launch_cp3(raocp_ctx* c) {
+    const int g = c->cp3_grid, C = c->unif_C, bx = c->box_mode, mL = c->cp3_mL;
+    if (c->f32) {
+        if (c->nx == 20) raocp::k_cp3<float, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
+        else if (c->nx == 32) raocp::k_cp3<float, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
+        else raocp::k_cp3<float, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
+    } else {
+        if (c->nx == 20) raocp::k_cp3<double, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
+        else raocp::k_cp3<double, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
+    }
+}
 // the solve's first half step Z[1] = prox-part(Z[0] - alpha L^T E[0]) (s_0 relaxation,
 // kernel projection): k_cp_primal; an fp32 context runs k_cpp2 on {p = z+ = Z[0], d = eta+ =
 // E[0]} (its residual partials are overwritten by iteration 0 before they are read)
@@ -614,6 +683,7 @@ bool fuse_check(const raocp_ctx* c) { return !c->comm && c->sh_R == 1 && !c->no_
 // z+_k = Z[k % 3] or eta+_k = E[k % 2]), and every later kernel exits on ctl->done, so the
 // result and the history are those of the eager test.
 bool defer_check(const raocp_ctx* c) {
+    if (c->dyn3 && c->sh_S == 0) return !(c->comm || c->sh_R != 1 || fuse_check(c) || c->no_defer_check || c->N < 1);
     if (c->comm || c->sh_R != 1 || fuse_check(c) || c->dyn2 || c->cut <= 0 || c->tiers.empty() || c->no_defer_check)
         return false;
     return c->tiers.back().nsub > 0;
@@ -647,11 +717,12 @@ int rccl_load() {
     return RAOCP_OK;
 }
 
-// The three exchanges of a sharded iteration:
+// The two exchanges of a sharded iteration:
 //   X2  after the tiers' backward sweeps: q rows of the boundary roots (all-gather);
 //   X1  after k_cpd: eta+ and xi2 of the roots' eta2 (all-gather), read by the
-//       replicated top families of k_cpp;
-//   X3  after k_cpp: the six residual maxima (+ the NaN-in-box flag), all-reduce max.
+//       replicated top families of k_cpp, carrying the previous iteration's 16-double
+//       residual record too (k_cp_reduce after k_cpp packs it; the stopping test runs one
+//       iteration late, k_cp_check_gather), so SURVEY.md's X3 all-reduce is not needed.
 // pack/unpack run on every shard; the collective itself is RCCL, or, for shards that
 // share a process (raocp_group_cp_run), host-driven copies between the phases.
 void shard_pack_x2(raocp_ctx* c) {
@@ -729,13 +800,54 @@ int enqueue_cp_iteration(raocp_ctx* c, int it) {
     const bool defer = defer_check(c);
     const raocp::ChkArg ck{c->ctl, c->hist, c->redpart, c->cp_rows, 1};
     launch_dynamics(c, c->bufs, 1, c->ctl, 0, defer && it > 0 ? &ck : nullptr);
-    launch_cpd(c);
-    const bool fuse = fuse_check(c);
-    launch_cpp(c, fuse);
+    const bool fuse = !c->cp3 && fuse_check(c);
+    if (c->cp3) {
+        launch_cp3(c);
+    } else {
+        launch_cpd(c);
+        launch_cpp(c, fuse);
+    }
     c->bufs = keep;
     if (!fuse && !defer) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
     return RAOCP_OK;
 }
+// the kernel the default selection launches for op (raocp_op_bench numbering: 0 L, 1 L^T,
+// 2 dual CP kernel, 6 primal CP kernel, 9 the dynamics projection), as rocprofv3 names it
+std::string kernel_name(const raocp_ctx* c, int op) {
+    const std::string T = c->f32 ? "float" : "double";
+    const bool exact = (c->nx == 20 && c->nu == 8) || (c->nx == 32 && c->nu == 12) || (c->nx == 64 && c->nu == 16) ||
+                       (c->nx == 3 && c->nu == 2);
+    const std::string nn = exact ? std::to_string(c->nx) + ", " + std::to_string(c->nu) : "0, 0";
+    const int rx = std::min(4, (c->nx + 15) / 16), ru = c->nu <= 16 ? 1 : 2;
+    const std::string rr = std::to_string(rx) + ", " + std::to_string(ru);
+    const bool big = (c->nx == 20 && c->nu == 8) || (c->nx == 32 && c->nu == 12) || (c->nx == 64 && c->nu == 16);
+    switch (op) {
+        case 0:
+            if (c->ell3 && big) return "k_ell3<" + T + ", " + nn + ">";
+            return c->f32 ? "k_ell2<float, " + rr + ">" : "k_ell<" + nn + ">";
+        case 1:
+            if (c->ellt3_C && big) return "k_ellt3<" + T + ", " + nn + ", " + std::to_string(4 / c->ellt3_C) + ">";
+            return c->f32 ? "k_ellt2<float, " + rr + ">" : "k_ell_t<" + nn + ">";
+        case 2:
+            if (!c->f32 && c->cp_v1) return "k_cpd<" + nn + ">";
+            return "k_cpd2<" + T + ", " + rr + ">";
+        case 6:
+            if (!c->f32 && c->cp_v1) return "k_cpp<" + nn + ">";
+            return "k_cpp2<" + T + ", " + rr + ">";
+        case 9:
+            if (c->dyn3 && c->sh_S == 0)
+                return "k_dy3_back<" + T + ", " + nn + "> + k_dy3_fwd<" + T + ", " + nn + "> (per stage)";
+            if (c->dyn2) return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
+            if (c->cut > 0)
+                return "k_dyn_bottom_back + k_dyn_top + k_dyn_bottom_fwd (" + std::to_string(c->tiers.size()) + " tiers)";
+            return "k_dyn_gather + k_dyn_stage_a / _b / _f (per stage)";
+        case 10:
+            if (c->cp3) return "k_cp3<" + T + ", " + nn + ">";
+            return kernel_name(c, 2) + " + " + kernel_name(c, 6);
+        default: return "";
+    }
+}
+
 // the end of a batch: the deferred test of its last iteration
 void enqueue_batch_tail(raocp_ctx* c) {
     if (defer_check(c)) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
@@ -1378,7 +1490,41 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         // stage, tiles of <= 16 nodes sharing a table (fp32 contexts; fp64 opt-in RAOCP_DYN2=1)
         c->dyn2 = c->f32;
         if (const char* e = getenv("RAOCP_DYN2")) c->dyn2 = c->dyn2 || atoi(e) != 0;
-        if (c->dyn2) {
+        {
+            // the per-stage streaming sweep (raocp_dyn3.hip): one branching factor C <= 4, the
+            // children's slot k of one kind at every parent of a stage, one class per stage, and
+            // the compile-time sizes
+            const int C = t->nch[0];
+            bool ok = C >= 1 && C <= 4 && ((nx == 20 && nu == 8) || (nx == 32 && nu == 12) || (nx == 64 && nu == 16));
+            for (int i = 0; i < m && ok; ++i)
+                if (t->nch[i] != C || t->ch_start[i] != 1 + C * i) ok = false;
+            std::vector<raocp::Dy3Stage> sts;
+            for (int st = 0; st < N && ok; ++st) {
+                raocp::Dy3Stage d{};
+                d.i0 = c->stage_ptr[st];
+                d.i1 = c->stage_ptr[st + 1];
+                d.leaf = st + 1 == N;
+                d.cls = pr->i_k[d.i0];
+                for (int k = 0; k < 4; ++k) {
+                    d.kind[k] = k < C ? kind[1 + C * d.i0 + k] : 0;
+                    d.pair[k] = k < C ? pair[1 + C * d.i0 + k] : 0;
+                }
+                for (int i = d.i0; i < d.i1 && ok; ++i) {
+                    if (pr->i_k[i] != d.cls) ok = false;
+                    for (int k = 0; k < C && ok; ++k)
+                        if (kind[1 + C * i + k] != d.kind[k] || pair[1 + C * i + k] != d.pair[k]) ok = false;
+                }
+                sts.push_back(d);
+            }
+            c->dyn3 = ok && c->f32;
+            if (const char* e = getenv("RAOCP_DYN3")) c->dyn3 = ok && atoi(e) != 0;
+            if (c->dyn3) {
+                c->d3st = sts;
+                c->dyn2 = false;
+                c->unif_branch = C;
+            }
+        }
+        if (c->dyn2 || c->dyn3) {
             const size_t nkd = std::max<size_t>(1, kinds.size()), npr = std::max<size_t>(1, pairs.size());
             std::vector<double> W2(nkd * R * nx, 0.0), RG2((size_t)std::max(1, nk) * R * nu, 0.0),
                 KM2((size_t)std::max(1, nk) * nu * nx, 0.0), F2(npr * nx * (nx + nu), 0.0);
@@ -1397,6 +1543,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             if ((rc = upload_t(c, &c->W2, W2)) || (rc = upload_t(c, &c->RG2, RG2)) || (rc = upload_t(c, &c->KM2, KM2)) ||
                 (rc = upload_t(c, &c->F2, F2)))
                 return bail(rc);
+        }
+        if (c->dyn3) {
+            if ((rc = c->alloc(&c->Q2, (size_t)n * nx)) || (rc = c->alloc(&c->Dd2, (size_t)m * nu))) return bail(rc);
+            c->dyn32 = c->f32;
+        }
+        if (c->dyn2) {
             std::vector<int> idx;
             std::vector<raocp::DynTile> tl;
             // nodes [a, b) grouped by table (stable), cut into tiles of <= 16
@@ -1900,7 +2052,16 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             for (int i = 0; i < m; ++i) nb += pr->i_box_nl[i] >= 0;
             for (int l = m; l < n; ++l) lb += pr->i_box_l[l] >= 0;
             c->box_mode = (nb == m ? 1 : nb == 0 ? 2 : 0) | ((lb == n - m ? 1 : lb == 0 ? 2 : 0) << 2);
-            if (const char* e = getenv("RAOCP_BOX_MODE")) c->box_mode = atoi(e);  // 0: always the tables
+            // RAOCP_BOX_MODE=0 forces the offset tables (always valid); any other value must
+            // agree with the computed pattern (a forced "all boxed" on a tree with unboxed nodes
+            // would compute eta7 / eta14 offsets for slots that do not exist)
+            if (const char* e = getenv("RAOCP_BOX_MODE")) {
+                const int v = atoi(e);
+                if (v != 0 && v != c->box_mode)
+                    return bail(fail(RAOCP_ERR_ARG, "RAOCP_BOX_MODE=" + std::to_string(v) + " disagrees with the tree's box "
+                                                    "pattern (" + std::to_string(c->box_mode) + "); only 0 may override"));
+                c->box_mode = v;
+            }
         }
         if (const char* e = getenv("RAOCP_ELLT3")) reg = reg && atoi(e) != 0;
         c->ellt3_C = reg ? C : 0;
@@ -1910,6 +2071,23 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         // vs 24.9 at 4,096, 28.0 at 1,024) and config 5 fp32 (109.4 vs 111.1 at 2,048)
         c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, 1536L));
         if (const char* e = getenv("RAOCP_ELLT3_GRID")) c->ellt3_grid = std::max(1, atoi(e));
+        // the fused CP iteration (raocp_cp3.hip): uniform branching and tables (unif_C), the
+        // compile-time sizes; RAOCP_CP3=0 keeps k_cpd* + k_cpp*
+        c->cp3 = c->unif_C > 0 && c->ell3 && cp3_sizes(c->f32, nx, nu);
+        if (const char* e = getenv("RAOCP_CP3")) c->cp3 = c->cp3 && atoi(e) != 0;
+        if (c->cp3) {
+            c->cp3_mL = c->stage_ptr[N - 1];
+            const long tiles = (long)(m - c->cp3_mL + 15) / 16 + (c->cp3_mL + 15) / 16;
+            c->cp3_grid = (int)std::max(1L, std::min((tiles + 3) / 4, 2048L));
+            if (const char* e = getenv("RAOCP_CP3_GRID")) c->cp3_grid = std::max(1, atoi(e));
+            if (c->cp3_grid > c->red_rows) {
+                c->red_rows = c->cp3_grid;
+                if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
+                if (hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)) != hipSuccess)
+                    return bail(fail(RAOCP_ERR_HIP, "memset"));
+            }
+            c->cp_rows = c->cp3_grid;
+        }
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels
     if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = atoi(e);
@@ -2004,6 +2182,25 @@ int raocp_get_dual(raocp_ctx* c, double* e, int flags) {
     return copy_out(c, e, c->cur_e, c->D, flags);
 }
 
+// the cold start of Solver.chock on a fresh Cache: primal and dual zero on the device
+int raocp_reset_iterate(raocp_ctx* c) {
+    DevGuard dg_(c);
+    if (!c) return fail(RAOCP_ERR_ARG, "null context");
+    HIPCHK(hipMemsetAsync(c->cur_z, 0, c->P * c->wsz, c->stream));
+    HIPCHK(hipMemsetAsync(c->cur_e, 0, c->D * c->wsz, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+
+int raocp_kernel_info(raocp_ctx* c, int op, char* buf, int cap) {
+    DevGuard dg_(c);
+    if (!c || !buf || cap < 1) return fail(RAOCP_ERR_ARG, "bad argument");
+    const std::string s = kernel_name(c, op);
+    if (s.empty()) return fail(RAOCP_ERR_ARG, "unknown op " + std::to_string(op));
+    snprintf(buf, (size_t)cap, "%s", s.c_str());
+    return RAOCP_OK;
+}
+
 int raocp_set_initial_state(raocp_ctx* c, const double* x0) {
     DevGuard dg_(c);
     if (!c || !x0) return fail(RAOCP_ERR_ARG, "null argument");
@@ -2030,23 +2227,11 @@ int raocp_relax_s0(raocp_ctx* c, double alpha) {
 
 int raocp_project_on_dynamics(raocp_ctx* c) {
     DevGuard dg_(c);
-    if (c && c->f32 && !c->dyn2) return fail(RAOCP_ERR_ARG, "fp32 context without a dynamics plan");
+    if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 context without a dynamics plan");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     if (!c->has_x0) return fail(RAOCP_ERR_STATE, "initial state not cached (call cache_initial_state first)");
     const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
-    const char* which = getenv("RAOCP_STAMP_KERNEL");
-    if (which && which[0] == 'p') {  // k_cpp on a valid control block (diagnostics)
-        std::vector<double> x0(c->nx, 0.0);
-        int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
-        if (rc2) return rc2;
-        launch_cpp(c);
-    } else if (which && which[0] == 'l') {  // k_ell on the staging buffers
-        launch_ell(c, c->tmpP, c->tmpD);
-    } else if (which && which[0] == 't') {  // k_ell_t
-        launch_ell_t(c, c->tmpD, c->tmpP);
-    } else {
-        launch_dynamics(c, solo, 0, nullptr);
-    }
+    launch_dynamics(c, solo, 0, nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
     return RAOCP_OK;
@@ -2389,6 +2574,7 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     c->sh_R = nranks;
     c->sh_r = rank;
     c->sh_S = S;
+    c->cp3 = false;  // a shard runs k_cpd* / k_cpp* on its owned blocks (build_cp_blocks sets cp_rows)
     std::vector<int> slc(2 * nranks);
     int xmax = 0;
     for (int r = 0; r < nranks; ++r) {
@@ -2565,8 +2751,8 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
     double* outD = c->E[1];
     // ops >= 2 time the CP kernels (or one role of them) on a valid control block
     if (op >= 2) {
-        if (c->f32 && (!c->dyn32 || (op != 2 && op != 6 && op != 9)))
-            return fail(RAOCP_ERR_ARG, "fp32 context: ops 0, 1, 2, 6 and 9 can be timed");
+        if (c->f32 && (!c->dyn32 || (op != 2 && op != 6 && op != 9 && op != 10)))
+            return fail(RAOCP_ERR_ARG, "fp32 context: ops 0, 1, 2, 6, 9 and 10 can be timed");
         if (int rh = ensure_hist(c, (size_t)reps + 16)) return rh;
         std::vector<double> x0(c->nx, 0.0);
         int rc = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
@@ -2583,6 +2769,14 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
             case 6: launch_cpp(c); break;
             case 7: case 8: launch_cp_primal(c, true, op - 6); break;
             case 9: launch_dynamics(c, c->bufs, 1, c->ctl); break;
+            case 10:  // the CP iteration's kernels after the dynamics
+                if (c->cp3) {
+                    launch_cp3(c);
+                } else {
+                    launch_cpd(c);
+                    launch_cpp(c);
+                }
+                break;
             default: raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
         }
     };
@@ -2614,6 +2808,69 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
     (void)hipEventDestroy(e1);
     if (gx) (void)hipGraphExecDestroy(gx);
     HIPCHK(hipGetLastError());
+    *ms_per_launch = ms / reps;
+    return RAOCP_OK;
+}
+
+// L (op 0) or L^T (op 1) with the launches cycling over `nsets` input / output buffer pairs:
+// with nsets (|P| + |D|) scalars beyond the 256 MiB Infinity Cache, every launch reads its
+// input from HBM (the repeated-buffer op_bench is L3-assisted once a working set fits)
+int raocp_op_bench_rot(raocp_ctx* c, int op, int reps, int nsets, float* ms_per_launch) {
+    DevGuard dg_(c);
+    if (!c || reps < 1 || nsets < 1 || nsets > 16 || !ms_per_launch || (op != 0 && op != 1))
+        return fail(RAOCP_ERR_ARG, "bad argument");
+    std::vector<double> hz(c->P), he(c->D);
+    std::mt19937_64 gen(1);
+    std::normal_distribution<double> nd(0.0, 1.0);
+    for (auto& v : hz) v = nd(gen);
+    for (auto& v : he) v = nd(gen);
+    int rci;
+    if ((rci = copy_in(c, c->tmpP, hz.data(), c->P, 0)) || (rci = copy_in(c, c->tmpD, he.data(), c->D, 0))) return rci;
+    std::vector<void*> mem;
+    auto release = [&]() {
+        for (void* q : mem) (void)hipFree(q);
+    };
+    std::vector<double*> P(nsets), D(nsets);
+    for (int k = 0; k < nsets; ++k) {
+        void* a = nullptr;
+        void* b = nullptr;
+        if (hipMalloc(&a, c->P * c->wsz + 64) != hipSuccess || (mem.push_back(a), hipMalloc(&b, c->D * c->wsz + 64)) != hipSuccess) {
+            release();
+            return fail(RAOCP_ERR_HIP, "hipMalloc (rotating buffer sets)");
+        }
+        mem.push_back(b);
+        P[k] = (double*)a;
+        D[k] = (double*)b;
+        (void)hipMemcpyAsync(P[k], c->tmpP, c->P * c->wsz, hipMemcpyDeviceToDevice, c->stream);
+        (void)hipMemcpyAsync(D[k], c->tmpD, c->D * c->wsz, hipMemcpyDeviceToDevice, c->stream);
+    }
+    auto run = [&](int i) {
+        const int k = i % nsets;
+        if (op == 0) launch_ell(c, P[k], D[k]);
+        else launch_ell_t(c, D[k], P[k]);
+    };
+    for (int i = 0; i < nsets; ++i) run(i);  // warm-up
+    hipGraphExec_t gx = nullptr;
+    hipGraph_t g = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    float ms = 0;
+    bool ok = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess;
+    if (ok) {
+        for (int i = 0; i < reps; ++i) run(i);
+        ok = hipStreamEndCapture(c->stream, &g) == hipSuccess && hipGraphInstantiate(&gx, g, nullptr, nullptr, 0) == hipSuccess;
+    }
+    if (g) (void)hipGraphDestroy(g);
+    ok = ok && hipGraphLaunch(gx, c->stream) == hipSuccess;  // warm-up replay
+    ok = ok && hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess;
+    ok = ok && hipEventRecord(e0, c->stream) == hipSuccess && hipGraphLaunch(gx, c->stream) == hipSuccess &&
+         hipEventRecord(e1, c->stream) == hipSuccess && hipEventSynchronize(e1) == hipSuccess &&
+         hipEventElapsedTime(&ms, e0, e1) == hipSuccess;
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (gx) (void)hipGraphExecDestroy(gx);
+    (void)hipStreamSynchronize(c->stream);
+    release();
+    if (!ok) return fail(RAOCP_ERR_HIP, std::string("op_bench_rot: ") + hipGetErrorString(hipGetLastError()));
     *ms_per_launch = ms / reps;
     return RAOCP_OK;
 }

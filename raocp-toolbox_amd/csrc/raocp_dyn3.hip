@@ -1,0 +1,199 @@
+// raocp_dyn3.hip — the dynamics projection (cache.py:259-288) stage by stage as streaming
+// MFMA wave tasks, for trees with one branching factor C <= 4 whose child slot k has the
+// same (A, B) pair at every parent of a stage and whose parents of a stage share one
+// offline class (host checks, raocp_capi.hip): the i.i.d. trees of configs 2, 4 and 5.
+// Included by raocp_kernels.hip after raocp_cp3.hip (the row layout, WL fragments, MFA).
+//
+// Device form (raocp_dyn.hip header):
+//   backward, stage t = N-1 .. 0, a tile of 16 parents i (lane lo = parent):
+//     h = sum_k B_k' q_j, a = sum_k A_k' q_j      (child j = 1 + C i + k; q_j = -x_j at leaves)
+//     v = u_i - h ;  d_i = Rinv v ;  q_i = (-x_i + a) + G v
+//   forward, stage t = 0 .. N-1 (x_0 = x0bar at stage 0):
+//     u_i = K x_i + d_i ;  x_j = Abar_k x_i + B_k d_i
+// One launch per stage and direction (the recursion is sequential in the stage); inside a
+// launch every product is a chain of 16x16x4 MFMAs in the transposed form of raocp_cp3.hip:
+// the children's products accumulate per parent in the MFMA accumulators, whose row layout
+// is directly the B operand of the parent's Rinv / G products. No LDS staging of vectors, no
+// barrier after the weight fill: a wave reads its parents' and children's rows with 16-B
+// loads straight into registers and writes its outputs from them.
+//
+// Weights: the stage's tables (slot k: B_k', A_k' backward, Abar_k, B_k forward; the class's
+// Rinv, G, K) are staged once per workgroup in LDS in fragment order (WLs below).
+
+// a fragment table taken from a column-major source with leading dimension ld, rows
+// [r0, r0 + R), columns [c0, c0 + K): lds[(ro KS + s) 64 + lane] = M[r][k] (transposed form)
+template <class T, int R, int K>
+struct WLs {
+    static constexpr int RO = (R + 15) / 16, RK = (K + 15) / 16, KS = 4 * RK, N = RO * KS * 64;
+    const __attribute__((address_space(3))) T* base;
+    __device__ __forceinline__ T get(int ro, int s) const { return base[(ro * KS + s) * 64 + (threadIdx.x & 63)]; }
+    static __device__ __forceinline__ void fill(__attribute__((address_space(3))) T* dst, const T* M, int ld, int r0,
+                                                int c0) {
+        for (int q = threadIdx.x; q < N; q += blockDim.x) {
+            const int l = q & 63, lo = l & 15, h = l >> 4, s = (q >> 6) % KS, ro = (q >> 6) / KS;
+            const int r = 16 * ro + MFA<T>::arow(lo), k = 16 * (s >> 2) + 4 * h + (s & 3);
+            dst[q] = (r < R && k < K) ? ((cglbp<T>)M)[(size_t)(c0 + k) * ld + r0 + r] : T(0);
+        }
+    }
+};
+template <class T, int R, int K>
+__device__ __forceinline__ void mmts(const WLs<T, R, K>& W, const T (&b)[(K + 15) / 16][4],
+                                     typename MF<T>::v4 (&acc)[(R + 15) / 16]) {
+    _Pragma("unroll") for (int s = 0; s < WLs<T, R, K>::KS; ++s)
+        _Pragma("unroll") for (int ro = 0; ro < WLs<T, R, K>::RO; ++ro)
+            acc[ro] = MF<T>::mma(W.get(ro, s), b[s >> 2][s & 3], acc[ro]);
+}
+
+// one stage of the sweep (host-built)
+struct Dy3Stage {
+    int i0, i1;   // parents of the stage
+    int leaf;     // the children are leaves (stage N - 1)
+    int cls;      // offline class of the stage's parents
+    int kind[4];  // child kind (A, B pair) of slot k
+    int pair[4];  // (kind, class) pair of slot k
+};
+
+template <class T, int NX, int NU>
+struct Dy3Lds {
+    typedef WLs<T, NU, NX> WB;  // B_k'
+    typedef WLs<T, NX, NX> WA;  // A_k' (backward) / Abar_k (forward)
+    typedef WLs<T, NU, NU> WRI; // Rinv
+    typedef WLs<T, NX, NU> WG;  // G (backward) / B_k (forward)
+    typedef WLs<T, NU, NX> WK;  // K
+    // LDS scalars of one stage's tables for C slots (host: dynamic shared bytes)
+    static constexpr __host__ __device__ int back_n(int C) { return C * (WB::N + WA::N) + WRI::N + WG::N; }
+    static constexpr __host__ __device__ int fwd_n(int C) { return WK::N + C * (WA::N + WG::N); }
+};
+
+// tables (column-major M[k R + r], raocp_capi.hip): W2[kind] = [B'; A'] (R = nu + nx rows,
+// nx columns), RG2[cls] = [Rinv; G] (R rows, nu columns), KM2[cls] = K (nu x nx),
+// F2[pair] = [Abar | B] (nx rows, nx + nu columns)
+template <class T, int NX, int NU>
+__global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__ ctl, ChkArg ck, double* __restrict__ z_,
+                                                  double* __restrict__ q_, double* __restrict__ d_, Dy3Stage st, int C,
+                                                  const double* __restrict__ W2, const double* __restrict__ RG2) {
+    typedef typename MF<T>::v4 v4;
+    typedef Dy3Lds<T, NX, NU> L;
+    constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16, R = NX + NU;
+    if (ck.on && blockIdx.x == gridDim.x - 1) {
+        // the previous CP iteration's stopping test (defer_check, raocp_capi.hip)
+        if (threadIdx.x < 64) cp_check_wave(ck);
+        return;
+    }
+    if (ctl && ctl->done) return;
+    extern __shared__ __attribute__((aligned(16))) double dsm_[];
+    typedef __attribute__((address_space(3))) T lT;
+    lT* wl = (lT*)dsm_;
+    const T* W = (const T*)W2 + 0;
+    for (int k = 0; k < C; ++k) {
+        L::WB::fill(wl + k * (L::WB::N + L::WA::N), W + (size_t)st.kind[k] * R * NX, R, 0, 0);
+        L::WA::fill(wl + k * (L::WB::N + L::WA::N) + L::WB::N, W + (size_t)st.kind[k] * R * NX, R, NU, 0);
+    }
+    lT* wr = wl + C * (L::WB::N + L::WA::N);
+    L::WRI::fill(wr, (const T*)RG2 + (size_t)st.cls * R * NU, R, 0, 0);
+    L::WG::fill(wr + L::WRI::N, (const T*)RG2 + (size_t)st.cls * R * NU, R, NU, 0);
+    __syncthreads();
+    const typename L::WRI wri{wr};
+    const typename L::WG wg{wr + L::WRI::N};
+    glbp<T> z = (glbp<T>)z_;
+    glbp<T> qb = (glbp<T>)q_;
+    glbp<T> db = (glbp<T>)d_;
+    const int lo = threadIdx.x & 15;
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int nw = (gridDim.x - ck.on) * (blockDim.x >> 6);
+    const int ntile = (st.i1 - st.i0 + 15) >> 4;
+    for (int task = gw; task < ntile; task += nw) {
+        const int i = st.i0 + 16 * task + lo;
+        const bool live = i < st.i1;
+        v4 ha[RU], aa[RX];
+        _Pragma("unroll") for (int r = 0; r < RU; ++r) ha[r] = v4{0, 0, 0, 0};
+        _Pragma("unroll") for (int r = 0; r < RX; ++r) aa[r] = v4{0, 0, 0, 0};
+        for (int k = 0; k < C; ++k) {
+            const int j = 1 + C * (live ? i : st.i0) + k;
+            T qj[RX][4];
+            if (st.leaf) {
+                ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)j * NX, live, qj);
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) qj[rt][e] = -qj[rt][e];
+            } else {
+                ld_rows<T, NX>((cglbp<T>)qb + (size_t)j * NX, live, qj);
+            }
+            const typename L::WB wb{wl + k * (L::WB::N + L::WA::N)};
+            const typename L::WA wa{wl + k * (L::WB::N + L::WA::N) + L::WB::N};
+            mmts(wb, qj, ha);
+            mmts(wa, qj, aa);
+        }
+        T u[RU][4], x[RX][4], v[RU][4];
+        ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)i * NU, live, u);
+        ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) v[rt][e] = u[rt][e] - ha[rt][e];
+        v4 dv[RU], gv[RX];
+        _Pragma("unroll") for (int r = 0; r < RU; ++r) dv[r] = v4{0, 0, 0, 0};
+        _Pragma("unroll") for (int r = 0; r < RX; ++r) gv[r] = v4{0, 0, 0, 0};
+        mmts(wri, v, dv);
+        mmts(wg, v, gv);
+        T dd[RU][4], qq[RX][4];
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) dd[rt][e] = dv[rt][e];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+            qq[rt][e] = (-x[rt][e] + aa[rt][e]) + gv[rt][e];
+        st_rows<T, NU>(db + (size_t)i * NU, live, dd);
+        st_rows<T, NX>(qb + (size_t)i * NX, live, qq);
+    }
+}
+
+template <class T, int NX, int NU>
+__global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ ctl, double* __restrict__ z_,
+                                                 const double* __restrict__ d_, const double* __restrict__ x0_, Dy3Stage st,
+                                                 int C, const double* __restrict__ KM2, const double* __restrict__ F2) {
+    typedef typename MF<T>::v4 v4;
+    typedef Dy3Lds<T, NX, NU> L;
+    constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
+    if (ctl && ctl->done) return;
+    extern __shared__ __attribute__((aligned(16))) double dsm_[];
+    typedef __attribute__((address_space(3))) T lT;
+    lT* wl = (lT*)dsm_;
+    L::WK::fill(wl, (const T*)KM2 + (size_t)st.cls * NU * NX, NU, 0, 0);
+    lT* wf = wl + L::WK::N;
+    for (int k = 0; k < C; ++k) {
+        const T* F = (const T*)F2 + (size_t)st.pair[k] * NX * (NX + NU);
+        L::WA::fill(wf + k * (L::WA::N + L::WG::N), F, NX, 0, 0);                 // Abar_k
+        L::WG::fill(wf + k * (L::WA::N + L::WG::N) + L::WA::N, F, NX, 0, NX);    // B_k
+    }
+    __syncthreads();
+    const typename L::WK wk{wl};
+    glbp<T> z = (glbp<T>)z_;
+    cglbp<T> db = (cglbp<T>)d_;
+    const int lo = threadIdx.x & 15;
+    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
+    const int ntile = (st.i1 - st.i0 + 15) >> 4;
+    for (int task = gw; task < ntile; task += nw) {
+        const int i = st.i0 + 16 * task + lo;
+        const bool live = i < st.i1;
+        T x[RX][4], d[RU][4];
+        if (i == 0) {
+            // x_0 = x0bar (cache.py:283), written into the iterate too
+            ld_rows<T, NX>((cglbp<T>)x0_, true, x);
+            st_rows<T, NX>(z + p.X0, true, x);
+        } else {
+            ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+        }
+        ld_rows<T, NU>(db + (size_t)i * NU, live, d);
+        v4 ku[RU];
+        _Pragma("unroll") for (int r = 0; r < RU; ++r) ku[r] = v4{0, 0, 0, 0};
+        mmts(wk, x, ku);
+        T u[RU][4];
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) u[rt][e] = ku[rt][e] + d[rt][e];
+        st_rows<T, NU>(z + p.U0 + (size_t)i * NU, live, u);
+        for (int k = 0; k < C; ++k) {
+            const int j = 1 + C * (live ? i : st.i0) + k;
+            const typename L::WA wa{wf + k * (L::WA::N + L::WG::N)};
+            const typename L::WG wb{wf + k * (L::WA::N + L::WG::N) + L::WA::N};
+            v4 xa[RX];
+            _Pragma("unroll") for (int r = 0; r < RX; ++r) xa[r] = v4{0, 0, 0, 0};
+            mmts(wa, x, xa);
+            mmts(wb, d, xa);
+            T xj[RX][4];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) xj[rt][e] = xa[rt][e];
+            st_rows<T, NX>(z + p.X0 + (size_t)j * NX, live, xj);
+        }
+    }
+}

@@ -200,17 +200,16 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
             _Pragma("unroll") for (int k = 0; k < (NU + 3) / 4; ++k) au[k] = au2[k];
         }
     } else {
-    // child tiles: loads of the wave's next tile are issued before the current tile's MFMAs
-    // and stores (vmcnt is in order: loads issued after a store would wait for it)
+    // child tiles (branching not uniform, C == 0): each child reads its ancestor's rows
+    // through its record; eta7 comes from the flat tasks (fbeg = 0). Loads of the wave's
+    // next tile are issued before the current tile's MFMAs and stores (vmcnt is in order:
+    // loads issued after a store would wait for it)
         int task = gw;
         auto fetch = [&](int tk, Rec& cr, T (&ax)[(NX + 3) / 4], T (&au)[(NU + 3) / 4]) {
             const int ja = 1 + 16 * tk + lo;
             const bool la = tk < Tc && ja < n;
-            // uniform branching C (host-checked BFS): the ancestor without a dependent record
-            // load, and w = the parent's eta7 offset on its first child (-1: none / C = 0)
             if (!la) cr = Rec{0, -1, -1, -1};
-            else if (C) cr = Rec{(ja - 1) / C, 0, 0, (ja - 1) % C == 0 ? o7_of<NX, NU>(p, (ja - 1) / C, bx) : -1};
-            else { cr = p.crec[ja]; cr.w = -1; }
+            else cr = p.crec[ja];
             load_arow<T, NX>(la ? z + p.X0 + (size_t)cr.x * nx : nullptr, ax);
             load_arow<T, NU>(la ? z + p.U0 + (size_t)cr.x * nu : nullptr, au);
         };
@@ -218,10 +217,9 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
         T ax[(NX + 3) / 4], au[(NU + 3) / 4];
         if (task < Tc) {
             fetch(task, cr, ax, au);
-            const int tq = C ? p.crec[1].y : __builtin_amdgcn_readfirstlane(cr.y);
-            const int tr = C ? p.crec[1].z : __builtin_amdgcn_readfirstlane(cr.z);
-            wq.load((const T*)p.SQ, tq);  // one table over the tiles (host check)
-            wr.load((const T*)p.SR, tr);
+            // one table over the tiles (host check); lane 0's record is a live child
+            wq.load((const T*)p.SQ, __builtin_amdgcn_readfirstlane(cr.y));
+            wr.load((const T*)p.SR, __builtin_amdgcn_readfirstlane(cr.z));
         }
         for (; task < Tc; task += nwv) {
             const int j0 = 1 + 16 * task;
@@ -241,15 +239,6 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
             if (lane < 2 * cnt) {
                 const int j = j0 + (lane >> 1);
                 eg[((lane & 1) ? p.E6 : p.E5) + j] = T(0.5) * tv;
-            }
-            if (cr.w >= 0) {
-                // eta7_i = [x_i; u_i] of a boxed parent, from its first child's A registers
-                // (lane (lo, h) holds entries KC h .. KC h + KC of the row)
-                constexpr int KX = (NX + 3) / 4, KU = (NU + 3) / 4;
-                _Pragma("unroll") for (int k = 0; k < KX; ++k)
-                    if (KX * h + k < nx) eg[cr.w + KX * h + k] = ax[k];
-                _Pragma("unroll") for (int k = 0; k < KU; ++k)
-                    if (KU * h + k < nu) eg[cr.w + nx + KU * h + k] = au[k];
             }
             cr = cr2;
             _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];

@@ -908,6 +908,8 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
 #include "raocp_cp2.hip"
 #include "raocp_ell2.hip"
 #include "raocp_ell3.hip"
+#include "raocp_cp3.hip"
+#include "raocp_dyn3.hip"
 #include "raocp_dyn2.hip"
 
 // ---- element-wise dual sub-steps of prox_g* (cache.py:329-347, 392-393)

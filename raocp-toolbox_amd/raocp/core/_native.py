@@ -27,6 +27,7 @@ EXPORTED_SYMBOLS = [
     "raocp_dual_scale", "raocp_dual_add_halves", "raocp_dual_project", "raocp_dual_moreau",
     "raocp_device_synchronize", "raocp_debug_dyn_stamps",
     "raocp_shard_setup", "raocp_shard_owned", "raocp_comm_unique_id", "raocp_comm_init", "raocp_group_cp_run",
+    "raocp_reset_iterate", "raocp_kernel_info", "raocp_op_bench_rot",
 ]
 
 _i32p = ctypes.POINTER(ctypes.c_int32)
@@ -83,6 +84,8 @@ def load_library():
         "raocp_set_dual": (c_int, [vp, vp, c_int]),
         "raocp_get_dual": (c_int, [vp, vp, c_int]),
         "raocp_set_initial_state": (c_int, [vp, vp]),
+        "raocp_reset_iterate": (c_int, [vp]),
+        "raocp_kernel_info": (c_int, [vp, c_int, ctypes.c_char_p, c_int]),
         "raocp_prox_f": (c_int, [vp, c_double]),
         "raocp_relax_s0": (c_int, [vp, c_double]),
         "raocp_project_on_dynamics": (c_int, [vp]),
@@ -94,6 +97,7 @@ def load_library():
         "raocp_cp_prepare": (c_int, [vp, vp, c_int, c_double]),
         "raocp_cp_bench": (c_int, [vp, vp, c_int, c_double, ctypes.POINTER(ctypes.c_float)]),
         "raocp_op_bench": (c_int, [vp, c_int, c_int, ctypes.POINTER(ctypes.c_float)]),
+        "raocp_op_bench_rot": (c_int, [vp, c_int, c_int, c_int, ctypes.POINTER(ctypes.c_float)]),
         "raocp_dual_scale": (c_int, [vp, c_double]),
         "raocp_dual_add_halves": (c_int, [vp]),
         "raocp_dual_project": (c_int, [vp, c_int]),
@@ -258,6 +262,17 @@ class NativeContext:
         self._check(self._lib.raocp_get_dual(self._h, _ptr(out), 0))
         return out
 
+    def reset_iterate(self):
+        """Zero the current primal / dual on the device (a fresh Cache's iterate)."""
+        self._check(self._lib.raocp_reset_iterate(self._h))
+
+    def kernel_info(self, op):
+        """rocprofv3 name of the kernel the default selection launches for op (raocp_op_bench
+        numbering: 0 L, 1 L^T, 2 / 6 the dual / primal CP kernels, 9 dynamics, 10 fused CP)."""
+        buf = ctypes.create_string_buffer(256)
+        self._check(self._lib.raocp_kernel_info(self._h, int(op), buf, 256))
+        return buf.value.decode()
+
     def set_initial_state(self, x0):
         x0 = self._vec(x0, self._packed.nx)
         self._check(self._lib.raocp_set_initial_state(self._h, _ptr(x0)))
@@ -305,8 +320,7 @@ class NativeContext:
         self._require_l()
         x0 = self._vec(x0, self._packed.nx)
         if not warm:
-            self.set_primal(np.zeros(self.P))
-            self.set_dual(np.zeros(self.D))
+            self.reset_iterate()
         err = np.zeros((max_iters + 1, 3))
         derr = np.zeros((max_iters + 1, 3))
         status, iters = ctypes.c_int(), ctypes.c_int()
@@ -357,4 +371,10 @@ class NativeContext:
     def op_bench(self, op, reps):
         ms = ctypes.c_float()
         self._check(self._lib.raocp_op_bench(self._h, int(op), int(reps), ctypes.byref(ms)))
+        return ms.value
+
+    def op_bench_rot(self, op, reps, nsets):
+        """L (0) / L^T (1) cycling over nsets buffer pairs (HBM-honest beyond 256 MiB)."""
+        ms = ctypes.c_float()
+        self._check(self._lib.raocp_op_bench_rot(self._h, int(op), int(reps), int(nsets), ctypes.byref(ms)))
         return ms.value

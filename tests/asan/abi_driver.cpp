@@ -150,6 +150,14 @@ static void gpu_checks() {
         CHECK(raocp_cp_bench(c, nullptr, 29, alpha, &ms) == RAOCP_OK);
         CHECK(raocp_cp_bench(c, nullptr, 29, alpha, &ms) == RAOCP_ERR_STATE);  // consumed
         CHECK(raocp_op_bench(c, 0, 10, &ms) == RAOCP_OK);
+        CHECK(raocp_op_bench_rot(c, 1, 6, 3, &ms) == RAOCP_OK && ms > 0);
+        CHECK(raocp_op_bench_rot(c, 2, 6, 3, &ms) == RAOCP_ERR_ARG);
+        char kn[128];
+        for (int op : {0, 1, 2, 6, 9, 10}) CHECK(raocp_kernel_info(c, op, kn, (int)sizeof(kn)) == RAOCP_OK && kn[0]);
+        CHECK(raocp_kernel_info(c, 5, kn, (int)sizeof(kn)) == RAOCP_ERR_ARG);
+        CHECK(raocp_reset_iterate(c) == RAOCP_OK);
+        CHECK(raocp_get_primal(c, z2.data(), 0) == RAOCP_OK);
+        for (int64_t i = 0; i < P; ++i) CHECK(z2[i] == 0.0);
         raocp_ctx_destroy(c);
     }
     // sharding: 2 shards in one process, device copies as the transport

@@ -15,14 +15,6 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
 
 
-def gpu_available():
-    try:
-        import torch  # noqa: F401  (device count only; does not initialise HIP on this image)
-        return torch.cuda.device_count() > 0
-    except Exception:
-        return os.path.exists("/dev/kfd")
-
-
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

@@ -6,6 +6,7 @@ This script is the only place that imports the reference. It runs here only
 fixtures the test-suite and the oracle are pinned against.
 
     python -B tests/golden/gen_golden.py            # writes tests/golden/*.npz
+    python -B tests/golden/gen_golden.py warm       # only warm_start.npz
 
 The reference needs `turtle` (tkinter) and `tikzplotlib`, both absent here:
 they are stubbed as empty modules (scenario_tree.py:4, solver.py:8 import them
@@ -327,6 +328,42 @@ def run_chock(name, r, max_iters, tol, out, pin_lambda=None):
           f"lambda={lam!r}")
 
 
+def gen_warm(out):
+    """Two chock calls on ONE reference Solver (main.py's problem): the second continues from
+    the cached primal / dual of the first with a new initial state written into node 0's
+    state (solver.py:97-102 with cache.py:79-82). Both traces, step sizes and iterates."""
+    r = recipe_main()
+    tree, prob = build_ref(r)
+    solver = core.Solver(problem_spec=prob)
+    orig = ref_solver.eigs
+    lams = []
+
+    def eigs_capture(op, *a, **k):
+        vals, _ = orig(op, *a, **k)
+        lams.append(float(np.real(max(vals))))
+        return vals, None
+
+    ref_solver.eigs = eigs_capture
+    out.update(recipe_arrays("warm", r))
+    out.update(tree_arrays("warm", tree))
+    try:
+        for call, (x0, iters) in enumerate(((r["x0"], 60), (r["x0"] / 2, 40))):
+            status = solver.chock(initial_state=x0.reshape(-1, 1), max_iters=iters, tol=0.0)
+            cache = solver._Solver__cache
+            z, _ = cache.get_primal()
+            e, _ = cache.get_dual()
+            out.update({f"warm/call{call}/x0": x0, f"warm/call{call}/max_iters": np.array(iters),
+                        f"warm/call{call}/status": np.array(status), f"warm/call{call}/lambda": np.array(lams[-1]),
+                        f"warm/call{call}/alpha": np.array(0.999 / lams[-1]),
+                        f"warm/call{call}/error": np.atleast_2d(solver._Solver__error_cache),
+                        f"warm/call{call}/delta_error": np.atleast_2d(solver._Solver__delta_error_cache),
+                        f"warm/call{call}/z": flat(z), f"warm/call{call}/eta": flat(e)})
+            print(f"warm call {call}: status={status} rows={np.atleast_2d(solver._Solver__error_cache).shape[0]} "
+                  f"lambda={lams[-1]!r}")
+    finally:
+        ref_solver.eigs = orig
+
+
 def gen_trees(out):
     rng = np.random.default_rng(5)
     p3 = np.array([[0.1, 0.8, 0.1], [0.4, 0.6, 0], [0, 0.3, 0.7]])
@@ -361,6 +398,11 @@ def gen_trees(out):
 
 def main():
     np.random.seed(12345)  # ARPACK start vectors come from numpy's global RNG inside scipy
+    if sys.argv[1:] == ["warm"]:  # only the warm-start fixture (added in round 3)
+        w = {}
+        gen_warm(w)
+        np.savez_compressed(os.path.join(OUT, "warm_start.npz"), **w)
+        return
     ops = {}
     gen_ops(ops)
     np.savez_compressed(os.path.join(OUT, "ops_kat.npz"), **ops)

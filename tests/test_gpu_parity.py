@@ -48,11 +48,15 @@ def dyn_engine(mode):
     return _env("RAOCP_DYN_PER_STAGE", "1" if mode == "per_stage" else "0")
 
 
+@contextlib.contextmanager
 def cp_kernels(mode):
-    """Contexts created inside use the CP kernels the library picks for the tree ("auto":
-    scalar below ~4k node tiles, MFMA above), the MFMA kernels (raocp_cp2.hip) or the
-    scalar ones (raocp_cp.hip)."""
-    return _env("RAOCP_CP_V1", {"auto": None, "mfma": "0", "scalar": "1"}[mode])
+    """Contexts created inside use the CP kernels the library picks for the tree ("auto": the
+    fused streaming k_cp3 on uniform trees of the benchmark sizes, else scalar below ~4k node
+    tiles and MFMA above), the two-launch MFMA kernels (raocp_cp2.hip) or the scalar ones
+    (raocp_cp.hip)."""
+    with _env("RAOCP_CP_V1", {"auto": None, "mfma": "0", "scalar": "1"}[mode]), \
+            _env("RAOCP_CP3", None if mode == "auto" else "0"):
+        yield
 
 
 @pytest.fixture(scope="module")
@@ -380,6 +384,24 @@ def test_large_cp_trace_vs_oracle(cfg, cpk):
     cache.set_dual_flat(ee)
     cache.proximal_of_g_conjugate(0.3)
     assert rel_err(cache.get_dual_flat(), orc.prox_gconj(ee, 0.3)) <= 1e-12
+
+
+def test_chock_warm_start_matches_reference_fixture(golden):
+    """The reference's own second Solver.chock on one solver (tests/golden/warm_start.npz,
+    generated by tests/golden/gen_golden.py gen_warm): 60 iterations from x0, then 40 from
+    x0 / 2 continuing from the cached primal / dual (solver.py:97-102, cache.py:79-82)."""
+    z = golden("warm_start")
+    r, tree, prob = problem_from_golden(z, "warm")
+    s = core.Solver(problem_spec=prob)
+    for call in (0, 1):
+        key = f"warm/call{call}/"
+        st = s.chock(z[key + "x0"].reshape(-1, 1), max_iters=int(z[key + "max_iters"]), tol=0.0,
+                     step_size=float(z[key + "alpha"]))
+        assert st == int(z[key + "status"])
+        assert trace_rel_err(s.error_cache, z[key + "error"]) <= 1e-8
+        assert trace_rel_err(s.delta_error_cache, z[key + "delta_error"]) <= 1e-8
+        assert rel_err(s.cache.get_primal_flat(), z[key + "z"]) <= 1e-9
+        assert rel_err(s.cache.get_dual_flat(), z[key + "eta"]) <= 1e-9
 
 
 def test_chock_warm_starts_like_reference(golden):

@@ -5,9 +5,15 @@ device of the test box and exchange through device copies (raocp_group_cp_run); 
 multi-GPU transport is RCCL with the same packing (bench.py --shard).
 
 Parity: the residual histories and the owned parts of the final iterate equal those of
-the unsharded solve (the per-node arithmetic is identical; only max reductions are
-regrouped, which is exact), and match the oracle within the north_star tolerance.
+the unsharded solve with the same kernels (a shard runs k_cpd* / k_cpp*, so the unsharded
+reference run sets RAOCP_CP3=0; the per-node arithmetic is identical and only max
+reductions are regrouped, which is exact), stay within 1e-10 of the default fused
+unsharded solve (k_cp3: other summation order) and match the oracle within the
+north_star tolerance. Configs 2 (the headline tree) and 4 (the tree the sharded bench leg
+runs, BASELINE configs[3]) at R = 2, 4, 8.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -29,20 +35,56 @@ def c2():
     return _cache(2)
 
 
+def _two_launch_cache(prob):
+    """An unsharded context on the kernels a shard runs (k_cpd* / k_cpp*, not k_cp3)."""
+    old = os.environ.get("RAOCP_CP3")
+    os.environ["RAOCP_CP3"] = "0"
+    try:
+        return core.Cache(prob)
+    finally:
+        if old is None:
+            os.environ.pop("RAOCP_CP3", None)
+        else:
+            os.environ["RAOCP_CP3"] = old
+
+
+_ORACLE = {}
+
+
+def _oracle_run(cfg, prob, x0, iters, alpha):
+    from oracle.raocp_oracle import OracleProblem
+    key = (cfg, iters, alpha)
+    if key not in _ORACLE:
+        _ORACLE[key] = OracleProblem(prob).chock(x0, iters, 0.0, alpha=alpha)
+    return _ORACLE[key]
+
+
 def _owned_x_slices(ctx):
     lo, hi = ctx.shard_owned()
     return [(int(a), int(b)) for a, b in zip(lo, hi)]
 
 
+_CFG = {}
+
+
+@pytest.mark.parametrize("cfg", [2, 4])
 @pytest.mark.parametrize("R", [2, 4, 8])
-def test_sharded_solve_matches_unsharded(c2, R):
-    r, tree, prob = c2
-    base = core.Cache(prob)
+def test_sharded_solve_matches_unsharded(cfg, R):
+    if cfg not in _CFG:
+        _CFG[cfg] = _cache(cfg)
+    r, tree, prob = _CFG[cfg]
+    base = _two_launch_cache(prob)
     lam = base.native.step_size()
     alpha = 0.999 / lam
-    iters = 40
+    iters = 40 if cfg == 2 else 12
     st0, err0, derr0 = base.native.cp_run(r["x0"], iters, 0.0, alpha)
     z0 = base.get_primal_flat()
+    fused = core.Cache(prob)
+    stf, errf, _ = fused.native.cp_run(r["x0"], iters, 0.0, alpha)
+    assert stf == st0 and np.max(np.abs(errf - err0) / np.abs(err0)) <= 1e-10
+    st_o, err_o, _, z_o, _, _ = _oracle_run(cfg, prob, r["x0"], iters, alpha)
+    assert np.max(np.abs(err0 - err_o) / np.abs(err_o)) <= 1e-8
+    assert np.max(np.abs(z0 - z_o)) <= 1e-10 * np.max(np.abs(z_o))
     shards = [core.Cache(prob) for _ in range(R)]
     for k, s in enumerate(shards):
         s.native.shard(k, R)
@@ -65,7 +107,7 @@ def test_sharded_stopping_and_status(c2):
     """The stopping test sees the all-reduced residuals: every shard stops together at
     the same iteration as the unsharded solve (tolerance reached before max_iters)."""
     r, tree, prob = c2
-    base = core.Cache(prob)
+    base = _two_launch_cache(prob)
     alpha = 0.999 / base.native.step_size()
     st0, err0, _ = base.native.cp_run(r["x0"], 400, 5e-2, alpha)
     shards = [core.Cache(prob) for _ in range(2)]

@@ -127,20 +127,26 @@ def test_ell_t_parent_tiles_bit_identical_to_staged(cfg):
     assert rel_err(a, OracleProblem(prob).ell_t(ee)) <= 1e-12
 
 
-@pytest.mark.parametrize("cfg", ["chain", 2, "2-nobox", "2-leafbox", 4, "4-c2"])
+@pytest.mark.parametrize("cfg", ["chain", 2, "2-nobox", "2-leafbox", 4, "4-c2", "stop", "stop-nobox"])
 def test_ell_t_streaming_vs_block_and_oracle(cfg):
     """k_ellt3 (streaming wave tasks, uniform tables and branching C <= 4; raocp_ell3.hip)
     against k_ell_t (RAOCP_ELLT3=0) and the oracle (operators.py:55-94) on random duals:
     a chain (C = 1), config 2 (C = 2) with all, no and leaf-only boxes (eta7 / eta14 terms),
     config 4 (C = 3, nx = 32) and a binary tree at nx = 32. The same for L (k_ell3 against
     k_ell, operators.py:19-53), and both with the eta7 / eta14 offsets read from the tables
-    (RAOCP_BOX_MODE=0) instead of computed from the all / none box patterns."""
+    (RAOCP_BOX_MODE=0) instead of computed from the all / none box patterns. "stop": a binary
+    tree whose stopping time (4) is below the horizon (10), so the branching is not uniform:
+    k_ell3 takes its child-tile branch (eta7 from the flat tasks) and L^T runs k_ell_t."""
     from oracle.raocp_oracle import OracleProblem
     from raocp.problems import recipe_synthetic
     if cfg == "chain":
         r = recipe_synthetic(np.ones((1, 1)), np.ones(1), 40, 40, 20, 8, seed=3)
     elif cfg == "4-c2":
         r = recipe_synthetic(np.full((2, 2), .5), np.full(2, .5), 9, 9, 32, 12, seed=4)
+    elif cfg in ("stop", "stop-nobox"):
+        r = recipe_synthetic(np.full((2, 2), .5), np.full(2, .5), 10, 4, 20, 8, seed=5)
+        if cfg == "stop-nobox":
+            r["nl_min"] = r["nl_max"] = None
     elif cfg in ("2-nobox", "2-leafbox"):
         r = recipe_config(2)
         r["nl_min"] = r["nl_max"] = None

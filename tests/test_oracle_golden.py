@@ -165,3 +165,22 @@ def test_oracle_chock_status_contract(golden):
     assert st == 1 and err.shape[0] == n_it
     st, err, _, _, _, _ = orc.chock(r["x0"], 0, 0.0, alpha=alpha)
     assert st == 1 and err.shape[0] == 1
+
+
+def test_oracle_warm_start_matches_reference(golden):
+    """Two chock calls on one reference Solver (tests/golden/gen_golden.py gen_warm): the
+    second continues from the first one's cached primal / dual with x0 / 2 written into
+    node 0's state (solver.py:97-102, cache.py:79-82). The oracle's p0 / d0 path reproduces
+    both calls' traces and iterates."""
+    z = golden("warm_start")
+    r, tree, prob = problem_from_golden(z, "warm")
+    orc = OracleProblem(prob)
+    p0 = d0 = None
+    for call in (0, 1):
+        key = f"warm/call{call}/"
+        st, err, derr, p0, d0, _ = orc.chock(z[key + "x0"], int(z[key + "max_iters"]), 0.0,
+                                             alpha=float(z[key + "alpha"]), p0=p0, d0=d0)
+        assert st == int(z[key + "status"])
+        assert trace_rel_err(err, z[key + "error"]) <= 1e-9
+        assert trace_rel_err(derr, z[key + "delta_error"]) <= 1e-9
+        assert rel_err(p0, z[key + "z"]) <= 1e-10 and rel_err(d0, z[key + "eta"]) <= 1e-10

@@ -1,0 +1,33 @@
+"""Per-launch device time of the CP iteration's kernels after the dynamics sweep (op_bench 10:
+k_cp3, or k_cpd* + k_cpp* with RAOCP_CP3=0), the dynamics projection (op 9) and the CP loop
+(cp_bench) at configs 2, 4 (fp64) and 5 (fp32). python tools/cp3_time.py [configs...]"""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if len(sys.argv) > 1 and sys.argv[1] == "child":
+    sys.path[:0] = [os.path.join(ROOT, "raocp-toolbox_amd"), ROOT]
+    import raocp.core as core
+    from raocp.problems import build_problem, recipe_config
+    cfg = int(sys.argv[2])
+    r = recipe_config(cfg)
+    c = core.Cache(build_problem(r)[1], dtype="float32" if cfg == 5 else "float64")
+    nat = c.native
+    reps = {2: 400, 4: 100, 5: 20}[cfg]
+    t10 = nat.op_bench(10, reps)
+    t9 = nat.op_bench(9, max(1, reps // 2))
+    alpha = 0.999 / nat.step_size(rtol=1e-7 if cfg == 5 else 1e-14)
+    K = {2: 480, 4: 120, 5: 24}[cfg]
+    ms = nat.cp_bench(r["x0"], K, alpha)
+    var = ",".join(f"{k[6:]}={os.environ[k]}" for k in ("RAOCP_CP3", "RAOCP_DYN3") if k in os.environ) or "default"
+    print(f"config {cfg} {var:8s} {nat.kernel_info(10):40s} {nat.kernel_info(9)[:34]:34s} "
+          f"cp {1e3 * t10:8.1f} us  dyn {1e3 * t9:8.1f} us  loop {1e3 * ms / K:8.1f} us/it", flush=True)
+    sys.exit(0)
+cfgs = sys.argv[1:] or ["2", "4", "5"]
+for cfg in cfgs:
+    for v in ({}, {"RAOCP_CP3": "0"}) + (({"RAOCP_DYN3": "1"},) if cfg != "5" else ({"RAOCP_DYN3": "0"},)):
+        env = dict(os.environ, **v)
+        out = subprocess.run([sys.executable, __file__, "child", cfg], env=env, capture_output=True, text=True,
+                             timeout=300)
+        print(out.stdout.strip() or out.stderr.strip()[-400:], flush=True)

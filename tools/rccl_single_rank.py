@@ -3,6 +3,7 @@ RCCL all-gathers / all-reduce, graph-captured, must reproduce the unsharded solv
 Run as its own process: torch must not be imported (see bench.py SocketGroup)."""
 import os, sys
 os.environ["RAOCP_SHARD_FORCE"] = "1"
+os.environ["RAOCP_CP3"] = "0"  # a shard runs k_cpd* / k_cpp*: compare with the same kernels unsharded
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raocp-toolbox_amd"))
 import numpy as np
 import raocp.core as core
