@@ -59,6 +59,7 @@ struct raocp_ctx {
     bool cp3 = false;            // the CP iteration after the dynamics as one streaming kernel (raocp_cp3.hip)
     int cp3_grid = 0;
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
+    int cp3_split = 0;           // leaves as tasks of their own (small trees: more waves, shorter chains)
     // per-stage MFMA dynamics (raocp_dyn2.hip): tables, node lists, tile lists per stage
     bool dyn2 = false;           // fp32 contexts always; fp64 opt-in RAOCP_DYN2=1
     const double *W2 = nullptr, *RG2 = nullptr, *KM2 = nullptr, *F2 = nullptr;
@@ -70,6 +71,7 @@ struct raocp_ctx {
     // class per stage; fp32 contexts by default, fp64 opt-in RAOCP_DYN3=1
     bool dyn3 = false;
     std::vector<raocp::Dy3Stage> d3st;
+    std::vector<raocp::Dy3Stage> d3own;  // a shard's stages (owned parent ranges below its cut)
     int wsz = 8;                 // bytes per scalar of the iterate
     hipStream_t stream = nullptr;
     Dev dev{};
@@ -401,41 +403,58 @@ struct Dyn2Op {
 
 // the per-stage streaming sweep (raocp_dyn3.hip) on z; ck: the previous iteration's stopping
 // test in an extra workgroup of the first launch (defer_check)
+// part: 0 the whole projection; 1 (a shard) the backward stages below its cut, on its owned
+// parents; 2 the replicated top backward, then every forward stage (owned below the cut)
 template <class T, int NX, int NU>
-void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck) {
+void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck, int part) {
     typedef raocp::Dy3Lds<T, NX, NU> L;
     const int C = c->unif_branch;
-    const size_t lb = (size_t)L::back_n(C) * sizeof(T), lf = (size_t)L::fwd_n(C) * sizeof(T);
+    constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
+    // LDS: the stage's tables; the backward kernel's slot sums of a cooperative tile after them
+    const size_t lb = (size_t)(L::back_n(C) + C * (RU + RX) * 4 * 64) * sizeof(T), lf = (size_t)L::fwd_n(C) * sizeof(T);
     const int thr = std::max(lb, lf) > 64 * 1024 ? 512 : 256, wpb = thr / 64;
+    const int per_cu = std::max<int>(1, std::min<int>(2048 / thr, (int)(160 * 1024 / std::max(lb, lf))));
+    const int cap = 256 * per_cu;  // one round of resident workgroups; waves loop over tiles
     auto kb = raocp::k_dy3_back<T, NX, NU>;
     auto kf = raocp::k_dy3_fwd<T, NX, NU>;
     allow_lds(kb, lb);
     allow_lds(kf, lf);
-    auto grid = [&](const raocp::Dy3Stage& st) {
+    // stages of few tiles run slot-parallel (a wave per child slot): the dependent MFMA chain
+    // of a tile is what a small stage costs
+    auto coop = [&](const raocp::Dy3Stage& st) { return (st.i1 - st.i0 + 15) / 16 * C <= 256 * wpb; };
+    auto grid = [&](const raocp::Dy3Stage& st, bool back) {
         const int tiles = (st.i1 - st.i0 + 15) / 16;
-        return std::max(1, std::min(512, (tiles + wpb - 1) / wpb));
+        if (coop(st)) return std::max(1, back ? tiles : (tiles * C + wpb - 1) / wpb);
+        return std::max(1, std::min(cap, (tiles + wpb - 1) / wpb));
     };
-    const int N = c->N;
+    const int N = c->N, S = c->sh_S;  // S > 0: a shard owns the stages >= S partly
+    auto stage = [&](int t) -> const raocp::Dy3Stage& { return S > 0 && t >= S ? c->d3own[t] : c->d3st[t]; };
     for (int t = N - 1; t >= 0; --t) {
-        const raocp::Dy3Stage& st = c->d3st[t];
+        if (part == 1 && t < S) break;
+        if (part == 2 && t >= S) continue;
+        const raocp::Dy3Stage& st = stage(t);
+        if (st.i1 <= st.i0) continue;
         raocp::ChkArg ca{};
         if (ck && t == N - 1) ca = *ck;
-        kb<<<grid(st) + ca.on, thr, lb, c->stream>>>(c->dev, ctl, ca, z, c->Q2, c->Dd2, st, C, c->W2, c->RG2);
+        kb<<<grid(st, true) + ca.on, thr, lb, c->stream>>>(c->dev, ctl, ca, z, c->Q2, c->Dd2, st, C, c->W2, c->RG2,
+                                                          coop(st) ? 1 : 0);
     }
+    if (part == 1) return;
     for (int t = 0; t < N; ++t) {
-        const raocp::Dy3Stage& st = c->d3st[t];
-        kf<<<grid(st), thr, lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, st, C, c->KM2, c->F2);
+        const raocp::Dy3Stage& st = stage(t);
+        if (st.i1 <= st.i0) continue;
+        kf<<<grid(st, false), thr, lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, st, C, c->KM2, c->F2, coop(st) ? 1 : 0);
     }
 }
-void launch_dyn3(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck) {
+void launch_dyn3(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck, int part) {
     if (c->f32) {
-        if (c->nx == 20) launch_dyn3t<float, 20, 8>(c, z, ctl, ck);
-        else if (c->nx == 32) launch_dyn3t<float, 32, 12>(c, z, ctl, ck);
-        else launch_dyn3t<float, 64, 16>(c, z, ctl, ck);
+        if (c->nx == 20) launch_dyn3t<float, 20, 8>(c, z, ctl, ck, part);
+        else if (c->nx == 32) launch_dyn3t<float, 32, 12>(c, z, ctl, ck, part);
+        else launch_dyn3t<float, 64, 16>(c, z, ctl, ck, part);
     } else {
-        if (c->nx == 20) launch_dyn3t<double, 20, 8>(c, z, ctl, ck);
-        else if (c->nx == 32) launch_dyn3t<double, 32, 12>(c, z, ctl, ck);
-        else launch_dyn3t<double, 64, 16>(c, z, ctl, ck);
+        if (c->nx == 20) launch_dyn3t<double, 20, 8>(c, z, ctl, ck, part);
+        else if (c->nx == 32) launch_dyn3t<double, 32, 12>(c, z, ctl, ck, part);
+        else launch_dyn3t<double, 64, 16>(c, z, ctl, ck, part);
     }
 }
 
@@ -529,9 +548,9 @@ struct DynOp {
 // launch (only where defer_check(c) holds)
 void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part = 0,
                      const raocp::ChkArg* ck = nullptr) {
-    if (c->dyn3 && c->sh_S == 0) {
+    if (c->dyn3) {
         double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
-        launch_dyn3(c, z, ctl, ck);
+        launch_dyn3(c, z, ctl, ck, part);
         return;
     }
     if (c->dyn2) {
@@ -650,14 +669,14 @@ bool cp3_sizes(bool f32, int nx, int nu) {
     return (nx == 20 && nu == 8) || (nx == 32 && nu == 12) || (f32 && nx == 64 && nu == 16);
 }
 void launch_cp3(raocp_ctx* c) {
-    const int g = c->cp3_grid, C = c->unif_C, bx = c->box_mode, mL = c->cp3_mL;
+    const int g = c->cp3_grid, C = c->unif_C, bx = c->box_mode, mL = c->cp3_mL, sp = c->cp3_split;
     if (c->f32) {
-        if (c->nx == 20) raocp::k_cp3<float, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
-        else if (c->nx == 32) raocp::k_cp3<float, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
-        else raocp::k_cp3<float, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
+        if (c->nx == 20) raocp::k_cp3<float, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
+        else if (c->nx == 32) raocp::k_cp3<float, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
+        else raocp::k_cp3<float, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
     } else {
-        if (c->nx == 20) raocp::k_cp3<double, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
-        else raocp::k_cp3<double, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL);
+        if (c->nx == 20) raocp::k_cp3<double, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
+        else raocp::k_cp3<double, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
     }
 }
 // the solve's first half step Z[1] = prox-part(Z[0] - alpha L^T E[0]) (s_0 relaxation,
@@ -725,26 +744,47 @@ int rccl_load() {
 //       iteration late, k_cp_check_gather), so SURVEY.md's X3 all-reduce is not needed.
 // pack/unpack run on every shard; the collective itself is RCCL, or, for shards that
 // share a process (raocp_group_cp_run), host-driven copies between the phases.
+// X2 rows: the tiered sweep's q rows (KP doubles each), or the per-stage sweep's (nx scalars
+// of the context's type, raocp_dyn3.hip)
+int x2_row(const raocp_ctx* c) { return c->dyn3 ? c->nx : c->KP; }
+int x2_elt(const raocp_ctx* c) { return c->dyn3 ? c->wsz : 8; }
+double* x2_q(const raocp_ctx* c) { return c->dyn3 ? c->Q2 : c->q; }
+size_t x2_bytes(const raocp_ctx* c) { return (size_t)c->x_max * x2_row(c) * x2_elt(c); }
 void shard_pack_x2(raocp_ctx* c) {
+    const size_t row = (size_t)x2_row(c) * x2_elt(c);
     if (c->own_cnt)
-        (void)hipMemcpyAsync(c->x2_send, c->q + (size_t)c->own_first * c->KP, (size_t)c->own_cnt * c->KP * sizeof(double),
+        (void)hipMemcpyAsync(c->x2_send, (char*)x2_q(c) + (size_t)c->own_first * row, (size_t)c->own_cnt * row,
                              hipMemcpyDeviceToDevice, c->stream);
 }
 void shard_unpack_x2(raocp_ctx* c) {
-    const int tot = c->sh_R * c->x_max * c->KP;
-    raocp::k_scatter_rows<<<std::max(1, std::min(256, cdiv(tot, kBlock))), kBlock, 0, c->stream>>>(
-        c->x2_recv, c->q, c->d_slc, c->sh_R, c->x_max, c->KP);
+    const int tot = c->sh_R * c->x_max * x2_row(c);
+    const int g = std::max(1, std::min(256, cdiv(tot, kBlock)));
+    if (x2_elt(c) == 4)
+        raocp::k_scatter_rows<float><<<g, kBlock, 0, c->stream>>>((const float*)c->x2_recv, (float*)x2_q(c), c->d_slc,
+                                                                   c->sh_R, c->x_max, x2_row(c));
+    else
+        raocp::k_scatter_rows<double><<<g, kBlock, 0, c->stream>>>(c->x2_recv, x2_q(c), c->d_slc, c->sh_R, c->x_max,
+                                                                    x2_row(c));
 }
 // X1 carries the roots' (eta+, xi2) eta2 entries and the previous iteration's residual record
 int x1_len(const raocp_ctx* c) { return 2 * c->x_max + 16; }
 void shard_pack_x1(raocp_ctx* c) {
-    raocp::k_pack_x1<<<std::max(1, cdiv(c->own_cnt, kBlock)), kBlock, 0, c->stream>>>(
-        c->x1_send, c->bufs.e1 + c->dev.E2 + c->own_first, c->XI2 + c->dev.E2 + c->own_first, c->own_cnt, c->x_max,
-        c->red8);
+    const int g = std::max(1, cdiv(c->own_cnt, kBlock)), o = c->dev.E2 + c->own_first;
+    if (c->f32)
+        raocp::k_pack_x1<float><<<g, kBlock, 0, c->stream>>>(c->x1_send, (const float*)c->bufs.e1 + o, (const float*)c->XI2 + o,
+                                                             c->own_cnt, c->x_max, c->red8);
+    else
+        raocp::k_pack_x1<double><<<g, kBlock, 0, c->stream>>>(c->x1_send, c->bufs.e1 + o, c->XI2 + o, c->own_cnt, c->x_max,
+                                                              c->red8);
 }
 void shard_unpack_x1(raocp_ctx* c) {
-    raocp::k_unpack_x1<<<std::max(1, cdiv(c->sh_R * c->x_max, kBlock)), kBlock, 0, c->stream>>>(
-        c->x1_recv, c->bufs.e1 + c->dev.E2, c->XI2 + c->dev.E2, c->d_slc, c->sh_R, c->x_max);
+    const int g = std::max(1, cdiv(c->sh_R * c->x_max, kBlock)), o = c->dev.E2;
+    if (c->f32)
+        raocp::k_unpack_x1<float><<<g, kBlock, 0, c->stream>>>(c->x1_recv, (float*)c->bufs.e1 + o, (float*)c->XI2 + o,
+                                                               c->d_slc, c->sh_R, c->x_max);
+    else
+        raocp::k_unpack_x1<double><<<g, kBlock, 0, c->stream>>>(c->x1_recv, c->bufs.e1 + o, c->XI2 + o, c->d_slc, c->sh_R,
+                                                                c->x_max);
     raocp::k_cp_check_gather<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->x1_recv, c->sh_R, c->x_max);
 }
 int rccl_check(ncclResult_t r, const char* what) {
@@ -759,7 +799,8 @@ int enqueue_shard_iteration(raocp_ctx* c) {
     int rc;
     launch_dynamics(c, c->bufs, 1, c->ctl, 1);
     shard_pack_x2(c);
-    if ((rc = rccl_check(g_rccl.all_gather(c->x2_send, c->x2_recv, (size_t)c->x_max * c->KP, ncclFloat64, comm, c->stream),
+    if ((rc = rccl_check(g_rccl.all_gather(c->x2_send, c->x2_recv, (size_t)c->x_max * x2_row(c),
+                                           x2_elt(c) == 4 ? ncclFloat32 : ncclFloat64, comm, c->stream),
                          "ncclAllGather(q)")))
         return rc;
     shard_unpack_x2(c);
@@ -835,7 +876,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             if (!c->f32 && c->cp_v1) return "k_cpp<" + nn + ">";
             return "k_cpp2<" + T + ", " + rr + ">";
         case 9:
-            if (c->dyn3 && c->sh_S == 0)
+            if (c->dyn3)
                 return "k_dy3_back<" + T + ", " + nn + "> + k_dy3_fwd<" + T + ", " + nn + "> (per stage)";
             if (c->dyn2) return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
             if (c->cut > 0)
@@ -2077,7 +2118,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         if (const char* e = getenv("RAOCP_CP3")) c->cp3 = c->cp3 && atoi(e) != 0;
         if (c->cp3) {
             c->cp3_mL = c->stage_ptr[N - 1];
-            const long tiles = (long)(m - c->cp3_mL + 15) / 16 + (c->cp3_mL + 15) / 16;
+            long tiles = (long)(m - c->cp3_mL + 15) / 16 + (c->cp3_mL + 15) / 16;
+            // small trees (latency-bound: config 2 has 256 family tiles, one wave each) split
+            // the leaves into tasks of their own: twice the waves, half the longest chain
+            c->cp3_split = tiles < 1024;
+            if (const char* e = getenv("RAOCP_CP3_SPLIT")) c->cp3_split = atoi(e) != 0;
+            if (c->cp3_split) tiles += (n - m + 15) / 16;
             c->cp3_grid = (int)std::max(1L, std::min((tiles + 3) / 4, 2048L));
             if (const char* e = getenv("RAOCP_CP3_GRID")) c->cp3_grid = std::max(1, atoi(e));
             if (c->cp3_grid > c->red_rows) {
@@ -2562,13 +2608,23 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
 // ---- subtree sharding ---------------------------------------------------------------
 int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     DevGuard dg_(c);
-    if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
+    if (c && c->f32 && !c->dyn3)
+        return fail(RAOCP_ERR_ARG, "fp32 sharding needs the per-stage streaming dynamics (uniform branching and slots)");
     if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(RAOCP_ERR_ARG, "bad shard arguments");
     // one shard is the unsharded solve, unless forced (tests run the exchange path with R = 1)
     if (nranks == 1 && !getenv("RAOCP_SHARD_FORCE")) return RAOCP_OK;
-    const int S = c->cut, N = c->N;
-    if (S <= 0 || S >= N || c->tiers.empty())
+    const int N = c->N;
+    int S = c->cut;
+    if (c->dyn3) {
+        // the per-stage sweep: cut at the first stage with at least 8 subtrees per shard (the
+        // replicated top above it is a few hundred nodes at most)
+        S = 0;
+        for (int t = 1; t < N && !S; ++t)
+            if (c->stage_ptr[t + 1] - c->stage_ptr[t] >= 8 * nranks) S = t;
+        if (!S) return fail(RAOCP_ERR_ARG, "tree too small to shard (no stage with 8 subtrees per shard)");
+    } else if (S <= 0 || S >= N || c->tiers.empty()) {
         return fail(RAOCP_ERR_ARG, "tree too small to shard (the dynamics plan has no tier below the top)");
+    }
     const int nb = c->stage_ptr[S + 1] - c->stage_ptr[S];
     if (nb < nranks) return fail(RAOCP_ERR_ARG, "fewer subtrees at the cut stage than shards");
     c->sh_R = nranks;
@@ -2604,8 +2660,14 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
         }
     }
     c->tier_own.clear();
-    for (const auto& tp : c->tiers)
-        c->tier_own.push_back({c->own_lo[tp.s0] - c->stage_ptr[tp.s0], c->own_hi[tp.s0] - c->own_lo[tp.s0]});
+    if (!c->dyn3)
+        for (const auto& tp : c->tiers)
+            c->tier_own.push_back({c->own_lo[tp.s0] - c->stage_ptr[tp.s0], c->own_hi[tp.s0] - c->own_lo[tp.s0]});
+    c->d3own = c->d3st;
+    for (int t = S; t < N && c->dyn3; ++t) {
+        c->d3own[t].i0 = c->own_lo[t];
+        c->d3own[t].i1 = c->own_hi[t];
+    }
     // CP blocks: the replicated top families plus the owned ones, the owned leaves
     std::vector<std::pair<int, int>> pr_;
     pr_.push_back({0, c->stage_ptr[S]});
@@ -2614,7 +2676,8 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     std::vector<std::pair<int, int>> lr_{{c->own_lo[N], c->own_hi[N]}};
     int rc;
     if ((rc = build_cp_blocks(c, pr_, lr_))) return rc;
-    if ((rc = c->alloc(&c->x2_send, (size_t)xmax * c->KP)) || (rc = c->alloc(&c->x2_recv, (size_t)nranks * xmax * c->KP)) ||
+    if ((rc = c->alloc(&c->x2_send, (size_t)xmax * std::max(c->KP, c->nx))) ||
+        (rc = c->alloc(&c->x2_recv, (size_t)nranks * xmax * std::max(c->KP, c->nx))) ||
         (rc = c->alloc(&c->x1_send, (size_t)2 * xmax + 16)) || (rc = c->alloc(&c->x1_recv, (size_t)nranks * (2 * xmax + 16))) ||
         (rc = c->alloc(&c->red8, 16)) || (rc = c->upload_vec(&c->d_slc, slc)))
         return rc;
@@ -2693,8 +2756,8 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
         for (int r = 0; r < R; ++r) {
             raocp_ctx* c = cs[r];
             for (int q = 0; q < R; ++q)
-                HIPCHK(hipMemcpyAsync(c->x2_recv + (size_t)q * c->x_max * c->KP, cs[q]->x2_send,
-                                      (size_t)c->x_max * c->KP * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+                HIPCHK(hipMemcpyAsync((char*)c->x2_recv + (size_t)q * x2_bytes(c), cs[q]->x2_send, x2_bytes(c),
+                                      hipMemcpyDeviceToDevice, c->stream));
             shard_unpack_x2(c);
             launch_dynamics(c, c->bufs, 1, c->ctl, 2);
             launch_cpd(c);

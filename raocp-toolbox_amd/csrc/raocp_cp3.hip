@@ -18,8 +18,8 @@
 //   phase 2  per child slot k: the SOC of (eta3, eta4, eta5 | eta6), eta+ / xi2 in registers,
 //            and L^T of (eta+, d - eta+, xi2) accumulated per parent by a second MFMA chain
 //   phase 3  x_i, u_i of the next half step and their residuals
-//   phase 4  (parents of leaves) per leaf slot: the leaf SOC (eta11, eta12 | eta13), eta14
-//            box, and the leaf's x row of the next half step (sqrtPf MFMA chains)
+//   phase 4  (parents of leaves, run first) per leaf slot: the leaf SOC (eta11, eta12 | eta13),
+//            eta14 box, and the leaf's x row of the next half step (sqrtPf MFMA chains)
 //   phase 5  s_j of the children (eta2_j of a nonleaf child recomputed here, bit-identical
 //            to its own tile's), then the closed-form AVaR kernel projection of the family
 //
@@ -30,31 +30,45 @@
 // Products in the transposed form: D = W V with the weights W (16 x 4 per k-step) as the A
 // operand and the node vectors V as the B operand (lane lo = node), so the accumulator of
 // the L product (rows on the lane groups and registers, node on lo) is already the B
-// operand of the L^T product (no transpose, no LDS). Lane (lo, h = lane >> 4), register e
-// of row tile rt holds row r = 16 rt + 4 h + e of node lo in every operand and accumulator
-// ("row layout"): the A rows are permuted (MF<T>::arow) so the f64 accumulator map (row
-// h + 4 e) and the f32 one (4 h + e) both produce it, and the k index of a k-step s is
-// 16 (s >> 2) + 4 h + (s & 3), so a lane's B values are 4 consecutive entries of its node:
-// whole 16-B vector loads and stores.
+// operand of the L^T product (no transpose, no LDS). "Row layout" of an R-row vector
+// (R = 4 KC): lane (lo, h = lane >> 4) holds the KC consecutive rows KC h .. KC h + KC - 1
+// of node lo, slot t = 4 rt + e (register e of row tile rt) holding row KC h + t (t < KC;
+// zero above). In every operand and accumulator: the k index of k-step s is KC h + s, so a
+// lane's B values are consecutive entries of its node (16-B vector loads and stores where
+// KC is a multiple of 4), and the A rows are permuted (MFA<T>::rows) so that the f64
+// accumulator map (row h + 4 e) and the f32 one (4 h + e) both land row KC h + 4 rt + e in
+// slot (rt, e). A product then takes ceil(KC_out / 4) x KC_in MFMAs: no k-step is padding
+// (nx = 20: 2 x 5, against 2 x 8 with 16-row tiles).
 
+// A row lo of an output row tile lands in lane group g, register e of the accumulator
 template <class T>
 struct MFA;
 template <>
-struct MFA<double> {
-    static __device__ __forceinline__ int arow(int lo) { return 4 * (lo & 3) + (lo >> 2); }
+struct MFA<double> {  // D row = h + 4 e
+    static __device__ __forceinline__ int g_of(int lo) { return lo & 3; }
+    static __device__ __forceinline__ int e_of(int lo) { return lo >> 2; }
 };
 template <>
-struct MFA<float> {
-    static __device__ __forceinline__ int arow(int lo) { return lo; }
+struct MFA<float> {  // D row = 4 h + e
+    static __device__ __forceinline__ int g_of(int lo) { return lo >> 2; }
+    static __device__ __forceinline__ int e_of(int lo) { return lo & 3; }
 };
+// the weight row A row lo of output row tile ro carries for an R-row output (-1: padding)
+template <class T, int R>
+__device__ __forceinline__ int wrow(int ro, int lo) {
+    constexpr int KC = R / 4;
+    const int t = 4 * ro + MFA<T>::e_of(lo);
+    return t < KC ? KC * MFA<T>::g_of(lo) + t : -1;
+}
 
 // weight fragments of one R x K table (column-major M[k R + r]) in the transposed form,
 // staged once per workgroup in LDS (registers are the scarce resource of this kernel: the
 // per-parent L products and three L^T accumulators stay live over the child slots):
-// lds[(ro KS + s) 64 + lane] = M[16 ro + arow(lo)][16 (s >> 2) + 4 h + (s & 3)]
+// lds[(ro KS + s) 64 + lane] = M[wrow(ro, lo)][K/4 h + s]
 template <class T, int R, int K>
 struct WL {
-    static constexpr int RO = (R + 15) / 16, RK = (K + 15) / 16, KS = 4 * RK, N = RO * KS * 64;
+    static_assert(R % 4 == 0 && K % 4 == 0, "row layout: R, K multiples of 4");
+    static constexpr int RO = (R / 4 + 3) / 4, KS = K / 4, N = RO * KS * 64;
     const __attribute__((address_space(3))) T* base;
     __device__ __forceinline__ T get(int ro, int s) const { return base[(ro * KS + s) * 64 + (threadIdx.x & 63)]; }
     // every thread of the workgroup takes part (a __syncthreads follows)
@@ -62,8 +76,8 @@ struct WL {
         cglbp<T> M = (cglbp<T>)(tab + (size_t)t * R * K);
         for (int q = threadIdx.x; q < N; q += blockDim.x) {
             const int l = q & 63, lo = l & 15, h = l >> 4, s = (q >> 6) % KS, ro = (q >> 6) / KS;
-            const int r = 16 * ro + MFA<T>::arow(lo), k = 16 * (s >> 2) + 4 * h + (s & 3);
-            dst[q] = (r < R && k < K) ? M[k * R + r] : T(0);
+            const int r = wrow<T, R>(ro, lo), k = KS * h + s;
+            dst[q] = r >= 0 ? M[k * R + r] : T(0);
         }
     }
 };
@@ -83,37 +97,42 @@ struct V4a {
     typedef T type __attribute__((ext_vector_type(4), aligned(sizeof(T))));
 };
 
-// row-layout load of an R-row node vector (R % 4 == 0): a[rt][e] = v[16 rt + 4 h + e]
+// slot (rt, e) of an R-row vector holds a row (t = 4 rt + e < R / 4)
+template <int R>
+__device__ __forceinline__ constexpr bool tok(int rt, int e) {
+    return 4 * rt + e < R / 4;
+}
+// row-layout load of an R-row node vector: a[rt][e] = v[R/4 h + 4 rt + e] (0 past R/4)
 template <class T, int R>
 __device__ __forceinline__ void ld_rows(cglbp<T> v, bool live, T (&a)[(R + 15) / 16][4]) {
     typedef typename V4a<T>::type vt;
-    const int h = (threadIdx.x & 63) >> 4;
+    constexpr int KC = R / 4;
+    cglbp<T> b = v + KC * ((threadIdx.x & 63) >> 4);
     _Pragma("unroll") for (int rt = 0; rt < (R + 15) / 16; ++rt) {
-        const int r0 = 16 * rt + 4 * h;
-        if (live && r0 < R) {
-            const vt w = *(const __attribute__((address_space(1))) vt*)(v + r0);
+        if (live && 4 * rt + 3 < KC) {
+            const vt w = *(const __attribute__((address_space(1))) vt*)(b + 4 * rt);
             _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = w[e];
         } else {
-            _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = T(0);
+            _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = (live && tok<R>(rt, e)) ? b[4 * rt + e] : T(0);
         }
     }
 }
 template <class T, int R>
 __device__ __forceinline__ void st_rows(glbp<T> v, bool live, const T (&a)[(R + 15) / 16][4]) {
     typedef typename V4a<T>::type vt;
-    const int h = (threadIdx.x & 63) >> 4;
+    constexpr int KC = R / 4;
+    glbp<T> b = v + KC * ((threadIdx.x & 63) >> 4);
     _Pragma("unroll") for (int rt = 0; rt < (R + 15) / 16; ++rt) {
-        const int r0 = 16 * rt + 4 * h;
-        if (live && r0 < R) {
+        if (!live) continue;
+        if (4 * rt + 3 < KC) {
             vt w;
             _Pragma("unroll") for (int e = 0; e < 4; ++e) w[e] = a[rt][e];
-            *(__attribute__((address_space(1))) vt*)(v + r0) = w;
+            *(__attribute__((address_space(1))) vt*)(b + 4 * rt) = w;
+        } else {
+            _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<R>(rt, e)) b[4 * rt + e] = a[rt][e];
         }
     }
-}
-template <class T, int R>
-__device__ __forceinline__ bool row_ok(int rt) {
-    return 16 * rt + 4 * ((threadIdx.x & 63) >> 4) < R;
 }
 
 // sum over the 4 lane groups (the rows of one node)
@@ -133,9 +152,42 @@ struct KpScratch {
     T s[16][4];
 };
 
+// the inputs of one child slot (child block rows of d, tau of z+ and p) and of one leaf slot
+template <class T, int NX, int NU>
+struct ChildIn {
+    T d3[(NX + 15) / 16][4], d4[(NU + 15) / 16][4];
+    T d5, d6, tz, tp;
+    __device__ __forceinline__ void load(const Dev& p, cglbp<T> zp, cglbp<T> pz, cglbp<T> d, int j, bool live) {
+        ld_rows<T, NX>(d + e3(p, live ? j : 1), live, d3);
+        ld_rows<T, NU>(d + e4(p, live ? j : 1), live, d4);
+        d5 = live ? d[p.E5 + j] : T(0);
+        d6 = live ? d[p.E6 + j] : T(0);
+        tz = live ? zp[p.T0 + j] : T(0);
+        tp = live ? pz[p.T0 + j] : T(0);
+    }
+};
+template <class T, int NX>
+struct LeafIn {
+    T lz[(NX + 15) / 16][4], lp[(NX + 15) / 16][4], d11[(NX + 15) / 16][4], d14[(NX + 15) / 16][4];
+    T d12, d13, sz, sp;
+    int o14;
+    __device__ __forceinline__ void load(const Dev& p, cglbp<T> zp, cglbp<T> pz, cglbp<T> d, int l, bool live, int bx,
+                                         int m, bool box) {
+        ld_rows<T, NX>(zp + p.X0 + (size_t)(live ? l : 0) * NX, live, lz);
+        ld_rows<T, NX>(pz + p.X0 + (size_t)(live ? l : 0) * NX, live, lp);
+        ld_rows<T, NX>(d + e11(p, live ? l : m), live, d11);
+        o14 = live && box ? o14_of<NX>(p, l, bx) : -1;
+        ld_rows<T, NX>(d + (o14 >= 0 ? o14 : 0), o14 >= 0, d14);
+        d12 = live ? d[p.E12 + l] : T(0);
+        d13 = live ? d[p.E13 + l] : T(0);
+        sz = live ? zp[p.S0 + l] : T(0);
+        sp = live ? pz[p.S0 + l] : T(0);
+    }
+};
+
 template <class T, int NX, int NU>
 __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs bf, double* __restrict__ part, int C,
-                                             int bx, int mL) {
+                                             int bx, int mL, int split) {
     typedef typename MF<T>::v4 v4;
     static_assert(NX % 4 == 0 && NU % 4 == 0, "row layout needs nx, nu multiples of 4");
     constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
@@ -186,14 +238,125 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
         m3 = nmax(m3, (double)fabs(dl0));
         m4 = nmax(m4, (double)fabs(dl1));
     };
+    // one leaf l (lane lo) of a slot k: full = the whole leaf (eta11..eta14 and x_l of the half
+    // step), else only its SOC scalars; pside = the parent's side (s_l of the half step into
+    // the kernel projection's scratch, and its residual terms)
+    auto leaf_work = [&](const LeafIn<T, NX>& cur, int l, int k, bool live, bool full, bool pside) {
+        const T (&lz)[RX][4] = cur.lz;
+        const T (&lp)[RX][4] = cur.lp;
+        const T (&d11)[RX][4] = cur.d11;
+        const T (&d14)[RX][4] = cur.d14;
+        const int o14 = cur.o14;
+        const T d12 = cur.d12, d13 = cur.d13, sz = cur.sz, sp = cur.sp;
+            v4 la[RX], lb[RX];
+            {
+                T a1[RX][4], a2[RX][4];
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                    a1[rt][e] = T(2) * lz[rt][e] - lp[rt][e];
+                    a2[rt][e] = lz[rt][e] - lp[rt][e];
+                }
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) la[rt] = lb[rt] = v4{0, 0, 0, 0};
+                mmt(wp, a1, la);
+                if (full) mmt(wp, a2, lb);
+            }
+            T v11[RX][4];
+            T ss = T(0);
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                v11[rt][e] = (d11[rt][e] + alpha * la[rt][e]) * ra;
+                if (tok<NX>(rt, e)) ss += v11[rt][e] * v11[rt][e];
+            }
+            ss = sum_h(ss);
+            const T a5 = T(0.5) * (T(2) * sz - sp), b5 = T(0.5) * (sz - sp);
+            const T v12 = (d12 + alpha * a5) * ra + T(-0.5);
+            const T v13 = (d13 + alpha * a5) * ra + T(0.5);
+            ss += v12 * v12;
+            const T nf = sqrt(ss), tt = v13;
+            T ep12, x212, ep13, x213;
+            fin(d12, v12, soc_apply_t(v12, false, nf, tt), b5, ep12, x212);
+            fin(d13, v13, soc_apply_t(v13, true, nf, tt), b5, ep13, x213);
+            if (pside && live && h == 0) {
+                ks.s[lo][k] = sz - alpha * (T(0.5) * (ep12 + ep13));
+                account(sp, sz, T(0.5) * ((d12 - ep12) + (d13 - ep13)), T(0.5) * (x212 + x213));
+            }
+            if (!full) return;
+            if (live && h == 0) eo[p.E12 + l] = ep12;
+            if (live && h == 1) eo[p.E13 + l] = ep13;
+            T eA[RX][4], eW[RX][4], eC[RX][4];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                T ep = T(0), x2 = T(0);
+                if (live && tok<NX>(rt, e))
+                    fin(d11[rt][e], v11[rt][e], soc_apply_t(v11[rt][e], false, nf, tt), lb[rt][e], ep, x2);
+                eA[rt][e] = ep;
+                eW[rt][e] = d11[rt][e] - ep;
+                eC[rt][e] = x2;
+            }
+            st_rows<T, NX>(eo + e11(p, live ? l : m), live, eA);
+            v4 gA[RX], gW[RX], gC[RX];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) gA[rt] = gW[rt] = gC[rt] = v4{0, 0, 0, 0};
+            mmt(wp, eA, gA);
+            mmt(wp, eW, gW);
+            mmt(wp, eC, gC);
+            // eta14 = x_l (box) and x_l = sqrtPf eta11 + eta14 (operators.py:86-94)
+            if (o14 >= 0) {
+                const int bl = p.iBl[l];
+                T l14[RX][4], h14[RX][4], e14[RX][4];
+                ld_rows<T, NX>((cglbp<T>)p.blo_l + (size_t)bl * NX, true, l14);
+                ld_rows<T, NX>((cglbp<T>)p.bhi_l + (size_t)bl * NX, true, h14);
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                    T ep = T(0), x2 = T(0);
+                    if (tok<NX>(rt, e)) {
+                        const T v = (d14[rt][e] + alpha * (T(2) * lz[rt][e] - lp[rt][e])) * ra;
+                        fin(d14[rt][e], v, box_apply_t(v, l14[rt][e], h14[rt][e], ctl), lz[rt][e] - lp[rt][e], ep, x2);
+                    }
+                    e14[rt][e] = ep;
+                    gA[rt][e] += ep;
+                    gW[rt][e] += d14[rt][e] - ep;
+                    gC[rt][e] += x2;
+                }
+                st_rows<T, NX>(eo + o14, true, e14);
+            }
+            T ox[RX][4];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                ox[rt][e] = lz[rt][e] - alpha * gA[rt][e];
+                if (live && tok<NX>(rt, e)) account(lp[rt][e], lz[rt][e], gW[rt][e], gC[rt][e]);
+            }
+            st_rows<T, NX>(out + p.X0 + (size_t)(live ? l : 0) * NX, live, ox);
+    };
     const int G = 2 * C + 1;
     const int nT1 = (m - mL + 15) >> 4, nT0 = (mL + 15) >> 4;  // leaf-parent tiles first (heavier)
-    for (int task = gw; task < nT0 + nT1; task += nwv) {
+    const int nTL = split ? (p.n - m + 15) >> 4 : 0;           // leaf tiles (split)
+    for (int tk = gw; tk < nTL + nT0 + nT1; tk += nwv) {
+        if (tk < nTL) {
+            // a tile of 16 consecutive leaves (split): everything of the leaf but s_l
+            const int l = m + 16 * tk + lo;
+            const bool live = l < p.n;
+            LeafIn<T, NX> cur;
+            cur.load(p, zp, pz, d, l, live, bx, m, true);
+            leaf_work(cur, l, 0, live, true, false);
+            continue;
+        }
+        const int task = tk - nTL;
         const bool leafp = task < nT1;
         const int i0 = leafp ? mL + 16 * task : 16 * (task - nT1), iend = leafp ? m : mL;
         const int i = i0 + lo;
         const bool live = i < iend;
-        // ---------------- phase 1: the parent's rows
+        // ---------------- phase 4 (first, on parents of leaves): leaf children (leaf SOC, eta14
+        // box, x_l of the half step); their s_l goes to the kernel projection's scratch. The
+        // next slot's rows are loaded before the current slot's arithmetic (vmcnt in order).
+        // split: the leaves are tasks of their own, the family computes only their SOC scalars
+        if (leafp) {
+            LeafIn<T, NX> cur, nxt;
+            cur.load(p, zp, pz, d, 1 + C * i, live, bx, m, !split);
+            for (int k = 0; k < C; ++k) {
+                const int l = 1 + C * i + k;
+                if (k + 1 < C) nxt.load(p, zp, pz, d, l + 1, live, bx, m, !split);
+                leaf_work(cur, l, k, live, !split, true);
+                if (k + 1 < C) cur = nxt;
+            }
+        }
+        // ---------------- phase 1: the parent's rows (child slot 0's rows in flight meanwhile)
+        ChildIn<T, NX, NU> ccu, cnx;
+        ccu.load(p, zp, pz, d, 1 + C * i, live);
         const int o7 = live ? o7_of<NX, NU>(p, i, bx) : -1;
         // eta2_i and the y entries: every lane group loads the C + 1 entries b' y reads
         const int yo = G * i;
@@ -280,7 +443,7 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) {
                 _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                     T ep = T(0), x2 = T(0);
-                    if (o7 >= 0 && row_ok<T, NX>(rt)) {
+                    if (o7 >= 0 && tok<NX>(rt, e)) {
                         const T v = (d7x[rt][e] + alpha * (T(2) * xz[rt][e] - xp[rt][e])) * ra;
                         fin(d7x[rt][e], v, box_apply_t(v, lx[rt][e], hx[rt][e], ctl), xz[rt][e] - xp[rt][e], ep, x2);
                     }
@@ -295,7 +458,7 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) {
                 _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                     T ep = T(0), x2 = T(0);
-                    if (o7 >= 0 && row_ok<T, NU>(rt)) {
+                    if (o7 >= 0 && tok<NU>(rt, e)) {
                         const T v = (d7u[rt][e] + alpha * (T(2) * uz[rt][e] - up[rt][e])) * ra;
                         fin(d7u[rt][e], v, box_apply_t(v, lu[rt][e], hu[rt][e], ctl), uz[rt][e] - up[rt][e], ep, x2);
                     }
@@ -307,23 +470,23 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             }
             st_rows<T, NU>(eo + (o7 >= 0 ? o7 + NX : 0), o7 >= 0, e7u);
         }
-        // ---------------- phase 2: child slots (child block SOC, L^T accumulation)
+        // ---------------- phase 2: child slots (child block SOC, L^T accumulation), the next
+        // slot's rows loaded before the current slot's arithmetic
         for (int k = 0; k < C; ++k) {
             const int j = 1 + C * i + k;
-            T d3[RX][4], d4[RU][4];
-            ld_rows<T, NX>(d + e3(p, live ? j : 1), live, d3);
-            ld_rows<T, NU>(d + e4(p, live ? j : 1), live, d4);
-            const T d5 = live ? d[p.E5 + j] : T(0), d6 = live ? d[p.E6 + j] : T(0);
-            const T tz = live ? zp[p.T0 + j] : T(0), tp = live ? pz[p.T0 + j] : T(0);
+            if (k + 1 < C) cnx.load(p, zp, pz, d, j + 1, live);
+            T (&d3)[RX][4] = ccu.d3;
+            T (&d4)[RU][4] = ccu.d4;
+            const T d5 = ccu.d5, d6 = ccu.d6, tz = ccu.tz, tp = ccu.tp;
             T v3[RX][4], v4_[RU][4];
             T ss = T(0);
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 v3[rt][e] = (d3[rt][e] + alpha * qa[rt][e]) * ra;
-                if (row_ok<T, NX>(rt)) ss += v3[rt][e] * v3[rt][e];
+                if (tok<NX>(rt, e)) ss += v3[rt][e] * v3[rt][e];
             }
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 v4_[rt][e] = (d4[rt][e] + alpha * ua[rt][e]) * ra;
-                if (row_ok<T, NU>(rt)) ss += v4_[rt][e] * v4_[rt][e];
+                if (tok<NU>(rt, e)) ss += v4_[rt][e] * v4_[rt][e];
             }
             ss = sum_h(ss);
             const T a5 = T(0.5) * (T(2) * tz - tp), b5 = T(0.5) * (tz - tp);
@@ -335,7 +498,7 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             T e3A[RX][4], e3W[RX][4], e3C[RX][4];
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 T ep = T(0), x2 = T(0);
-                if (live && row_ok<T, NX>(rt))
+                if (live && tok<NX>(rt, e))
                     fin(d3[rt][e], v3[rt][e], soc_apply_t(v3[rt][e], false, nf, tt), qb[rt][e], ep, x2);
                 e3A[rt][e] = ep;
                 e3W[rt][e] = d3[rt][e] - ep;
@@ -348,7 +511,7 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             T e4A[RU][4], e4W[RU][4], e4C[RU][4];
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 T ep = T(0), x2 = T(0);
-                if (live && row_ok<T, NU>(rt))
+                if (live && tok<NU>(rt, e))
                     fin(d4[rt][e], v4_[rt][e], soc_apply_t(v4_[rt][e], false, nf, tt), ub[rt][e], ep, x2);
                 e4A[rt][e] = ep;
                 e4W[rt][e] = d4[rt][e] - ep;
@@ -390,6 +553,7 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
                 ks.s[lo][k] = sz - alpha * ep;
                 account(sp, sz, dj - ep, x2);
             }
+            if (k + 1 < C) ccu = cnx;
         }
         // ---------------- phase 3: x_i, u_i of the half step
         {
@@ -401,100 +565,14 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             T ox[RX][4], ou[RU][4];
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 ox[rt][e] = xz[rt][e] - alpha * gxA[rt][e];
-                if (live && row_ok<T, NX>(rt)) account(xp[rt][e], xz[rt][e], gxW[rt][e], gxC[rt][e]);
+                if (live && tok<NX>(rt, e)) account(xp[rt][e], xz[rt][e], gxW[rt][e], gxC[rt][e]);
             }
             st_rows<T, NX>(out + p.X0 + (size_t)i * NX, live, ox);
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 ou[rt][e] = uz[rt][e] - alpha * guA[rt][e];
-                if (live && row_ok<T, NU>(rt)) account(up[rt][e], uz[rt][e], guW[rt][e], guC[rt][e]);
+                if (live && tok<NU>(rt, e)) account(up[rt][e], uz[rt][e], guW[rt][e], guC[rt][e]);
             }
             st_rows<T, NU>(out + p.U0 + (size_t)i * NU, live, ou);
-        }
-        // ---------------- phase 4: leaf children (leaf SOC, eta14 box, x_l of the half step)
-        if (leafp) {
-            for (int k = 0; k < C; ++k) {
-                const int l = 1 + C * i + k;
-                T lz[RX][4], lp[RX][4], d11[RX][4], d14[RX][4];
-                ld_rows<T, NX>(zp + p.X0 + (size_t)(live ? l : 0) * NX, live, lz);
-                ld_rows<T, NX>(pz + p.X0 + (size_t)(live ? l : 0) * NX, live, lp);
-                ld_rows<T, NX>(d + e11(p, live ? l : m), live, d11);
-                const int o14 = live ? o14_of<NX>(p, l, bx) : -1;
-                ld_rows<T, NX>(d + (o14 >= 0 ? o14 : 0), o14 >= 0, d14);
-                const T d12 = live ? d[p.E12 + l] : T(0), d13 = live ? d[p.E13 + l] : T(0);
-                const T sz = live ? zp[p.S0 + l] : T(0), sp = live ? pz[p.S0 + l] : T(0);
-                v4 la[RX], lb[RX];
-                {
-                    T a1[RX][4], a2[RX][4];
-                    _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                        a1[rt][e] = T(2) * lz[rt][e] - lp[rt][e];
-                        a2[rt][e] = lz[rt][e] - lp[rt][e];
-                    }
-                    _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) la[rt] = lb[rt] = v4{0, 0, 0, 0};
-                    mmt(wp, a1, la);
-                    mmt(wp, a2, lb);
-                }
-                T v11[RX][4];
-                T ss = T(0);
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    v11[rt][e] = (d11[rt][e] + alpha * la[rt][e]) * ra;
-                    if (row_ok<T, NX>(rt)) ss += v11[rt][e] * v11[rt][e];
-                }
-                ss = sum_h(ss);
-                const T a5 = T(0.5) * (T(2) * sz - sp), b5 = T(0.5) * (sz - sp);
-                const T v12 = (d12 + alpha * a5) * ra + T(-0.5);
-                const T v13 = (d13 + alpha * a5) * ra + T(0.5);
-                ss += v12 * v12;
-                const T nf = sqrt(ss), tt = v13;
-                T eA[RX][4], eW[RX][4], eC[RX][4];
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    T ep = T(0), x2 = T(0);
-                    if (live && row_ok<T, NX>(rt))
-                        fin(d11[rt][e], v11[rt][e], soc_apply_t(v11[rt][e], false, nf, tt), lb[rt][e], ep, x2);
-                    eA[rt][e] = ep;
-                    eW[rt][e] = d11[rt][e] - ep;
-                    eC[rt][e] = x2;
-                }
-                st_rows<T, NX>(eo + e11(p, live ? l : m), live, eA);
-                v4 gA[RX], gW[RX], gC[RX];
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) gA[rt] = gW[rt] = gC[rt] = v4{0, 0, 0, 0};
-                mmt(wp, eA, gA);
-                mmt(wp, eW, gW);
-                mmt(wp, eC, gC);
-                T ep12, x212, ep13, x213;
-                fin(d12, v12, soc_apply_t(v12, false, nf, tt), b5, ep12, x212);
-                fin(d13, v13, soc_apply_t(v13, true, nf, tt), b5, ep13, x213);
-                if (live && h == 0) eo[p.E12 + l] = ep12;
-                if (live && h == 1) eo[p.E13 + l] = ep13;
-                // eta14 = x_l (box) and x_l = sqrtPf eta11 + eta14 (operators.py:86-94)
-                if (o14 >= 0) {
-                    const int bl = p.iBl[l];
-                    T l14[RX][4], h14[RX][4], e14[RX][4];
-                    ld_rows<T, NX>((cglbp<T>)p.blo_l + (size_t)bl * NX, true, l14);
-                    ld_rows<T, NX>((cglbp<T>)p.bhi_l + (size_t)bl * NX, true, h14);
-                    _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                        T ep = T(0), x2 = T(0);
-                        if (row_ok<T, NX>(rt)) {
-                            const T v = (d14[rt][e] + alpha * (T(2) * lz[rt][e] - lp[rt][e])) * ra;
-                            fin(d14[rt][e], v, box_apply_t(v, l14[rt][e], h14[rt][e], ctl), lz[rt][e] - lp[rt][e], ep, x2);
-                        }
-                        e14[rt][e] = ep;
-                        gA[rt][e] += ep;
-                        gW[rt][e] += d14[rt][e] - ep;
-                        gC[rt][e] += x2;
-                    }
-                    st_rows<T, NX>(eo + o14, true, e14);
-                }
-                T ox[RX][4];
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    ox[rt][e] = lz[rt][e] - alpha * gA[rt][e];
-                    if (live && row_ok<T, NX>(rt)) account(lp[rt][e], lz[rt][e], gW[rt][e], gC[rt][e]);
-                }
-                st_rows<T, NX>(out + p.X0 + (size_t)(live ? l : 0) * NX, live, ox);
-                if (live && h == 0) {
-                    ks.s[lo][k] = sz - alpha * (T(0.5) * (ep12 + ep13));
-                    account(sp, sz, T(0.5) * ((d12 - ep12) + (d13 - ep13)), T(0.5) * (x212 + x213));
-                }
-            }
         }
         // ---------------- phase 5: AVaR kernel projection of the family (cache.py:290-317,
         // closed form: r_k = alpha_r y_k - y_{C+k} + y_2C - tau_k - s_k, w = (r - 1 sum(r) /

@@ -21,18 +21,20 @@
 // Rinv, G, K) are staged once per workgroup in LDS in fragment order (WLs below).
 
 // a fragment table taken from a column-major source with leading dimension ld, rows
-// [r0, r0 + R), columns [c0, c0 + K): lds[(ro KS + s) 64 + lane] = M[r][k] (transposed form)
+// [r0, r0 + R), columns [c0, c0 + K): lds[(ro KS + s) 64 + lane] = M[r][k] (transposed form,
+// row layout of raocp_cp3.hip)
 template <class T, int R, int K>
 struct WLs {
-    static constexpr int RO = (R + 15) / 16, RK = (K + 15) / 16, KS = 4 * RK, N = RO * KS * 64;
+    static_assert(R % 4 == 0 && K % 4 == 0, "row layout: R, K multiples of 4");
+    static constexpr int RO = (R / 4 + 3) / 4, KS = K / 4, N = RO * KS * 64;
     const __attribute__((address_space(3))) T* base;
     __device__ __forceinline__ T get(int ro, int s) const { return base[(ro * KS + s) * 64 + (threadIdx.x & 63)]; }
     static __device__ __forceinline__ void fill(__attribute__((address_space(3))) T* dst, const T* M, int ld, int r0,
                                                 int c0) {
         for (int q = threadIdx.x; q < N; q += blockDim.x) {
             const int l = q & 63, lo = l & 15, h = l >> 4, s = (q >> 6) % KS, ro = (q >> 6) / KS;
-            const int r = 16 * ro + MFA<T>::arow(lo), k = 16 * (s >> 2) + 4 * h + (s & 3);
-            dst[q] = (r < R && k < K) ? ((cglbp<T>)M)[(size_t)(c0 + k) * ld + r0 + r] : T(0);
+            const int r = wrow<T, R>(ro, lo), k = KS * h + s;
+            dst[q] = r >= 0 ? ((cglbp<T>)M)[(size_t)(c0 + k) * ld + r0 + r] : T(0);
         }
     }
 };
@@ -71,7 +73,7 @@ struct Dy3Lds {
 template <class T, int NX, int NU>
 __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__ ctl, ChkArg ck, double* __restrict__ z_,
                                                   double* __restrict__ q_, double* __restrict__ d_, Dy3Stage st, int C,
-                                                  const double* __restrict__ W2, const double* __restrict__ RG2) {
+                                                  const double* __restrict__ W2, const double* __restrict__ RG2, int sp) {
     typedef typename MF<T>::v4 v4;
     typedef Dy3Lds<T, NX, NU> L;
     constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16, R = NX + NU;
@@ -98,17 +100,21 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
     glbp<T> z = (glbp<T>)z_;
     glbp<T> qb = (glbp<T>)q_;
     glbp<T> db = (glbp<T>)d_;
-    const int lo = threadIdx.x & 15;
-    const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const int nw = (gridDim.x - ck.on) * (blockDim.x >> 6);
+    const int lo = threadIdx.x & 15, wv = threadIdx.x >> 6;
     const int ntile = (st.i1 - st.i0 + 15) >> 4;
+    // sp (stages of few tiles): a workgroup per tile, wave k on child slot k, the slot sums
+    // gathered in LDS (slot order) by wave 0; else a wave per tile, slots in sequence
+    const int gw = sp ? blockIdx.x : blockIdx.x * (blockDim.x >> 6) + wv;
+    const int nw = (gridDim.x - ck.on) * (sp ? 1 : (blockDim.x >> 6));
+    lT* red = wl + L::back_n(C);  // sp: [C][RU + RX][4][64 lanes]
     for (int task = gw; task < ntile; task += nw) {
         const int i = st.i0 + 16 * task + lo;
         const bool live = i < st.i1;
         v4 ha[RU], aa[RX];
         _Pragma("unroll") for (int r = 0; r < RU; ++r) ha[r] = v4{0, 0, 0, 0};
         _Pragma("unroll") for (int r = 0; r < RX; ++r) aa[r] = v4{0, 0, 0, 0};
-        for (int k = 0; k < C; ++k) {
+        const int k0 = sp ? wv : 0, k1 = sp ? (wv < C ? wv + 1 : 0) : C;
+        for (int k = k0; k < k1; ++k) {
             const int j = 1 + C * (live ? i : st.i0) + k;
             T qj[RX][4];
             if (st.leaf) {
@@ -121,6 +127,26 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
             const typename L::WA wa{wl + k * (L::WB::N + L::WA::N) + L::WB::N};
             mmts(wb, qj, ha);
             mmts(wa, qj, aa);
+        }
+        if (sp) {
+            const int l = threadIdx.x & 63;
+            if (wv < C) {
+                _Pragma("unroll") for (int r = 0; r < RU; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                    red[((wv * (RU + RX) + r) * 4 + e) * 64 + l] = ha[r][e];
+                _Pragma("unroll") for (int r = 0; r < RX; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                    red[((wv * (RU + RX) + RU + r) * 4 + e) * 64 + l] = aa[r][e];
+            }
+            __syncthreads();
+            if (wv == 0) {
+                for (int k = 1; k < C; ++k) {
+                    _Pragma("unroll") for (int r = 0; r < RU; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                        ha[r][e] += red[((k * (RU + RX) + r) * 4 + e) * 64 + l];
+                    _Pragma("unroll") for (int r = 0; r < RX; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                        aa[r][e] += red[((k * (RU + RX) + RU + r) * 4 + e) * 64 + l];
+                }
+            }
+            __syncthreads();  // red is rewritten by the next tile
+            if (wv != 0) continue;
         }
         T u[RU][4], x[RX][4], v[RU][4];
         ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)i * NU, live, u);
@@ -143,7 +169,7 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
 template <class T, int NX, int NU>
 __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ ctl, double* __restrict__ z_,
                                                  const double* __restrict__ d_, const double* __restrict__ x0_, Dy3Stage st,
-                                                 int C, const double* __restrict__ KM2, const double* __restrict__ F2) {
+                                                 int C, const double* __restrict__ KM2, const double* __restrict__ F2, int sp) {
     typedef typename MF<T>::v4 v4;
     typedef Dy3Lds<T, NX, NU> L;
     constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
@@ -165,14 +191,17 @@ __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ 
     const int lo = threadIdx.x & 15;
     const int gw = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = gridDim.x * (blockDim.x >> 6);
     const int ntile = (st.i1 - st.i0 + 15) >> 4;
-    for (int task = gw; task < ntile; task += nw) {
+    // sp (stages of few tiles): a task per (tile, child slot), slot 0 also writing u
+    const int ntask = sp ? ntile * C : ntile;
+    for (int tk = gw; tk < ntask; tk += nw) {
+        const int task = sp ? tk / C : tk, ks = sp ? tk % C : 0, ke = sp ? ks + 1 : C;
         const int i = st.i0 + 16 * task + lo;
         const bool live = i < st.i1;
         T x[RX][4], d[RU][4];
         if (i == 0) {
-            // x_0 = x0bar (cache.py:283), written into the iterate too
+            // x_0 = x0bar (cache.py:283), written into the iterate too (by the slot-0 task)
             ld_rows<T, NX>((cglbp<T>)x0_, true, x);
-            st_rows<T, NX>(z + p.X0, true, x);
+            if (ks == 0) st_rows<T, NX>(z + p.X0, true, x);
         } else {
             ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
         }
@@ -182,8 +211,8 @@ __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ 
         mmts(wk, x, ku);
         T u[RU][4];
         _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) u[rt][e] = ku[rt][e] + d[rt][e];
-        st_rows<T, NU>(z + p.U0 + (size_t)i * NU, live, u);
-        for (int k = 0; k < C; ++k) {
+        if (ks == 0) st_rows<T, NU>(z + p.U0 + (size_t)i * NU, live, u);
+        for (int k = ks; k < ke; ++k) {
             const int j = 1 + C * (live ? i : st.i0) + k;
             const typename L::WA wa{wf + k * (L::WA::N + L::WG::N)};
             const typename L::WG wb{wf + k * (L::WA::N + L::WG::N) + L::WA::N};

@@ -956,7 +956,8 @@ __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, con
 // ---- subtree sharding (raocp_capi.hip, raocp_shard_setup): exchange packing and the
 // residual reduction split around the all-reduce
 // recv holds R slices of maxc rows of w doubles; slice r goes to dst rows lo_r .. lo_r + cnt_r
-__global__ void k_scatter_rows(const double* __restrict__ recv, double* __restrict__ dst, const int* __restrict__ slc,
+template <class T>
+__global__ void k_scatter_rows(const T* __restrict__ recv, T* __restrict__ dst, const int* __restrict__ slc,
                                int R, int maxc, int w) {
     const int tot = R * maxc * w;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
@@ -968,7 +969,9 @@ __global__ void k_scatter_rows(const double* __restrict__ recv, double* __restri
 // roots, then the 16-double residual record of its PREVIOUS iteration (k_cp_reduce; the
 // stopping test runs one iteration late, so the residual all-reduce rides on this
 // all-gather: two collectives per iteration)
-__global__ void k_pack_x1(double* __restrict__ send, const double* __restrict__ a, const double* __restrict__ b, int cnt,
+// (the message is fp64; T = the context's scalar type of a / b)
+template <class T>
+__global__ void k_pack_x1(double* __restrict__ send, const T* __restrict__ a, const T* __restrict__ b, int cnt,
                           int maxc, const double* __restrict__ red16) {
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < cnt; i += gridDim.x * blockDim.x) {
         send[2 * i] = a[i];
@@ -976,14 +979,15 @@ __global__ void k_pack_x1(double* __restrict__ send, const double* __restrict__ 
     }
     if (blockIdx.x == 0 && threadIdx.x < 16) send[2 * maxc + threadIdx.x] = red16[threadIdx.x];
 }
-__global__ void k_unpack_x1(const double* __restrict__ recv, double* __restrict__ a, double* __restrict__ b,
+template <class T>
+__global__ void k_unpack_x1(const double* __restrict__ recv, T* __restrict__ a, T* __restrict__ b,
                             const int* __restrict__ slc, int R, int maxc) {
     const int stride = 2 * maxc + 16;
     for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < R * maxc; e += gridDim.x * blockDim.x) {
         const int r = e / maxc, i = e - r * maxc;
         if (i < slc[2 * r + 1]) {
-            a[slc[2 * r] + i] = recv[(size_t)r * stride + 2 * i];
-            b[slc[2 * r] + i] = recv[(size_t)r * stride + 2 * i + 1];
+            a[slc[2 * r] + i] = (T)recv[(size_t)r * stride + 2 * i];
+            b[slc[2 * r] + i] = (T)recv[(size_t)r * stride + 2 * i + 1];
         }
     }
 }

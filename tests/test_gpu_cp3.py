@@ -107,6 +107,26 @@ def test_cp3_early_stop_and_batches():
     assert trace_rel_err(e1, e2) <= 1e-10
 
 
+@pytest.mark.parametrize("cfg", ["c2", "c4", "chain"])
+def test_cp3_split_matches_fused(cfg):
+    """The split task layout (RAOCP_CP3_SPLIT=1, default on small trees: leaves as tasks of
+    their own, the family recomputing only their SOC scalars) against the fused family
+    tiles: the same arithmetic per entry, so the runs agree to rounding (1e-10)."""
+    r = _recipe(cfg)
+    tree, prob = build_problem(r)
+    a = _with_env({"RAOCP_CP3_SPLIT": "1"}, lambda: core.Cache(prob))
+    b = _with_env({"RAOCP_CP3_SPLIT": "0"}, lambda: core.Cache(prob))
+    alpha = 0.999 / a.native.step_size()
+    K = 10 if cfg == "c4" else 20
+    out = []
+    for cache in (a, b):
+        st, err, derr = cache.native.cp_run(r["x0"], K, 0.0, alpha)
+        out.append((st, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
+    (s1, e1, d1, z1, y1), (s2, e2, d2, z2, y2) = out
+    assert s1 == s2 and trace_rel_err(e1, e2) <= 1e-10 and trace_rel_err(d1, d2) <= 1e-10
+    assert rel_err(z1, z2) <= 1e-11 and rel_err(y1, y2) <= 1e-11
+
+
 @pytest.mark.parametrize("cfg", ["c2", "c4", "c5"])
 def test_cp3_fp32_drift_vs_fp64(cfg):
     """30 fp32 CP iterations (k_cp3<float, ...>) against the fp64 run of the same problem and

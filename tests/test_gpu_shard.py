@@ -10,7 +10,7 @@ reference run sets RAOCP_CP3=0; the per-node arithmetic is identical and only ma
 reductions are regrouped, which is exact), stay within 1e-10 of the default fused
 unsharded solve (k_cp3: other summation order) and match the oracle within the
 north_star tolerance. Configs 2 (the headline tree) and 4 (the tree the sharded bench leg
-runs, BASELINE configs[3]) at R = 2, 4, 8.
+runs, BASELINE configs[3]) at R = 2, 4, 8; config 5 in fp32 (BASELINE configs[4]) at R = 2, 4.
 """
 import os
 
@@ -139,3 +139,48 @@ def test_rccl_transport_single_rank():
                          text=True, timeout=300, env=env)
     assert res.returncode == 0, res.stdout[-2000:] + res.stderr[-2000:]
     assert "bit-identical" in res.stdout
+
+
+@pytest.mark.parametrize("R", [2, 4])
+def test_fp32_sharded_config5_matches_unsharded(R):
+    """BASELINE configs[4] ("fp32, 8 x MI355X"): one config-5 tree in fp32 split across R
+    shards. The per-stage streaming sweep (raocp_dyn3.hip) runs the owned parents of every
+    stage below the cut and the replicated top, exchanging the roots' q rows (X2, fp32);
+    the CP kernels k_cpd2 / k_cpp2<float> run the owned families with the X1 exchange. The
+    residual history and the owned iterate equal the unsharded fp32 solve on the same
+    kernels bit for bit (only max reductions are regrouped); the default fused unsharded
+    solve (k_cp3<float>) agrees to fp32 rounding (1e-4 per trace entry)."""
+    r = recipe_config(5, seed=0)
+    tree, prob = build_problem(r)
+    old = os.environ.get("RAOCP_CP3")
+    os.environ["RAOCP_CP3"] = "0"
+    try:
+        base = core.Cache(prob, dtype="float32")
+        shards = [core.Cache(prob, dtype="float32") for _ in range(R)]
+    finally:
+        if old is None:
+            os.environ.pop("RAOCP_CP3", None)
+        else:
+            os.environ["RAOCP_CP3"] = old
+    assert base.native.kernel_info(9).startswith("k_dy3_back<float")
+    alpha = 0.999 / base.native.step_size(rtol=1e-7)
+    iters = 6
+    st0, err0, derr0 = base.native.cp_run(r["x0"], iters, 0.0, alpha)
+    z0 = base.get_primal_flat()
+    for k, s in enumerate(shards):
+        s.native.shard(k, R)
+    st, err, derr = group_cp_run([s.native for s in shards], r["x0"], iters, 0.0, alpha)
+    assert st == st0 and err.shape == err0.shape == (iters + 1, 3)
+    assert np.array_equal(err, err0) and np.array_equal(derr, derr0)
+    nx = base.packed.nx
+    covered = np.zeros(tree.num_nodes, dtype=bool)
+    for s in shards:
+        z = s.get_primal_flat()
+        for (a, b) in _owned_x_slices(s.native):
+            if b > a:
+                np.testing.assert_array_equal(z[a * nx:b * nx], z0[a * nx:b * nx])
+                covered[a:b] = True
+    assert covered.all()
+    fused = core.Cache(prob, dtype="float32")
+    stf, errf, _ = fused.native.cp_run(r["x0"], iters, 0.0, alpha)
+    assert stf == st0 and np.max(np.abs(errf - err0) / np.abs(err0)) <= 1e-4

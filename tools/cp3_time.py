@@ -20,13 +20,16 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
     alpha = 0.999 / nat.step_size(rtol=1e-7 if cfg == 5 else 1e-14)
     K = {2: 480, 4: 120, 5: 24}[cfg]
     ms = nat.cp_bench(r["x0"], K, alpha)
-    var = ",".join(f"{k[6:]}={os.environ[k]}" for k in ("RAOCP_CP3", "RAOCP_DYN3") if k in os.environ) or "default"
-    print(f"config {cfg} {var:8s} {nat.kernel_info(10):40s} {nat.kernel_info(9)[:34]:34s} "
+    var = ",".join(f"{k[6:]}={os.environ[k]}" for k in ("RAOCP_CP3", "RAOCP_CP3_SPLIT", "RAOCP_DYN3")
+                   if k in os.environ) or "default"
+    print(f"config {cfg} {var:12s} {nat.kernel_info(10):40s} {nat.kernel_info(9)[:34]:34s} "
           f"cp {1e3 * t10:8.1f} us  dyn {1e3 * t9:8.1f} us  loop {1e3 * ms / K:8.1f} us/it", flush=True)
     sys.exit(0)
 cfgs = sys.argv[1:] or ["2", "4", "5"]
 for cfg in cfgs:
-    for v in ({}, {"RAOCP_CP3": "0"}) + (({"RAOCP_DYN3": "1"},) if cfg != "5" else ({"RAOCP_DYN3": "0"},)):
+    variants = [{}, {"RAOCP_CP3": "0"}, {"RAOCP_CP3_SPLIT": "1" if cfg != "2" else "0"}]
+    variants.append({"RAOCP_DYN3": "1"} if cfg != "5" else {"RAOCP_DYN3": "0"})
+    for v in variants:
         env = dict(os.environ, **v)
         out = subprocess.run([sys.executable, __file__, "child", cfg], env=env, capture_output=True, text=True,
                              timeout=300)
