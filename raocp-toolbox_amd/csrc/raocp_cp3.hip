@@ -16,8 +16,9 @@
 //   phase 1  parent rows: L products sqrtQ (2x+ - p), sqrtQ (x+ - p) (and sqrtR on u) as MFMA
 //            tiles; eta7 (box), eta1 / eta2 (AVaR cone) and their L^T terms on y
 //   phase 2  per child slot k: the SOC of (eta3, eta4, eta5 | eta6), eta+ / xi2 in registers,
-//            and L^T of (eta+, d - eta+, xi2) accumulated per parent by a second MFMA chain
-//   phase 3  x_i, u_i of the next half step and their residuals
+//            (eta+, d - eta+, xi2) of the children summed per parent
+//   phase 3  eta7 (box) and x_i, u_i of the next half step with their residuals: L^T of the
+//            summed child rows (one sqrtQ over the children) as a second MFMA chain
 //   phase 4  (parents of leaves, run first) per leaf slot: the leaf SOC (eta11, eta12 | eta13),
 //            eta14 box, and the leaf's x row of the next half step (sqrtPf MFMA chains)
 //   phase 5  s_j of the children (eta2_j of a nonleaf child recomputed here, bit-identical
@@ -403,9 +404,6 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
         }
         // L products of the parent: a = L(2z+ - p), b = L(z+ - p) on the children's rows
         v4 qa[RX], qb[RX], ua[RU], ub[RU];
-        // L^T accumulators of x_i / u_i over (eta+, d - eta+, xi2), starting from Gamma' eta7
-        // (operators.py:73-78: C7' eta7 first, then the children in order)
-        v4 gxA[RX], gxW[RX], gxC[RX], guA[RU], guW[RU], guC[RU];
         {
             // the parent's x, u rows (reloaded in phase 3: registers, not HBM, are short here)
             T xz[RX][4], xp[RX][4], uz[RU][4], up[RU][4];
@@ -413,9 +411,6 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             ld_rows<T, NX>(pz + p.X0 + (size_t)i * NX, live, xp);
             ld_rows<T, NU>(zp + p.U0 + (size_t)i * NU, live, uz);
             ld_rows<T, NU>(pz + p.U0 + (size_t)i * NU, live, up);
-            T d7x[RX][4], d7u[RU][4];
-            ld_rows<T, NX>(d + (o7 >= 0 ? o7 : 0), o7 >= 0, d7x);
-            ld_rows<T, NU>(d + (o7 >= 0 ? o7 + NX : 0), o7 >= 0, d7u);
             T a1[RX][4], a2[RX][4];
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 a1[rt][e] = T(2) * xz[rt][e] - xp[rt][e];
@@ -432,44 +427,15 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) ua[rt] = ub[rt] = v4{0, 0, 0, 0};
             mmt(wr, c1, ua);
             mmt(wr, c2, ub);
-            const int bi = o7 >= 0 ? p.iBnl[i] : 0;
-            cglbp<T> blo = (cglbp<T>)p.blo_nl + (size_t)bi * (NX + NU), bhi = (cglbp<T>)p.bhi_nl + (size_t)bi * (NX + NU);
-            T lx[RX][4], hx[RX][4], lu[RU][4], hu[RU][4];
-            ld_rows<T, NX>(blo, o7 >= 0, lx);
-            ld_rows<T, NX>(bhi, o7 >= 0, hx);
-            ld_rows<T, NU>(blo + NX, o7 >= 0, lu);
-            ld_rows<T, NU>(bhi + NX, o7 >= 0, hu);
-            T e7[RX][4];
-            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) {
-                _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    T ep = T(0), x2 = T(0);
-                    if (o7 >= 0 && tok<NX>(rt, e)) {
-                        const T v = (d7x[rt][e] + alpha * (T(2) * xz[rt][e] - xp[rt][e])) * ra;
-                        fin(d7x[rt][e], v, box_apply_t(v, lx[rt][e], hx[rt][e], ctl), xz[rt][e] - xp[rt][e], ep, x2);
-                    }
-                    e7[rt][e] = ep;
-                    gxA[rt][e] = ep;
-                    gxW[rt][e] = d7x[rt][e] - ep;
-                    gxC[rt][e] = x2;
-                }
-            }
-            st_rows<T, NX>(eo + (o7 >= 0 ? o7 : 0), o7 >= 0, e7);
-            T e7u[RU][4];
-            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) {
-                _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    T ep = T(0), x2 = T(0);
-                    if (o7 >= 0 && tok<NU>(rt, e)) {
-                        const T v = (d7u[rt][e] + alpha * (T(2) * uz[rt][e] - up[rt][e])) * ra;
-                        fin(d7u[rt][e], v, box_apply_t(v, lu[rt][e], hu[rt][e], ctl), uz[rt][e] - up[rt][e], ep, x2);
-                    }
-                    e7u[rt][e] = ep;
-                    guA[rt][e] = ep;
-                    guW[rt][e] = d7u[rt][e] - ep;
-                    guC[rt][e] = x2;
-                }
-            }
-            st_rows<T, NU>(eo + (o7 >= 0 ? o7 + NX : 0), o7 >= 0, e7u);
         }
+        // the children's (eta+, d - eta+, xi2) eta3 / eta4 rows summed per parent in registers:
+        // with one sqrtQ / sqrtR over the children, L^T's sum over them is one product of the
+        // summed rows (one MFMA chain per stream and family instead of one per child)
+        T sxA[RX][4], sxW[RX][4], sxC[RX][4], suA[RU][4], suW[RU][4], suC[RU][4];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+            sxA[rt][e] = sxW[rt][e] = sxC[rt][e] = T(0);
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+            suA[rt][e] = suW[rt][e] = suC[rt][e] = T(0);
         // ---------------- phase 2: child slots (child block SOC, L^T accumulation), the next
         // slot's rows loaded before the current slot's arithmetic
         for (int k = 0; k < C; ++k) {
@@ -505,9 +471,11 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
                 e3C[rt][e] = x2;
             }
             st_rows<T, NX>(eo + e3(p, live ? j : 1), live, e3A);
-            mmt(wq, e3A, gxA);
-            mmt(wq, e3W, gxW);
-            mmt(wq, e3C, gxC);
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                sxA[rt][e] += e3A[rt][e];
+                sxW[rt][e] += e3W[rt][e];
+                sxC[rt][e] += e3C[rt][e];
+            }
             T e4A[RU][4], e4W[RU][4], e4C[RU][4];
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 T ep = T(0), x2 = T(0);
@@ -518,9 +486,11 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
                 e4C[rt][e] = x2;
             }
             st_rows<T, NU>(eo + e4(p, live ? j : 1), live, e4A);
-            mmt(wr, e4A, guA);
-            mmt(wr, e4W, guW);
-            mmt(wr, e4C, guC);
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                suA[rt][e] += e4A[rt][e];
+                suW[rt][e] += e4W[rt][e];
+                suC[rt][e] += e4C[rt][e];
+            }
             // eta5 / eta6 and tau_j of the half step (before the kernel projection)
             T ep5, x25, ep6, x26;
             fin(d5, v5, soc_apply_t(v5, false, nf, tt), b5, ep5, x25);
@@ -555,13 +525,60 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             }
             if (k + 1 < C) ccu = cnx;
         }
-        // ---------------- phase 3: x_i, u_i of the half step
+        // ---------------- phase 3: eta7 (box on [x_i; u_i]) and x_i, u_i of the half step:
+        // L^T = Gamma' eta7 + sqrtQ (sum of the children's eta3) (operators.py:73-85)
         {
             T xz[RX][4], xp[RX][4], uz[RU][4], up[RU][4];
             ld_rows<T, NX>(zp + p.X0 + (size_t)i * NX, live, xz);
             ld_rows<T, NX>(pz + p.X0 + (size_t)i * NX, live, xp);
             ld_rows<T, NU>(zp + p.U0 + (size_t)i * NU, live, uz);
             ld_rows<T, NU>(pz + p.U0 + (size_t)i * NU, live, up);
+            T d7x[RX][4], d7u[RU][4];
+            ld_rows<T, NX>(d + (o7 >= 0 ? o7 : 0), o7 >= 0, d7x);
+            ld_rows<T, NU>(d + (o7 >= 0 ? o7 + NX : 0), o7 >= 0, d7u);
+            const int bi = o7 >= 0 ? p.iBnl[i] : 0;
+            cglbp<T> blo = (cglbp<T>)p.blo_nl + (size_t)bi * (NX + NU), bhi = (cglbp<T>)p.bhi_nl + (size_t)bi * (NX + NU);
+            v4 gxA[RX], gxW[RX], gxC[RX], guA[RU], guW[RU], guC[RU];
+            {
+                T lx[RX][4], hx[RX][4], e7[RX][4];
+                ld_rows<T, NX>(blo, o7 >= 0, lx);
+                ld_rows<T, NX>(bhi, o7 >= 0, hx);
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                    T ep = T(0), x2 = T(0);
+                    if (o7 >= 0 && tok<NX>(rt, e)) {
+                        const T v = (d7x[rt][e] + alpha * (T(2) * xz[rt][e] - xp[rt][e])) * ra;
+                        fin(d7x[rt][e], v, box_apply_t(v, lx[rt][e], hx[rt][e], ctl), xz[rt][e] - xp[rt][e], ep, x2);
+                    }
+                    e7[rt][e] = ep;
+                    gxA[rt][e] = ep;
+                    gxW[rt][e] = d7x[rt][e] - ep;
+                    gxC[rt][e] = x2;
+                }
+                st_rows<T, NX>(eo + (o7 >= 0 ? o7 : 0), o7 >= 0, e7);
+            }
+            {
+                T lu[RU][4], hu[RU][4], e7u[RU][4];
+                ld_rows<T, NU>(blo + NX, o7 >= 0, lu);
+                ld_rows<T, NU>(bhi + NX, o7 >= 0, hu);
+                _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                    T ep = T(0), x2 = T(0);
+                    if (o7 >= 0 && tok<NU>(rt, e)) {
+                        const T v = (d7u[rt][e] + alpha * (T(2) * uz[rt][e] - up[rt][e])) * ra;
+                        fin(d7u[rt][e], v, box_apply_t(v, lu[rt][e], hu[rt][e], ctl), uz[rt][e] - up[rt][e], ep, x2);
+                    }
+                    e7u[rt][e] = ep;
+                    guA[rt][e] = ep;
+                    guW[rt][e] = d7u[rt][e] - ep;
+                    guC[rt][e] = x2;
+                }
+                st_rows<T, NU>(eo + (o7 >= 0 ? o7 + NX : 0), o7 >= 0, e7u);
+            }
+            mmt(wq, sxA, gxA);
+            mmt(wq, sxW, gxW);
+            mmt(wq, sxC, gxC);
+            mmt(wr, suA, guA);
+            mmt(wr, suW, guW);
+            mmt(wr, suC, guC);
             T ox[RX][4], ou[RU][4];
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
                 ox[rt][e] = xz[rt][e] - alpha * gxA[rt][e];
