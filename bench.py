@@ -99,15 +99,22 @@ def kernel_bytes(cache, w=8):
 def pmc_traffic(kernel):
     """HBM bytes per launch of `kernel` from the newest committed PMC summary
     (profiles/<round>/traffic.json, written by tools/traffic.py from rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes of this bench), or None."""
+    WRITE_SIZE passes of this bench), or None. `kernel` may list several launches as
+    "name xcount" terms joined by " + " (raocp_kernel_info of the dynamics projection):
+    their per-launch traffic is summed."""
     import glob
+    import re
+    terms = []
+    for t in kernel.split(" + "):
+        m = re.fullmatch(r"(.*) x(\d+)", t.strip())
+        terms.append((m.group(1), int(m.group(2))) if m else (t.strip(), 1))
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json")), reverse=True):
         try:
-            k = json.load(open(f))["kernels"].get(kernel)
+            ks = json.load(open(f))["kernels"]
         except Exception:
             continue
-        if k:
-            return k["traffic_bytes"], os.path.relpath(f, ROOT)
+        if all(name in ks for name, _ in terms):
+            return sum(cnt * ks[name]["traffic_bytes"] for name, cnt in terms), os.path.relpath(f, ROOT)
     return None, None
 
 
@@ -358,7 +365,7 @@ def iteration_kernels(nat, cache, w, reps, dev_ms_per_step):
     for k in kernels.values():
         k["share_of_step"] = k["us_per_launch"] / dev_us if dev_us > 0 else None
     dom = max(kernels, key=lambda k: kernels[k]["us_per_launch"])
-    traffic, src = pmc_traffic(kernels[dom]["kernel"]) if dom == "cp" else (None, None)
+    traffic, src = pmc_traffic(kernels[dom]["kernel"])
     roofline = {"bound": "hbm", "kernel": kernels[dom]["kernel"], "part": dom, "achieved": kernels[dom]["achieved"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kernels[dom]["frac"], "traffic": traffic,
                 "traffic_source": src, "bytes_per_launch": kernels[dom]["bytes_per_launch"],

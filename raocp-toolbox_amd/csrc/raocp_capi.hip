@@ -634,33 +634,39 @@ struct Cpp2Op {
                                                                                 c->redpart, c->cp2_nbF);
     }
 };
+// the node-block kernels (raocp_cp.hip): fp64 at every size; fp32 contexts whose CP blocks
+// mix weight tables (per-mode costs) at runtime sizes
+template <class T>
 struct CpdOp {
     template <int NX, int NU>
     void run(raocp_ctx* c) {
-        auto k = raocp::k_cpd<NX, NU>;
+        auto k = raocp::k_cpd<T, NX, NU>;
         allow_lds(k, c->lds_cpd);
         k<<<c->cp_nbF + c->cp_nbL, kBlock, c->lds_cpd, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2, c->redpart,
                                                                      c->cp_nbF);
     }
 };
+template <class T>
 struct CppOp {
     // fuse: the stopping test rides on the launch's last block (the CP iteration only)
     template <int NX, int NU>
     void run(raocp_ctx* c, bool fuse) {
-        auto k = raocp::k_cpp<NX, NU>;
+        auto k = raocp::k_cpp<T, NX, NU>;
         allow_lds(k, c->lds_cpp);
         k<<<c->cp_nbF + c->cp_nbL, kBlock, c->lds_cpp, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2, c->redpart,
                                                                      c->cp_nbF, c->hist, fuse ? c->ticket : nullptr);
     }
 };
 void launch_cpd(raocp_ctx* c) {
-    if (c->f32) dispatch_rt(c->nx, c->nu, Cpd2Op<float>{}, c);
-    else if (c->cp_v1) dispatch(c->nx, c->nu, CpdOp{}, c);
+    if (c->f32 && c->cp_v1) CpdOp<float>{}.run<0, 0>(c);
+    else if (c->f32) dispatch_rt(c->nx, c->nu, Cpd2Op<float>{}, c);
+    else if (c->cp_v1) dispatch(c->nx, c->nu, CpdOp<double>{}, c);
     else dispatch_rt(c->nx, c->nu, Cpd2Op<double>{}, c);
 }
 void launch_cpp(raocp_ctx* c, bool fuse = false) {
-    if (c->f32) dispatch_rt(c->nx, c->nu, Cpp2Op<float>{}, c);
-    else if (c->cp_v1 || fuse) dispatch(c->nx, c->nu, CppOp{}, c, fuse);
+    if (c->f32 && c->cp_v1) CppOp<float>{}.run<0, 0>(c, fuse);
+    else if (c->f32) dispatch_rt(c->nx, c->nu, Cpp2Op<float>{}, c);
+    else if (c->cp_v1 || fuse) dispatch(c->nx, c->nu, CppOp<double>{}, c, fuse);
     else dispatch_rt(c->nx, c->nu, Cpp2Op<double>{}, c);
 }
 // the fused CP iteration (raocp_cp3.hip): compile-time sizes of the benchmark configs
@@ -870,18 +876,41 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             if (c->ellt3_C && big) return "k_ellt3<" + T + ", " + nn + ", " + std::to_string(4 / c->ellt3_C) + ">";
             return c->f32 ? "k_ellt2<float, " + rr + ">" : "k_ell_t<" + nn + ">";
         case 2:
-            if (!c->f32 && c->cp_v1) return "k_cpd<" + nn + ">";
+            if (c->cp_v1) return "k_cpd<" + T + ", " + (c->f32 ? std::string("0, 0") : nn) + ">";
             return "k_cpd2<" + T + ", " + rr + ">";
         case 6:
-            if (!c->f32 && c->cp_v1) return "k_cpp<" + nn + ">";
+            if (c->cp_v1) return "k_cpp<" + T + ", " + (c->f32 ? std::string("0, 0") : nn) + ">";
             return "k_cpp2<" + T + ", " + rr + ">";
-        case 9:
-            if (c->dyn3)
-                return "k_dy3_back<" + T + ", " + nn + "> + k_dy3_fwd<" + T + ", " + nn + "> (per stage)";
-            if (c->dyn2) return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
-            if (c->cut > 0)
-                return "k_dyn_bottom_back + k_dyn_top + k_dyn_bottom_fwd (" + std::to_string(c->tiers.size()) + " tiers)";
-            return "k_dyn_gather + k_dyn_stage_a / _b / _f (per stage)";
+        case 9: {
+            // the launches of one projection as "name xcount" terms (bench.py sums the PMC
+            // traffic of these terms)
+            std::vector<std::pair<std::string, int>> terms;
+            auto add = [&](const std::string& k) {
+                for (auto& t : terms)
+                    if (t.first == k) {
+                        ++t.second;
+                        return;
+                    }
+                terms.push_back({k, 1});
+            };
+            auto b = [](bool v) { return std::string(v ? "true" : "false"); };
+            if (c->dyn3) {  // one backward and one forward launch per nonleaf stage
+                for (int t = 0; t < c->N; ++t) add("k_dy3_back<" + T + ", " + nn + ">");
+                for (int t = 0; t < c->N; ++t) add("k_dy3_fwd<" + T + ", " + nn + ">");
+            } else if (c->dyn2) {
+                return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
+            } else if (c->cut > 0) {
+                for (int k = (int)c->tiers.size() - 1; k >= 0; --k)
+                    add("k_dyn_bottom_back<" + nn + ", " + b(c->tiers[k].fold) + ">");
+                add("k_dyn_top<" + nn + ", " + b(c->f_lds_top) + ", " + b(c->fold_top) + ">");
+                for (const auto& tp : c->tiers) add("k_dyn_bottom_fwd<" + nn + ", " + b(tp.fl) + ">");
+            } else {
+                return "k_dyn_gather + k_dyn_stage_a / _b / _f (per stage)";
+            }
+            std::string s;
+            for (const auto& t : terms) s += (s.empty() ? "" : " + ") + t.first + " x" + std::to_string(t.second);
+            return s;
+        }
         case 10:
             if (c->cp3) return "k_cp3<" + T + ", " + nn + ">";
             return kernel_name(c, 2) + " + " + kernel_name(c, 6);
@@ -1222,9 +1251,6 @@ int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& prange
                 c->cp_v1 = true;
         for (int b = 0; b < c->cp2_nbL; ++b)
             if (leaf2[raocp::kCpLeafRecs * b + 1].x < 0) c->cp_v1 = true;
-        if (c->f32 && c->cp_v1)
-            return fail(RAOCP_ERR_ARG, "fp32 contexts need the nodes of every CP block on one weight table "
-                                       "(costs that differ per mode within a family)");
         c->lds_cpd2 = (size_t)nd2;
         c->lds_cpp2 = (size_t)np2;
         c->cp_rows = c->cp_v1 ? c->cp_nbF + c->cp_nbL : c->cp2_nbF + c->cp2_nbL;
@@ -1931,8 +1957,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             // 23.6 us for k_cpd / k_cpp); from ~4k tiles the MFMA kernels win (config 4:
             // 200 / 196 us vs 210 / 318 us; config 3 464 vs 505 us per iteration)
             c->cp_v1 = (long)(n - 1 + 15) / 16 + (long)(n - m + 15) / 16 < 4096;
+            if (c->f32) c->cp_v1 = false;  // fp32: the MFMA kernels unless blocks mix weight tables
             if (const char* e = getenv("RAOCP_CP_V1")) c->cp_v1 = atoi(e) != 0;
-            if (c->f32) c->cp_v1 = false;  // only the T-templated kernels run fp32
         }
         if ((rc = build_cp_blocks(c, allp, alll))) return bail(rc);
     }
@@ -2578,6 +2604,9 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
     DevGuard dg_(c);
     if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c || !out || cap <= 0) return fail(RAOCP_ERR_ARG, "bad argument");
+    // the tiered sweep stamps 64 slots per launch (2 per tier + the top)
+    if (c->cut > 0 && (size_t)cap < 64 * (2 * c->tiers.size() + 1))
+        return fail(RAOCP_ERR_ARG, "stamp buffer too small: 64 slots per dynamics launch");
     unsigned long long* st = nullptr;
     int rc = c->alloc(&st, (size_t)cap);
     if (rc) return rc;

@@ -904,8 +904,8 @@ __global__ void __launch_bounds__(kBlock) k_cp_dual(Dev p, Ctl* __restrict__ ctl
     }
 }
 
-#include "raocp_cp.hip"
 #include "raocp_cp2.hip"
+#include "raocp_cp.hip"
 #include "raocp_ell2.hip"
 #include "raocp_ell3.hip"
 #include "raocp_cp3.hip"

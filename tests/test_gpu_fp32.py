@@ -12,7 +12,7 @@ import pytest
 
 import raocp.core as core
 from raocp.problems import build_problem, recipe_config
-from helpers import problem_from_golden, rel_err
+from helpers import problem_from_golden, rel_err, trace_rel_err
 
 pytestmark = pytest.mark.gpu
 
@@ -62,13 +62,69 @@ def test_fp32_step_size_close_to_fp64():
     assert abs(l32 - l64) <= 1e-5 * l64
 
 
-def test_fp32_rejects_mixed_weight_blocks(golden):
-    """ops2x2 has a different cost per mode, so a family's children use different sqrtQ
-    tables: the fp32 MFMA blocks need one table per block, and context creation says so."""
+def _cp_drift(c32, c64, x0, K):
+    """K + 1 CP iterations of an fp32 and an fp64 context with the fp64 step size: relative
+    trace errors (per entry) and iterate errors (to the largest entry)."""
+    alpha = 0.999 / c64.native.step_size()
+    s32, e32, d32 = c32.native.cp_run(x0, K, 0.0, alpha)
+    s64, e64, d64 = c64.native.cp_run(x0, K, 0.0, alpha)
+    assert s32 == s64 == 1 and e32.shape == e64.shape == (K + 1, 3)
+    return (trace_rel_err(e32, e64), trace_rel_err(d32, d64), rel_err(c32.get_primal_flat(), c64.get_primal_flat()),
+            rel_err(c32.get_dual_flat(), c64.get_dual_flat()), alpha, e64)
+
+
+def test_fp32_mixed_weight_tables_ops2x2(golden):
+    """ops2x2 has a different cost per mode (raocp_spec.py:118-131, with_markovian_nonleaf_costs),
+    so a family's children use different sqrtQ / sqrtR tables: fp32 contexts run the node-block
+    kernels k_cpd / k_cpp<float> (raocp_cp.hip), which read a table per child. 30 iterations
+    against the fp64 context and the oracle (fp64): traces within 1e-4 per entry, iterates
+    within 1e-5 of the largest entry (fp32 rounding over 30 iterations)."""
+    from oracle.raocp_oracle import OracleProblem
     r, tree, prob = problem_from_golden(golden("ops_kat"), "ops2x2")
-    from raocp.core._native import RaocpError
-    with pytest.raises(RaocpError, match="one weight table"):
-        core.Cache(prob, dtype="float32")
+    c32, c64 = core.Cache(prob, dtype="float32"), core.Cache(prob)
+    assert c32.native.kernel_info(10) == "k_cpd<float, 0, 0> + k_cpp<float, 0, 0>"
+    K = 29
+    te, td, zr, er, alpha, e64 = _cp_drift(c32, c64, r["x0"], K)
+    print(f"fp32 mixed ops2x2: traces {te:.2e} / {td:.2e}, iterate {zr:.2e} / {er:.2e}")
+    assert te <= 1e-4 and td <= 1e-4 and zr <= 1e-5 and er <= 1e-5
+    _, eo, _, zo, _, _ = OracleProblem(prob).chock(r["x0"], max_iters=K, tol=0.0, alpha=alpha)
+    assert trace_rel_err(e64, eo) <= 1e-8
+    assert rel_err(c32.get_primal_flat(), zo) <= 1e-5
+
+
+def test_fp32_mixed_weight_tables_config4_modes():
+    """Config 4 with a cost per mode (the consecutive children of every family on different
+    tables, as in test_gpu_parity's "4-modes"): fp32 k_cpd / k_cpp<float> against the fp64
+    context over 20 iterations (traces 1e-4 per entry, iterates 1e-5)."""
+    r = recipe_config(4)
+    r["Q"] = np.array([(1.0 + k) * q for k, q in enumerate(r["Q"])])
+    r["R"] = np.array([(2.0 + k) * q for k, q in enumerate(r["R"])])
+    tree, prob = build_problem(r)
+    c32, c64 = core.Cache(prob, dtype="float32"), core.Cache(prob)
+    assert c32.native.kernel_info(10).startswith("k_cpd<float")
+    te, td, zr, er, _, _ = _cp_drift(c32, c64, r["x0"], 19)
+    print(f"fp32 mixed config 4: traces {te:.2e} / {td:.2e}, iterate {zr:.2e} / {er:.2e}")
+    assert te <= 1e-4 and td <= 1e-4 and zr <= 1e-5 and er <= 1e-5
+
+
+def test_fp32_node_block_kernels_match_mfma_kernels():
+    """RAOCP_CP_V1=1 forces k_cpd / k_cpp<float> on a tree with one table per block
+    (config 2): the same iterations as the fused fp32 k_cp3 up to fp32 rounding."""
+    import os
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    os.environ["RAOCP_CP_V1"] = "1"
+    os.environ["RAOCP_CP3"] = "0"
+    try:
+        v1 = core.Cache(prob, dtype="float32")
+    finally:
+        del os.environ["RAOCP_CP_V1"], os.environ["RAOCP_CP3"]
+    v3 = core.Cache(prob, dtype="float32")
+    assert v1.native.kernel_info(10).startswith("k_cpd<float")
+    assert v3.native.kernel_info(10).startswith("k_cp3<float")
+    te, td, zr, er, _, _ = _cp_drift(v1, v3, r["x0"], 19)
+    print(f"fp32 v1 vs k_cp3 config 2: traces {te:.2e} / {td:.2e}, iterate {zr:.2e} / {er:.2e}")
+    assert te <= 1e-4 and td <= 1e-4 and zr <= 1e-5 and er <= 1e-5
 
 
 def test_fp32_dynamics_projection_config5(c5):

@@ -12,9 +12,9 @@ cache = core.Cache(prob)
 cache.cache_initial_state(r["x0"])
 cache.set_primal_flat(np.random.default_rng(0).standard_normal(cache.primal_size))
 for rep in range(5):
-    st = cache.native.debug_dyn_stamps(64 * 16).astype(np.int64).reshape(16, 64)
+    st = cache.native.debug_dyn_stamps(64 * 64).astype(np.int64).reshape(64, 64)
 t0 = st[0, 0]
-for k in range(16):
+for k in range(64):
     row = st[k]
     n = np.count_nonzero(row)
     if n == 0:
