@@ -71,6 +71,7 @@ struct raocp_ctx {
     // class per stage; fp32 contexts by default, fp64 opt-in RAOCP_DYN3=1
     bool dyn3 = false;
     std::vector<raocp::Dy3Stage> d3st;
+    double *d3img_b = nullptr, *d3img_f = nullptr;  // per-stage table images (k_dy3_image)
     std::vector<raocp::Dy3Stage> d3own;  // a shard's stages (owned parent ranges below its cut)
     int wsz = 8;                 // bytes per scalar of the iterate
     hipStream_t stream = nullptr;
@@ -99,7 +100,7 @@ struct raocp_ctx {
     struct TierPlan {            // a tier [s0, s1) below the top: one workgroup per subtree
         int s0, s1, nsub, maxch;
         size_t lds_b, lds_f;
-        bool fl;                 // F staged in LDS by the forward kernel
+        int fm;                  // F in the forward kernel: 0 global, 1 LDS, 2 LDS per level
         bool fold;               // one-phase backward levels (WT tables)
         const raocp::Rec* lv;    // level ranges of its subtrees
         raocp::TierArg ta;       // the same, as a kernel argument, when the tier is regular
@@ -420,11 +421,12 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
     allow_lds(kb, lb);
     allow_lds(kf, lf);
     // stages of few tiles run slot-parallel (a wave per child slot): the dependent MFMA chain
-    // of a tile is what a small stage costs
-    auto coop = [&](const raocp::Dy3Stage& st) { return (st.i1 - st.i0 + 15) / 16 * C <= 256 * wpb; };
-    auto grid = [&](const raocp::Dy3Stage& st, bool back) {
+    // of a tile is what a small stage costs. Decided on the whole stage, so a shard sums a
+    // parent's child slots in the same order as the unsharded sweep (bit-identical results).
+    auto coop = [&](int t) { return (c->d3st[t].i1 - c->d3st[t].i0 + 15) / 16 * C <= 256 * wpb; };
+    auto grid = [&](const raocp::Dy3Stage& st, int t, bool back) {
         const int tiles = (st.i1 - st.i0 + 15) / 16;
-        if (coop(st)) return std::max(1, back ? tiles : (tiles * C + wpb - 1) / wpb);
+        if (coop(t)) return std::max(1, back ? tiles : (tiles * C + wpb - 1) / wpb);
         return std::max(1, std::min(cap, (tiles + wpb - 1) / wpb));
     };
     const int N = c->N, S = c->sh_S;  // S > 0: a shard owns the stages >= S partly
@@ -436,15 +438,43 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
         if (st.i1 <= st.i0) continue;
         raocp::ChkArg ca{};
         if (ck && t == N - 1) ca = *ck;
-        kb<<<grid(st, true) + ca.on, thr, lb, c->stream>>>(c->dev, ctl, ca, z, c->Q2, c->Dd2, st, C, c->W2, c->RG2,
-                                                          coop(st) ? 1 : 0);
+        const double* img = (const double*)((const char*)c->d3img_b + (size_t)t * L::back_n(C) * sizeof(T));
+        kb<<<grid(st, t, true) + ca.on, thr, lb, c->stream>>>(c->dev, ctl, ca, z, c->Q2, c->Dd2, st, C, img,
+                                                             coop(t) ? 1 : 0);
     }
     if (part == 1) return;
     for (int t = 0; t < N; ++t) {
         const raocp::Dy3Stage& st = stage(t);
         if (st.i1 <= st.i0) continue;
-        kf<<<grid(st, false), thr, lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, st, C, c->KM2, c->F2, coop(st) ? 1 : 0);
+        const double* img = (const double*)((const char*)c->d3img_f + (size_t)t * L::fwd_n(C) * sizeof(T));
+        kf<<<grid(st, t, false), thr, lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, st, C, img, coop(t) ? 1 : 0);
     }
+}
+// the per-stage table images of the sweep, laid out once (k_dy3_image, one workgroup per stage)
+template <class T, int NX, int NU>
+int dyn3_imagest(raocp_ctx* c) {
+    typedef raocp::Dy3Lds<T, NX, NU> L;
+    const int C = c->unif_branch, N = (int)c->d3st.size();
+    const size_t nb = (size_t)L::back_n(C) * sizeof(T) / 8, nf = (size_t)L::fwd_n(C) * sizeof(T) / 8;
+    int rc;
+    if ((rc = c->alloc(&c->d3img_b, std::max<size_t>(1, N * nb))) || (rc = c->alloc(&c->d3img_f, std::max<size_t>(1, N * nf))))
+        return rc;
+    for (int t = 0; t < N; ++t)
+        raocp::k_dy3_image<T, NX, NU><<<1, 512, 0, c->stream>>>(c->d3st[t], C, c->W2, c->RG2, c->KM2, c->F2,
+                                                                c->d3img_b + t * nb, c->d3img_f + t * nf);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+int dyn3_images(raocp_ctx* c) {
+    if (c->f32) {
+        if (c->nx == 20) return dyn3_imagest<float, 20, 8>(c);
+        if (c->nx == 32) return dyn3_imagest<float, 32, 12>(c);
+        return dyn3_imagest<float, 64, 16>(c);
+    }
+    if (c->nx == 20) return dyn3_imagest<double, 20, 8>(c);
+    if (c->nx == 32) return dyn3_imagest<double, 32, 12>(c);
+    return dyn3_imagest<double, 64, 16>(c);
 }
 void launch_dyn3(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck, int part) {
     if (c->f32) {
@@ -512,7 +542,8 @@ struct DynOp {
             for (int k = 0; k < (int)c->tiers.size(); ++k) {
                 const auto& tp = c->tiers[k];
                 const int c0 = c->cls_ptr[tp.s0], c1 = c->cls_ptr[tp.s1], p0 = c->pair_ptr[c0], p1 = c->pair_ptr[c1];
-                auto kf = tp.fl ? raocp::k_dyn_bottom_fwd<NX, NU, true> : raocp::k_dyn_bottom_fwd<NX, NU, false>;
+                auto kf = tp.fm == 1 ? raocp::k_dyn_bottom_fwd<NX, NU, 1>
+                                     : (tp.fm == 2 ? raocp::k_dyn_bottom_fwd<NX, NU, 2> : raocp::k_dyn_bottom_fwd<NX, NU, 0>);
                 allow_lds(kf, tp.lds_f);
                 if (tier_blocks(k) > 0)
                     kf<<<tier_blocks(k), B, tp.lds_f, c->stream>>>(dev_for(), bf, ctl, zsel, c->d, tp.s0, tp.s1, c0, c1,
@@ -903,7 +934,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
                 for (int k = (int)c->tiers.size() - 1; k >= 0; --k)
                     add("k_dyn_bottom_back<" + nn + ", " + b(c->tiers[k].fold) + ">");
                 add("k_dyn_top<" + nn + ", " + b(c->f_lds_top) + ", " + b(c->fold_top) + ">");
-                for (const auto& tp : c->tiers) add("k_dyn_bottom_fwd<" + nn + ", " + b(tp.fl) + ">");
+                for (const auto& tp : c->tiers) add("k_dyn_bottom_fwd<" + nn + ", " + std::to_string(tp.fm) + ">");
             } else {
                 return "k_dyn_gather + k_dyn_stage_a / _b / _f (per stage)";
             }
@@ -1583,7 +1614,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 }
                 sts.push_back(d);
             }
-            c->dyn3 = ok && c->f32;
+            // default: fp32, and fp64 trees of >= 64k nodes (config 4: 118 vs 143 us for the
+            // tiers; config 2 keeps the tiers, whose few launches win on small trees)
+            c->dyn3 = ok && (c->f32 || n >= 65536);
             if (const char* e = getenv("RAOCP_DYN3")) c->dyn3 = ok && atoi(e) != 0;
             if (c->dyn3) {
                 c->d3st = sts;
@@ -1612,7 +1645,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 return bail(rc);
         }
         if (c->dyn3) {
-            if ((rc = c->alloc(&c->Q2, (size_t)n * nx)) || (rc = c->alloc(&c->Dd2, (size_t)m * nu))) return bail(rc);
+            if ((rc = c->alloc(&c->Q2, (size_t)n * nx)) || (rc = c->alloc(&c->Dd2, (size_t)m * nu)) ||
+                (rc = dyn3_images(c)))
+                return bail(rc);
             c->dyn32 = c->f32;
         }
         if (c->dyn2) {
@@ -1730,7 +1765,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             int maxch = 0;
             double cost = 0;
             size_t bb = 0, bf = 0;
-            bool fl = true, ok = false, fold = false;
+            int fm = 1;
+            bool ok = false, fold = false;
         };
         auto tier = [&](int a, int b) {  // subtrees rooted at stage a, levels a..b-1, boundary b (worst case)
             Tier w;
@@ -1764,9 +1800,21 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             }
             w.bf = 8 * (ncl * KM1 + npr * F1 + w.nnl * KF + recs(w.nnl + w.nall - 1) + st_f);
             if (w.bf > kLds) {
-                w.fl = false;
-                w.bf -= 8 * npr * F1;
-                w.cost += 2 * (b - a);
+                // the pairs of one level at a time (restaged per level: one LDS round trip each),
+                // else F from L2: measured 86.7 us for the config-4 tier [6,10) forward, whose
+                // leaf level alone took 18.7 us per round (profiles/r03_v2/stamps_c4.log)
+                size_t npl = 0;
+                for (int t = a; t < b; ++t) npl = std::max<size_t>(npl, pp[cp[t + 1]] - pp[cp[t]]);
+                const size_t bf2 = w.bf - 8 * (npr - npl) * F1;
+                if (bf2 <= kLds) {
+                    w.fm = 2;
+                    w.bf = bf2;
+                    w.cost += (b - a - 1);
+                } else {
+                    w.fm = 0;
+                    w.bf -= 8 * npr * F1;
+                    w.cost += 8 * (b - a);
+                }
             }
             // the tier's subtrees run as rounds of co-resident workgroups (2048 lanes per CU
             // at most, fewer workgroups when their LDS does not fit): every round
@@ -1840,7 +1888,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             tp.maxch = w.maxch;
             tp.lds_b = w.bb;
             tp.lds_f = w.bf;
-            tp.fl = w.fl;
+            tp.fm = w.fm;
             tp.fold = w.fold;
             std::vector<raocp::Rec> lv;  // level ranges {lo, hi, off} of every subtree of the tier
             for (int r = c->stage_ptr[a]; r < c->stage_ptr[a + 1]; ++r) {
@@ -1858,6 +1906,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             if ((rc = c->upload_vec(&tp.lv, lv))) return bail(rc);
             // regular tier: every subtree has the same level sizes and consecutive ids
             memset(&tp.ta, 0, sizeof(tp.ta));
+            for (int l = 0; l <= L; ++l) tp.ta.pl0[l] = c->pair_ptr[c->cls_ptr[a + l]];
             tp.ta.regular = 1;
             for (int l = 0; l <= L; ++l) {
                 tp.ta.lo0[l] = lv[l].x;
@@ -1878,7 +1927,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                     c->f_lds_top ? "(lds)" : "(global)", c->fold_top ? " fold" : "");
             for (const auto& tp : c->tiers)
                 fprintf(stderr, " | tier [%d,%d) x%d lds %zu/%zu F%s%s", tp.s0, tp.s1, tp.nsub, tp.lds_b, tp.lds_f,
-                        tp.fl ? "(lds)" : "(global)", tp.fold ? " fold" : "");
+                        tp.fm == 1 ? "(lds)" : (tp.fm == 2 ? "(lds per level)" : "(global)"), tp.fold ? " fold" : "");
             fprintf(stderr, "\n");
         }
     }

@@ -635,6 +635,7 @@ struct TierArg {
     int boff;  // first subtree of this launch (a shard launches only the subtrees it owns)
     int lo0[kMaxLevels + 1];
     int cnt[kMaxLevels + 1];
+    int pl0[kMaxLevels + 1];  // first (kind, class) pair of the parents of level l (absolute)
 };
 
 __device__ __forceinline__ void tier_levels(Prologue& pl, const TierArg& ta, const Rec* __restrict__ sub_lv, int L) {
@@ -776,13 +777,18 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     tflush(p, pl, 4 + 2 * L);
 }
 
-// tier forward: [KM (classes c0..c1) | F (pairs p0..p1, if FL) | XD rows (nonleaf, KF) | NL | CH]
+// tier forward: [KM (classes c0..c1) | F | XD rows (nonleaf, KF) | NL | CH]
 // XD rows = [x (the root's; the others are written by the sweep) | d | 0]
-template <int NXc, int NUc, bool FL>
+// FM: where the [A_bar | B] rows F live. 0: global (L2); 1: every pair of the tier (p0..p1)
+// staged in the prologue; 2: only the pairs of one level's parents (ta.pl0[l] ..
+// ta.pl0[l + 1]), restaged before each level — a deep tier whose whole F does not fit LDS
+// reads its rows from LDS anyway, for one LDS round trip per level.
+template <int NXc, int NUc, int FM>
 __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
                                                                const double* dbuf_, int s, int s1, int c0, int c1,
                                                                int p0, int p1, const Rec* __restrict__ sub_lv,
                                                                TierArg ta) {
+    constexpr bool FL = FM != 0;
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
     tstamp(p, pl, 0);
@@ -792,12 +798,18 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     const int tid = threadIdx.x, nthr = blockDim.x;
     ldsd* smem = (ldsd*)smem_;
     const int L = s1 - s;
-    const int oKM = 0, oF = oKM + (c1 - c0) * ts.KM1, oXD = oF + (FL ? (p1 - p0) * ts.F1 : 0);
+    int npl = p1 - p0;  // pairs held in LDS
+    if constexpr (FM == 2) {
+        npl = 0;
+        for (int l = 0; l < L; ++l) npl = max(npl, ta.pl0[l + 1] - ta.pl0[l]);
+    }
+    const int oKM = 0, oF = oKM + (c1 - c0) * ts.KM1, oXD = oF + (FL ? npl * ts.F1 : 0);
     int rot = p.dyn_rot ? 0 : -1;
     if (!p.dyn_regtab) {
         dma_r(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1, rot);
-        if (FL) dma_r(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1, rot);
+        if (FM == 1) dma_r(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1, rot);
     }
+    if (FM == 2) dma_r(smem + oF, p.dF + (size_t)ta.pl0[0] * ts.F1, (ta.pl0[1] - ta.pl0[0]) * ts.F1, rot);
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
     lds_sync();
@@ -839,7 +851,7 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     if (p.dyn_regtab) {
         TabCopy tc;
         tc.add(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1);
-        if (FL) tc.add(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
+        if (FM == 1) tc.add(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
         tc.run();
     }
     const int done = ctl_done(ctl);
@@ -851,9 +863,17 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     const ldsrec* NL = (const ldsrec*)NLd;
     const ldsrec* CH = (const ldsrec*)CHd;
     typedef typename std::conditional<FL, const ldsd*, const glbd*>::type PF;
-    const TabsT<const ldsd*, PF> tb{nullptr, nullptr, smem + oKM,
-                                    FL ? (PF)(smem + oF) : (PF)((const glbd*)p.dF), c0, FL ? p0 : 0};
+    TabsT<const ldsd*, PF> tb{nullptr, nullptr, smem + oKM,
+                              FL ? (PF)(smem + oF) : (PF)((const glbd*)p.dF), c0, FL ? p0 : 0};
     for (int l = 0; l < L; ++l) {
+        if constexpr (FM == 2) {
+            tb.p0 = ta.pl0[l];
+            if (l > 0) {  // level l-1's products are done (the barrier that ended it)
+                dma(smem + oF, p.dF + (size_t)ta.pl0[l] * ts.F1, (ta.pl0[l + 1] - ta.pl0[l]) * ts.F1);
+                dma_wait();
+                lds_sync();
+            }
+        }
         const InfoT<const ldsrec*> inf{NL + pl.off[l], pl.lo[l], CH + pl.off[l + 1] - 1, pl.lo[l + 1]};
         const LRows xd_l{XD + (size_t)pl.off[l] * g.KF, pl.lo[l], g.KF};
         if (l + 1 < L) {

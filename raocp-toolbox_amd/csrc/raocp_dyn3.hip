@@ -18,7 +18,10 @@
 // loads straight into registers and writes its outputs from them.
 //
 // Weights: the stage's tables (slot k: B_k', A_k' backward, Abar_k, B_k forward; the class's
-// Rinv, G, K) are staged once per workgroup in LDS in fragment order (WLs below).
+// Rinv, G, K) in fragment order (WLs below): k_dy3_image lays them out once per context as
+// one contiguous image per stage and direction, which every workgroup copies into LDS by
+// LDS-DMA (one memory round trip; the element-wise fragment gather it replaces was most of
+// the ~10 us a launch of a one-tile stage cost at config 5, profiles/r03_v2).
 
 // a fragment table taken from a column-major source with leading dimension ld, rows
 // [r0, r0 + R), columns [c0, c0 + K): lds[(ro KS + s) 64 + lane] = M[r][k] (transposed form,
@@ -29,8 +32,8 @@ struct WLs {
     static constexpr int RO = (R / 4 + 3) / 4, KS = K / 4, N = RO * KS * 64;
     const __attribute__((address_space(3))) T* base;
     __device__ __forceinline__ T get(int ro, int s) const { return base[(ro * KS + s) * 64 + (threadIdx.x & 63)]; }
-    static __device__ __forceinline__ void fill(__attribute__((address_space(3))) T* dst, const T* M, int ld, int r0,
-                                                int c0) {
+    template <class DP>
+    static __device__ __forceinline__ void fill(DP dst, const T* M, int ld, int r0, int c0) {
         for (int q = threadIdx.x; q < N; q += blockDim.x) {
             const int l = q & 63, lo = l & 15, h = l >> 4, s = (q >> 6) % KS, ro = (q >> 6) / KS;
             const int r = wrow<T, R>(ro, lo), k = KS * h + s;
@@ -70,31 +73,62 @@ struct Dy3Lds {
 // tables (column-major M[k R + r], raocp_capi.hip): W2[kind] = [B'; A'] (R = nu + nx rows,
 // nx columns), RG2[cls] = [Rinv; G] (R rows, nu columns), KM2[cls] = K (nu x nx),
 // F2[pair] = [Abar | B] (nx rows, nx + nu columns)
+// backward image of a stage: per slot k [B_k' | A_k'], then [Rinv | G] of its class
+template <class T, int NX, int NU, class DP>
+__device__ __forceinline__ void dy3_back_tables(DP wl, const Dy3Stage& st, int C, const double* W2, const double* RG2) {
+    typedef Dy3Lds<T, NX, NU> L;
+    constexpr int R = NX + NU;
+    const T* W = (const T*)W2;
+    for (int k = 0; k < C; ++k) {
+        L::WB::fill(wl + k * (L::WB::N + L::WA::N), W + (size_t)st.kind[k] * R * NX, R, 0, 0);
+        L::WA::fill(wl + k * (L::WB::N + L::WA::N) + L::WB::N, W + (size_t)st.kind[k] * R * NX, R, NU, 0);
+    }
+    DP wr = wl + C * (L::WB::N + L::WA::N);
+    L::WRI::fill(wr, (const T*)RG2 + (size_t)st.cls * R * NU, R, 0, 0);
+    L::WG::fill(wr + L::WRI::N, (const T*)RG2 + (size_t)st.cls * R * NU, R, NU, 0);
+}
+// forward image: K of the class, then per slot k [Abar_k | B_k]
+template <class T, int NX, int NU, class DP>
+__device__ __forceinline__ void dy3_fwd_tables(DP wl, const Dy3Stage& st, int C, const double* KM2, const double* F2) {
+    typedef Dy3Lds<T, NX, NU> L;
+    L::WK::fill(wl, (const T*)KM2 + (size_t)st.cls * NU * NX, NU, 0, 0);
+    DP wf = wl + L::WK::N;
+    for (int k = 0; k < C; ++k) {
+        const T* F = (const T*)F2 + (size_t)st.pair[k] * NX * (NX + NU);
+        L::WA::fill(wf + k * (L::WA::N + L::WG::N), F, NX, 0, 0);                 // Abar_k
+        L::WG::fill(wf + k * (L::WA::N + L::WG::N) + L::WA::N, F, NX, 0, NX);    // B_k
+    }
+}
+// one workgroup per stage, at context creation: the stage's backward and forward images
+template <class T, int NX, int NU>
+__global__ void __launch_bounds__(512) k_dy3_image(Dy3Stage st, int C, const double* __restrict__ W2,
+                                                   const double* __restrict__ RG2, const double* __restrict__ KM2,
+                                                   const double* __restrict__ F2, double* bimg, double* fimg) {
+    dy3_back_tables<T, NX, NU>((glbp<T>)bimg, st, C, W2, RG2);
+    dy3_fwd_tables<T, NX, NU>((glbp<T>)fimg, st, C, KM2, F2);
+}
+
 template <class T, int NX, int NU>
 __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__ ctl, ChkArg ck, double* __restrict__ z_,
                                                   double* __restrict__ q_, double* __restrict__ d_, Dy3Stage st, int C,
-                                                  const double* __restrict__ W2, const double* __restrict__ RG2, int sp) {
+                                                  const double* __restrict__ img, int sp) {
     typedef typename MF<T>::v4 v4;
     typedef Dy3Lds<T, NX, NU> L;
-    constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16, R = NX + NU;
+    constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
     if (ck.on && blockIdx.x == gridDim.x - 1) {
         // the previous CP iteration's stopping test (defer_check, raocp_capi.hip)
         if (threadIdx.x < 64) cp_check_wave(ck);
         return;
     }
-    if (ctl && ctl->done) return;
     extern __shared__ __attribute__((aligned(16))) double dsm_[];
     typedef __attribute__((address_space(3))) T lT;
     lT* wl = (lT*)dsm_;
-    const T* W = (const T*)W2 + 0;
-    for (int k = 0; k < C; ++k) {
-        L::WB::fill(wl + k * (L::WB::N + L::WA::N), W + (size_t)st.kind[k] * R * NX, R, 0, 0);
-        L::WA::fill(wl + k * (L::WB::N + L::WA::N) + L::WB::N, W + (size_t)st.kind[k] * R * NX, R, NU, 0);
-    }
-    lT* wr = wl + C * (L::WB::N + L::WA::N);
-    L::WRI::fill(wr, (const T*)RG2 + (size_t)st.cls * R * NU, R, 0, 0);
-    L::WG::fill(wr + L::WRI::N, (const T*)RG2 + (size_t)st.cls * R * NU, R, NU, 0);
+    dma((ldsd*)dsm_, img, L::back_n(C) * (int)sizeof(T) / 8);  // whole 16-B chunks (N: multiples of 64)
+    const int done = ctl_done(ctl);  // read while the image is in flight (raocp_dyn.hip)
+    dma_wait();
     __syncthreads();
+    if (done) return;
+    lT* wr = wl + C * (L::WB::N + L::WA::N);
     const typename L::WRI wri{wr};
     const typename L::WG wg{wr + L::WRI::N};
     glbp<T> z = (glbp<T>)z_;
@@ -169,22 +203,19 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
 template <class T, int NX, int NU>
 __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ ctl, double* __restrict__ z_,
                                                  const double* __restrict__ d_, const double* __restrict__ x0_, Dy3Stage st,
-                                                 int C, const double* __restrict__ KM2, const double* __restrict__ F2, int sp) {
+                                                 int C, const double* __restrict__ img, int sp) {
     typedef typename MF<T>::v4 v4;
     typedef Dy3Lds<T, NX, NU> L;
     constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
-    if (ctl && ctl->done) return;
     extern __shared__ __attribute__((aligned(16))) double dsm_[];
     typedef __attribute__((address_space(3))) T lT;
     lT* wl = (lT*)dsm_;
-    L::WK::fill(wl, (const T*)KM2 + (size_t)st.cls * NU * NX, NU, 0, 0);
-    lT* wf = wl + L::WK::N;
-    for (int k = 0; k < C; ++k) {
-        const T* F = (const T*)F2 + (size_t)st.pair[k] * NX * (NX + NU);
-        L::WA::fill(wf + k * (L::WA::N + L::WG::N), F, NX, 0, 0);                 // Abar_k
-        L::WG::fill(wf + k * (L::WA::N + L::WG::N) + L::WA::N, F, NX, 0, NX);    // B_k
-    }
+    dma((ldsd*)dsm_, img, L::fwd_n(C) * (int)sizeof(T) / 8);
+    const int done = ctl_done(ctl);
+    dma_wait();
     __syncthreads();
+    if (done) return;
+    lT* wf = wl + L::WK::N;
     const typename L::WK wk{wl};
     glbp<T> z = (glbp<T>)z_;
     cglbp<T> db = (cglbp<T>)d_;

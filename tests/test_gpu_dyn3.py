@@ -1,8 +1,9 @@
 """GPU parity of the per-stage streaming dynamics sweep k_dy3_back / k_dy3_fwd
 (raocp_dyn3.hip: one launch per stage and direction, the children's products accumulated
-per parent in MFMA registers; cache.py:259-288). It is the default of fp32 contexts on
-trees with one branching factor whose child slots keep their (A, B) pair across a stage
-(configs 2, 4, 5) and an fp64 opt-in (RAOCP_DYN3=1) next to the tiered kernels.
+per parent in MFMA registers; cache.py:259-288). It is the default of fp32 contexts and of
+fp64 trees of >= 64k nodes with one branching factor whose child slots keep their (A, B)
+pair across a stage (configs 4, 5; config 2 in fp32), and an fp64 opt-in (RAOCP_DYN3=1) on
+smaller trees next to the tiered kernels (RAOCP_DYN3=0 forces the tiers).
 
 Tolerances: the projection against the oracle within 1e-12 of the largest entry (fp64) and
 exact feasibility x_j = A_j x_i + B_j u_i of its output to 1e-12; the CP loop against the
@@ -71,7 +72,7 @@ def test_dyn3_cp_loop_matches_tiers_and_oracle(cfg):
     r = _recipe(cfg)
     tree, prob = build_problem(r)
     d3 = _with_env({"RAOCP_DYN3": "1"}, lambda: core.Cache(prob))
-    tiers = core.Cache(prob)
+    tiers = _with_env({"RAOCP_DYN3": "0"}, lambda: core.Cache(prob))
     assert not tiers.native.kernel_info(9).startswith("k_dy3")
     alpha = 0.999 / tiers.native.step_size()
     K = 12 if cfg == "c4" else 20

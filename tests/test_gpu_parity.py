@@ -43,9 +43,13 @@ def _env(key, value):
             os.environ[key] = old
 
 
+@contextlib.contextmanager
 def dyn_engine(mode):
-    """Contexts created inside use the tiered dynamics kernels or the per-stage fallback."""
-    return _env("RAOCP_DYN_PER_STAGE", "1" if mode == "per_stage" else "0")
+    """Contexts created inside use the tiered dynamics kernels or the per-stage fallback (not
+    the streaming per-stage sweep k_dy3, the default of fp64 trees of >= 64k nodes, which
+    tests/test_gpu_dyn3.py covers)."""
+    with _env("RAOCP_DYN_PER_STAGE", "1" if mode == "per_stage" else "0"), _env("RAOCP_DYN3", "0"):
+        yield
 
 
 @contextlib.contextmanager
