@@ -57,9 +57,12 @@ struct raocp_ctx {
     int ellt3_C = 0;             // L^T by streaming wave tasks: uniform branching factor (0 = off)
     int ellt3_grid = 0;
     bool cp3 = false;            // the CP iteration after the dynamics as one streaming kernel (raocp_cp3.hip)
-    int cp3_grid = 0;
+    int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
     int cp3_split = 0;           // leaves as tasks of their own (small trees: more waves, shorter chains)
+    raocp::Cp3Tasks cp3_ta{};    // the launch's task list (a shard: its own families + the top)
+    raocp::Cp3Tasks cp3_tb{};    // a shard's second launch: the cut's parents, after X1
+    int cp3_gridb = 0;
     // per-stage MFMA dynamics (raocp_dyn2.hip): tables, node lists, tile lists per stage
     bool dyn2 = false;           // fp32 contexts always; fp64 opt-in RAOCP_DYN2=1
     const double *W2 = nullptr, *RG2 = nullptr, *KM2 = nullptr, *F2 = nullptr;
@@ -450,6 +453,20 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
         kf<<<grid(st, t, false), thr, lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, st, C, img, coop(t) ? 1 : 0);
     }
 }
+// LDS bytes of the sweep's larger launch (tables + the slot-parallel sums; launch_dyn3t)
+template <class T, int NX, int NU>
+size_t dyn3_lds(int C) {
+    typedef raocp::Dy3Lds<T, NX, NU> L;
+    constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
+    return std::max((size_t)(L::back_n(C) + C * (RU + RX) * 4 * 64) * sizeof(T), (size_t)L::fwd_n(C) * sizeof(T));
+}
+bool dyn3_lds_fits(bool f32, int nx, int nu, int C) {
+    size_t b = ~(size_t)0;
+    if (nx == 20 && nu == 8) b = f32 ? dyn3_lds<float, 20, 8>(C) : dyn3_lds<double, 20, 8>(C);
+    else if (nx == 32 && nu == 12) b = f32 ? dyn3_lds<float, 32, 12>(C) : dyn3_lds<double, 32, 12>(C);
+    else if (nx == 64 && nu == 16) b = f32 ? dyn3_lds<float, 64, 16>(C) : dyn3_lds<double, 64, 16>(C);
+    return b <= 160 * 1024;
+}
 // the per-stage table images of the sweep, laid out once (k_dy3_image, one workgroup per stage)
 template <class T, int NX, int NU>
 int dyn3_imagest(raocp_ctx* c) {
@@ -705,16 +722,50 @@ void launch_cpp(raocp_ctx* c, bool fuse = false) {
 bool cp3_sizes(bool f32, int nx, int nu) {
     return (nx == 20 && nu == 8) || (nx == 32 && nu == 12) || (f32 && nx == 64 && nu == 16);
 }
-void launch_cp3(raocp_ctx* c) {
-    const int g = c->cp3_grid, C = c->unif_C, bx = c->box_mode, mL = c->cp3_mL, sp = c->cp3_split;
-    if (c->f32) {
-        if (c->nx == 20) raocp::k_cp3<float, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
-        else if (c->nx == 32) raocp::k_cp3<float, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
-        else raocp::k_cp3<float, 64, 16><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
-    } else {
-        if (c->nx == 20) raocp::k_cp3<double, 20, 8><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
-        else raocp::k_cp3<double, 32, 12><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, c->redpart, C, bx, mL, sp);
+// a k_cp3 task list: split leaf tiles [l0, l1), then the parent ranges in order; returns
+// the tiles
+long cp3_tasks(raocp::Cp3Tasks& tk, const std::vector<std::pair<int, int>>& ranges, int l0, int l1, int split,
+               int mL) {
+    tk = raocp::Cp3Tasks{};
+    tk.l0 = l0;
+    tk.l1 = std::max(l0, l1);
+    tk.split = split;
+    tk.mL = mL;
+    long tiles = (tk.l1 - tk.l0 + 15) / 16;
+    for (const auto& r : ranges) {
+        if (r.second <= r.first || tk.nr >= raocp::kCp3MaxR) continue;
+        tk.lo[tk.nr] = r.first;
+        tk.hi[tk.nr] = r.second;
+        tk.t0[tk.nr + 1] = tk.t0[tk.nr] + (r.second - r.first + 15) / 16;
+        ++tk.nr;
     }
+    if (tk.nr == 0) {  // an empty launch still needs one range (no tiles)
+        tk.nr = 1;
+        tk.t0[1] = 0;
+    }
+    return tiles + tk.t0[tk.nr];
+}
+int cp3_grid_of(long tiles) { return (int)std::max(1L, std::min((tiles + 3) / 4, 2048L)); }
+// part 0: the unsharded launch, or a shard's first; 1: a shard's second (after X1), whose
+// residual partials follow the first launch's rows
+template <bool SH>
+void launch_cp3t(raocp_ctx* c, int g, double* rp, const raocp::Cp3Tasks& tk) {
+    const int C = c->unif_C, bx = c->box_mode;
+    if (c->f32) {
+        if (c->nx == 20) raocp::k_cp3<float, 20, 8, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
+        else if (c->nx == 32) raocp::k_cp3<float, 32, 12, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
+        else raocp::k_cp3<float, 64, 16, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
+    } else {
+        if (c->nx == 20) raocp::k_cp3<double, 20, 8, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
+        else raocp::k_cp3<double, 32, 12, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
+    }
+}
+void launch_cp3(raocp_ctx* c, int part = 0) {
+    if (c->sh_S > 0)
+        launch_cp3t<true>(c, part ? c->cp3_gridb : c->cp3_grid, c->redpart + (part ? (size_t)c->cp3_grid * 6 : 0),
+                          part ? c->cp3_tb : c->cp3_ta);
+    else
+        launch_cp3t<false>(c, c->cp3_grid, c->redpart, c->cp3_ta);
 }
 // the solve's first half step Z[1] = prox-part(Z[0] - alpha L^T E[0]) (s_0 relaxation,
 // kernel projection): k_cp_primal; an fp32 context runs k_cpp2 on {p = z+ = Z[0], d = eta+ =
@@ -842,13 +893,15 @@ int enqueue_shard_iteration(raocp_ctx* c) {
         return rc;
     shard_unpack_x2(c);
     launch_dynamics(c, c->bufs, 1, c->ctl, 2);
-    launch_cpd(c);
+    if (c->cp3) launch_cp3(c, 0);
+    else launch_cpd(c);
     shard_pack_x1(c);
     if ((rc = rccl_check(g_rccl.all_gather(c->x1_send, c->x1_recv, (size_t)x1_len(c), ncclFloat64, comm, c->stream),
                          "ncclAllGather(eta2, residuals)")))
         return rc;
     shard_unpack_x1(c);  // + the previous iteration's stopping test
-    launch_cpp(c);
+    if (c->cp3) launch_cp3(c, 1);
+    else launch_cpp(c);
     raocp::k_cp_reduce<<<1, kBlock, 0, c->stream>>>(c->ctl, c->redpart, c->cp_rows, c->red8);
     return RAOCP_OK;
 }
@@ -943,7 +996,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             return s;
         }
         case 10:
-            if (c->cp3) return "k_cp3<" + T + ", " + nn + ">";
+            if (c->cp3) return "k_cp3<" + T + ", " + nn + (c->sh_S > 0 ? ", true> x2" : ", false>");
             return kernel_name(c, 2) + " + " + kernel_name(c, 6);
         default: return "";
     }
@@ -1593,7 +1646,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             // children's slot k of one kind at every parent of a stage, one class per stage, and
             // the compile-time sizes
             const int C = t->nch[0];
-            bool ok = C >= 1 && C <= 4 && ((nx == 20 && nu == 8) || (nx == 32 && nu == 12) || (nx == 64 && nu == 16));
+            // (fp64 at nx = 64: the stage's tables exceed the 160 KB of LDS)
+            bool ok = C >= 1 && C <= 4 && ((nx == 20 && nu == 8) || (nx == 32 && nu == 12) || (nx == 64 && nu == 16)) &&
+                      dyn3_lds_fits(c->f32, nx, nu, C);
             for (int i = 0; i < m && ok; ++i)
                 if (t->nch[i] != C || t->ch_start[i] != 1 + C * i) ok = false;
             std::vector<raocp::Dy3Stage> sts;
@@ -2193,13 +2248,15 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         if (const char* e = getenv("RAOCP_CP3")) c->cp3 = c->cp3 && atoi(e) != 0;
         if (c->cp3) {
             c->cp3_mL = c->stage_ptr[N - 1];
-            long tiles = (long)(m - c->cp3_mL + 15) / 16 + (c->cp3_mL + 15) / 16;
+            const long ptiles = (long)(m - c->cp3_mL + 15) / 16 + (c->cp3_mL + 15) / 16;
             // small trees (latency-bound: config 2 has 256 family tiles, one wave each) split
             // the leaves into tasks of their own: twice the waves, half the longest chain
-            c->cp3_split = tiles < 1024;
+            c->cp3_split = ptiles < 1024;
             if (const char* e = getenv("RAOCP_CP3_SPLIT")) c->cp3_split = atoi(e) != 0;
-            if (c->cp3_split) tiles += (n - m + 15) / 16;
-            c->cp3_grid = (int)std::max(1L, std::min((tiles + 3) / 4, 2048L));
+            // leaf-parent tiles first (heavier), then the rest
+            const long tiles = cp3_tasks(c->cp3_ta, {{c->cp3_mL, m}, {0, c->cp3_mL}}, m, c->cp3_split ? n : m,
+                                         c->cp3_split, c->cp3_mL);
+            c->cp3_grid = cp3_grid_of(tiles);
             if (const char* e = getenv("RAOCP_CP3_GRID")) c->cp3_grid = std::max(1, atoi(e));
             if (c->cp3_grid > c->red_rows) {
                 c->red_rows = c->cp3_grid;
@@ -2708,7 +2765,7 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     c->sh_R = nranks;
     c->sh_r = rank;
     c->sh_S = S;
-    c->cp3 = false;  // a shard runs k_cpd* / k_cpp* on its owned blocks (build_cp_blocks sets cp_rows)
+    if (const char* e = getenv("RAOCP_SHARD_CP3")) c->cp3 = c->cp3 && atoi(e) != 0;
     std::vector<int> slc(2 * nranks);
     int xmax = 0;
     for (int r = 0; r < nranks; ++r) {
@@ -2754,6 +2811,29 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     std::vector<std::pair<int, int>> lr_{{c->own_lo[N], c->own_hi[N]}};
     int rc;
     if ((rc = build_cp_blocks(c, pr_, lr_))) return rc;
+    if (c->cp3) {
+        // k_cp3 in two launches: the owned families and leaves plus the replicated top above
+        // the cut's parents (storing its roots' xi2 for X1), then the cut's parents with the
+        // roots' eta2 entries from X1
+        std::vector<std::pair<int, int>> ra;
+        if (N - 1 >= S) ra.push_back({c->own_lo[N - 1], c->own_hi[N - 1]});
+        for (int t = S; t < N - 1; ++t) ra.push_back({c->own_lo[t], c->own_hi[t]});
+        if (S >= 2) ra.push_back({0, c->stage_ptr[S - 1]});
+        const long ta = cp3_tasks(c->cp3_ta, ra, c->own_lo[N], c->cp3_split ? c->own_hi[N] : c->own_lo[N], c->cp3_split,
+                                  c->cp3_mL);
+        c->cp3_ta.xlo = c->own_first;
+        c->cp3_ta.xhi = c->own_first + c->own_cnt;
+        const long tb = cp3_tasks(c->cp3_tb, {{c->stage_ptr[S - 1], c->stage_ptr[S]}}, 0, 0, c->cp3_split, c->cp3_mL);
+        c->cp3_tb.ext2 = 1;
+        c->cp3_grid = cp3_grid_of(ta);
+        c->cp3_gridb = cp3_grid_of(tb);
+        c->cp_rows = c->cp3_grid + c->cp3_gridb;
+        if (c->cp_rows > c->red_rows) {
+            c->red_rows = c->cp_rows;
+            if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return rc;
+        }
+        HIPCHK(hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)));
+    }
     if ((rc = c->alloc(&c->x2_send, (size_t)xmax * std::max(c->KP, c->nx))) ||
         (rc = c->alloc(&c->x2_recv, (size_t)nranks * xmax * std::max(c->KP, c->nx))) ||
         (rc = c->alloc(&c->x1_send, (size_t)2 * xmax + 16)) || (rc = c->alloc(&c->x1_recv, (size_t)nranks * (2 * xmax + 16))) ||
@@ -2838,7 +2918,8 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
                                       hipMemcpyDeviceToDevice, c->stream));
             shard_unpack_x2(c);
             launch_dynamics(c, c->bufs, 1, c->ctl, 2);
-            launch_cpd(c);
+            if (c->cp3) launch_cp3(c, 0);
+            else launch_cpd(c);
             shard_pack_x1(c);
         }
         if ((rc = sync_all())) return rc;
@@ -2848,7 +2929,8 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
                 HIPCHK(hipMemcpyAsync(c->x1_recv + (size_t)q * x1_len(c), cs[q]->x1_send, (size_t)x1_len(c) * sizeof(double),
                                       hipMemcpyDeviceToDevice, c->stream));
             shard_unpack_x1(c);
-            launch_cpp(c);
+            if (c->cp3) launch_cp3(c, 1);
+            else launch_cpp(c);
             raocp::k_cp_reduce<<<1, kBlock, 0, c->stream>>>(c->ctl, c->redpart, c->cp_rows, c->red8);
             HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
         }

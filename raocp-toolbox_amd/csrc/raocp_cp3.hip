@@ -186,9 +186,30 @@ struct LeafIn {
     }
 };
 
-template <class T, int NX, int NU>
-__global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs bf, double* __restrict__ part, int C,
-                                             int bx, int mL, int split) {
+// The task list of a launch (host-built, raocp_capi.hip cp3_tasks): tiles of 16 leaves
+// [l0, l1) when the leaves run as tasks of their own (split), then tiles of 16 parents from
+// the start of each parent range [lo[r], hi[r]). Unsharded: the leaf parents, then the rest.
+// A shard launches its own families and leaves plus the
+// replicated top above the cut's parents, then -- after X1 -- the cut's parents, whose
+// children's eta2 entries (eta+, xi2) come from the buffers the exchange filled (ext2)
+// instead of being recomputed from rows another shard owns; the first launch stores xi2 of
+// its roots' eta2 (parents [xlo, xhi)) for X1.
+constexpr int kCp3MaxR = 36;
+struct Cp3Tasks {
+    int l0, l1;    // split leaf tiles (l0 == l1: none)
+    int split;     // the leaf rows belong to the leaf tasks (1) or to their parents' tiles (0)
+    int mL;        // first parent whose children are leaves
+    int ext2;      // children's eta2 (eta+, xi2) from the buffers
+    int xlo, xhi;  // parents whose xi2 of eta2 is stored
+    int nr;        // parent ranges
+    int lo[kCp3MaxR], hi[kCp3MaxR], t0[kCp3MaxR + 1];  // t0: first task of each range
+};
+
+// SH: a shard's launches (the xi2 store and ext2 paths compiled in; the unsharded kernel
+// keeps its registers)
+template <class T, int NX, int NU, bool SH>
+__global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs bf, double* __restrict__ part,
+                                             double* __restrict__ xi2_, int C, int bx, Cp3Tasks tk) {
     typedef typename MF<T>::v4 v4;
     static_assert(NX % 4 == 0 && NU % 4 == 0, "row layout needs nx, nu multiples of 4");
     constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
@@ -324,21 +345,24 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             st_rows<T, NX>(out + p.X0 + (size_t)(live ? l : 0) * NX, live, ox);
     };
     const int G = 2 * C + 1;
-    const int nT1 = (m - mL + 15) >> 4, nT0 = (mL + 15) >> 4;  // leaf-parent tiles first (heavier)
-    const int nTL = split ? (p.n - m + 15) >> 4 : 0;           // leaf tiles (split)
-    for (int tk = gw; tk < nTL + nT0 + nT1; tk += nwv) {
-        if (tk < nTL) {
+    glbp<T> xi2 = (glbp<T>)xi2_;
+    const int split = tk.split;
+    const int nTL = (tk.l1 - tk.l0 + 15) >> 4;  // leaf tiles (split), then the parent ranges' tiles
+    for (int tt = gw; tt < nTL + tk.t0[tk.nr]; tt += nwv) {
+        if (tt < nTL) {
             // a tile of 16 consecutive leaves (split): everything of the leaf but s_l
-            const int l = m + 16 * tk + lo;
-            const bool live = l < p.n;
+            const int l = tk.l0 + 16 * tt + lo;
+            const bool live = l < tk.l1;
             LeafIn<T, NX> cur;
             cur.load(p, zp, pz, d, l, live, bx, m, true);
             leaf_work(cur, l, 0, live, true, false);
             continue;
         }
-        const int task = tk - nTL;
-        const bool leafp = task < nT1;
-        const int i0 = leafp ? mL + 16 * task : 16 * (task - nT1), iend = leafp ? m : mL;
+        const int task = tt - nTL;
+        int r = 0;
+        while (r + 1 < tk.nr && task >= tk.t0[r + 1]) ++r;
+        const int i0 = tk.lo[r] + 16 * (task - tk.t0[r]), iend = tk.hi[r];
+        const bool leafp = tk.lo[r] >= tk.mL;
         const int i = i0 + lo;
         const bool live = i < iend;
         // ---------------- phase 4 (first, on parents of leaves): leaf children (leaf SOC, eta14
@@ -382,6 +406,7 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             fin(d2, v, fmax(v, T(0)), bb, e2A, x2);
             e2C = x2;
             if (live && h == 0) eo[p.E2 + i] = e2A;
+            if (SH && live && h == 1 && i >= tk.xlo && i < tk.xhi) xi2[p.E2 + i] = x2;  // a shard's roots (X1)
         }
         const T e2W = d2 - e2A;
         if (live && i == 0 && h == 0) {
@@ -504,22 +529,29 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
             }
             if (!leafp && live && h == 0) {
                 // s_j of a nonleaf child: its eta2 recomputed (the same arithmetic as its own
-                // tile's, phase 1), then the half step
-                const int yj = G * j;
-                T ba = T(0), bb2 = T(0);
-                for (int q = 0; q < C; ++q) {
-                    const T cp = cond[1 + C * j + q], zy = zp[p.Y0 + yj + q], py = pz[p.Y0 + yj + q];
-                    ba = fma(cp, T(2) * zy - py, ba);
-                    bb2 = fma(cp, zy - py, bb2);
-                }
-                const T zy = zp[p.Y0 + yj + 2 * C], py = pz[p.Y0 + yj + 2 * C];
-                ba += T(2) * zy - py;
-                bb2 += zy - py;
+                // tile's, phase 1) or, across a shard boundary, as X1 delivered it; then the
+                // half step
                 const T sz = zp[p.S0 + j], sp = pz[p.S0 + j], dj = d[p.E2 + j];
-                const T av = (T(2) * sz - sp) - ba, bb = (sz - sp) - bb2;
-                const T v = (dj + alpha * av) * ra;
-                const T ep = alpha * (v - fmax(v, T(0)));
-                const T x2 = (dj - ep) * ra + bb;
+                T ep, x2;
+                if (SH && tk.ext2) {
+                    ep = eo[p.E2 + j];
+                    x2 = xi2[p.E2 + j];
+                } else {
+                    const int yj = G * j;
+                    T ba = T(0), bb2 = T(0);
+                    for (int q = 0; q < C; ++q) {
+                        const T cp = cond[1 + C * j + q], zy = zp[p.Y0 + yj + q], py = pz[p.Y0 + yj + q];
+                        ba = fma(cp, T(2) * zy - py, ba);
+                        bb2 = fma(cp, zy - py, bb2);
+                    }
+                    const T zy = zp[p.Y0 + yj + 2 * C], py = pz[p.Y0 + yj + 2 * C];
+                    ba += T(2) * zy - py;
+                    bb2 += zy - py;
+                    const T av = (T(2) * sz - sp) - ba, bb = (sz - sp) - bb2;
+                    const T v = (dj + alpha * av) * ra;
+                    ep = alpha * (v - fmax(v, T(0)));
+                    x2 = (dj - ep) * ra + bb;
+                }
                 ks.s[lo][k] = sz - alpha * ep;
                 account(sp, sz, dj - ep, x2);
             }

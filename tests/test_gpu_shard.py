@@ -5,12 +5,13 @@ device of the test box and exchange through device copies (raocp_group_cp_run); 
 multi-GPU transport is RCCL with the same packing (bench.py --shard).
 
 Parity: the residual histories and the owned parts of the final iterate equal those of
-the unsharded solve with the same kernels (a shard runs k_cpd* / k_cpp*, so the unsharded
-reference run sets RAOCP_CP3=0; the per-node arithmetic is identical and only max
-reductions are regrouped, which is exact), stay within 1e-10 of the default fused
-unsharded solve (k_cp3: other summation order) and match the oracle within the
-north_star tolerance. Configs 2 (the headline tree) and 4 (the tree the sharded bench leg
-runs, BASELINE configs[3]) at R = 2, 4, 8; config 5 in fp32 (BASELINE configs[4]) at R = 2, 4.
+the unsharded solve on the same CP kernels -- the fused k_cp3 (a shard runs it as two
+launches around X1, the cut's parents reading their children's eta2 entries from the
+exchange) or the two-launch k_cpd* / k_cpp* (RAOCP_CP3=0) -- bit for bit: the per-node
+arithmetic is identical and only max reductions are regrouped, which is exact. The two
+kernel families agree within 1e-10 and match the oracle within the north_star tolerance.
+Configs 2 (the headline tree) and 4 (the tree the sharded bench leg runs, BASELINE
+configs[3]) at R = 2, 4, 8; config 5 in fp32 (BASELINE configs[4]) at R = 2, 4.
 """
 import os
 
@@ -35,17 +36,23 @@ def c2():
     return _cache(2)
 
 
-def _two_launch_cache(prob):
-    """An unsharded context on the kernels a shard runs (k_cpd* / k_cpp*, not k_cp3)."""
+def _kern_cache(prob, kern, dtype=None):
+    """A context on the fused CP kernel k_cp3 ("fused", the default) or the two-launch
+    k_cpd* / k_cpp* ("two", RAOCP_CP3=0)."""
     old = os.environ.get("RAOCP_CP3")
-    os.environ["RAOCP_CP3"] = "0"
+    if kern == "two":
+        os.environ["RAOCP_CP3"] = "0"
     try:
-        return core.Cache(prob)
+        return core.Cache(prob, dtype=dtype) if dtype else core.Cache(prob)
     finally:
         if old is None:
             os.environ.pop("RAOCP_CP3", None)
         else:
             os.environ["RAOCP_CP3"] = old
+
+
+def _two_launch_cache(prob):
+    return _kern_cache(prob, "two")
 
 
 _ORACLE = {}
@@ -67,25 +74,27 @@ def _owned_x_slices(ctx):
 _CFG = {}
 
 
+@pytest.mark.parametrize("kern", ["fused", "two"])
 @pytest.mark.parametrize("cfg", [2, 4])
 @pytest.mark.parametrize("R", [2, 4, 8])
-def test_sharded_solve_matches_unsharded(cfg, R):
+def test_sharded_solve_matches_unsharded(cfg, R, kern):
     if cfg not in _CFG:
         _CFG[cfg] = _cache(cfg)
     r, tree, prob = _CFG[cfg]
-    base = _two_launch_cache(prob)
+    base = _kern_cache(prob, kern)
+    assert base.native.kernel_info(10).startswith("k_cp3") == (kern == "fused")
     lam = base.native.step_size()
     alpha = 0.999 / lam
     iters = 40 if cfg == 2 else 12
     st0, err0, derr0 = base.native.cp_run(r["x0"], iters, 0.0, alpha)
     z0 = base.get_primal_flat()
-    fused = core.Cache(prob)
-    stf, errf, _ = fused.native.cp_run(r["x0"], iters, 0.0, alpha)
+    other = _kern_cache(prob, "two" if kern == "fused" else "fused")
+    stf, errf, _ = other.native.cp_run(r["x0"], iters, 0.0, alpha)
     assert stf == st0 and np.max(np.abs(errf - err0) / np.abs(err0)) <= 1e-10
     st_o, err_o, _, z_o, _, _ = _oracle_run(cfg, prob, r["x0"], iters, alpha)
     assert np.max(np.abs(err0 - err_o) / np.abs(err_o)) <= 1e-8
     assert np.max(np.abs(z0 - z_o)) <= 1e-10 * np.max(np.abs(z_o))
-    shards = [core.Cache(prob) for _ in range(R)]
+    shards = [_kern_cache(prob, kern) for _ in range(R)]
     for k, s in enumerate(shards):
         s.native.shard(k, R)
     st, err, derr = group_cp_run([s.native for s in shards], r["x0"], iters, 0.0, alpha)
@@ -110,7 +119,7 @@ def test_sharded_stopping_and_status(c2):
     base = _two_launch_cache(prob)
     alpha = 0.999 / base.native.step_size()
     st0, err0, _ = base.native.cp_run(r["x0"], 400, 5e-2, alpha)
-    shards = [core.Cache(prob) for _ in range(2)]
+    shards = [_two_launch_cache(prob) for _ in range(2)]
     for k, s in enumerate(shards):
         s.native.shard(k, 2)
     st, err, _ = group_cp_run([s.native for s in shards], r["x0"], 400, 5e-2, alpha)
@@ -141,27 +150,20 @@ def test_rccl_transport_single_rank():
     assert "bit-identical" in res.stdout
 
 
+@pytest.mark.parametrize("kern", ["fused", "two"])
 @pytest.mark.parametrize("R", [2, 4])
-def test_fp32_sharded_config5_matches_unsharded(R):
+def test_fp32_sharded_config5_matches_unsharded(R, kern):
     """BASELINE configs[4] ("fp32, 8 x MI355X"): one config-5 tree in fp32 split across R
     shards. The per-stage streaming sweep (raocp_dyn3.hip) runs the owned parents of every
     stage below the cut and the replicated top, exchanging the roots' q rows (X2, fp32);
-    the CP kernels k_cpd2 / k_cpp2<float> run the owned families with the X1 exchange. The
-    residual history and the owned iterate equal the unsharded fp32 solve on the same
-    kernels bit for bit (only max reductions are regrouped); the default fused unsharded
-    solve (k_cp3<float>) agrees to fp32 rounding (1e-4 per trace entry)."""
+    the CP kernels (k_cp3<float> in two launches, or k_cpd2 / k_cpp2<float>) run the owned
+    families with the X1 exchange. The residual history and the owned iterate equal the
+    unsharded fp32 solve on the same kernels bit for bit (only max reductions are
+    regrouped); the two kernel families agree to fp32 rounding (1e-4 per trace entry)."""
     r = recipe_config(5, seed=0)
     tree, prob = build_problem(r)
-    old = os.environ.get("RAOCP_CP3")
-    os.environ["RAOCP_CP3"] = "0"
-    try:
-        base = core.Cache(prob, dtype="float32")
-        shards = [core.Cache(prob, dtype="float32") for _ in range(R)]
-    finally:
-        if old is None:
-            os.environ.pop("RAOCP_CP3", None)
-        else:
-            os.environ["RAOCP_CP3"] = old
+    base = _kern_cache(prob, kern, "float32")
+    shards = [_kern_cache(prob, kern, "float32") for _ in range(R)]
     assert base.native.kernel_info(9).startswith("k_dy3_back<float")
     alpha = 0.999 / base.native.step_size(rtol=1e-7)
     iters = 6
@@ -181,6 +183,6 @@ def test_fp32_sharded_config5_matches_unsharded(R):
                 np.testing.assert_array_equal(z[a * nx:b * nx], z0[a * nx:b * nx])
                 covered[a:b] = True
     assert covered.all()
-    fused = core.Cache(prob, dtype="float32")
-    stf, errf, _ = fused.native.cp_run(r["x0"], iters, 0.0, alpha)
+    other = _kern_cache(prob, "two" if kern == "fused" else "fused", "float32")
+    stf, errf, _ = other.native.cp_run(r["x0"], iters, 0.0, alpha)
     assert stf == st0 and np.max(np.abs(errf - err0) / np.abs(err0)) <= 1e-4

@@ -1,9 +1,9 @@
 """The RCCL shard transport with ONE rank (R = 1 forced): the sharded iteration with its
-RCCL all-gathers / all-reduce, graph-captured, must reproduce the unsharded solve exactly.
-Run as its own process: torch must not be imported (see bench.py SocketGroup)."""
+RCCL all-gathers, graph-captured, must reproduce the unsharded solve exactly, on the
+two-launch CP kernels (RAOCP_CP3=0) and on the fused k_cp3 (a shard's two k_cp3 launches
+around X1). Run as its own process: torch must not be imported (see bench.py SocketGroup)."""
 import os, sys
 os.environ["RAOCP_SHARD_FORCE"] = "1"
-os.environ["RAOCP_CP3"] = "0"  # a shard runs k_cpd* / k_cpp*: compare with the same kernels unsharded
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raocp-toolbox_amd"))
 import numpy as np
 import raocp.core as core
@@ -11,16 +11,18 @@ from raocp.core._native import comm_unique_id
 from raocp.problems import build_problem, recipe_config
 r = recipe_config(2)
 tree, prob = build_problem(r)
-base = core.Cache(prob)
-alpha = 0.999 / base.native.step_size()
-st0, e0, d0 = base.native.cp_run(r["x0"], 60, 0.0, alpha)
-sh = core.Cache(prob)
-sh.native.shard(0, 1)
-sh.native.comm_init(comm_unique_id(), 0, 1)
-st1, e1, d1 = sh.native.cp_run(r["x0"], 60, 0.0, alpha)
-assert st0 == st1 and np.array_equal(e0, e1) and np.array_equal(d0, d1), (np.max(np.abs(e0 - e1)))
-assert np.array_equal(base.get_primal_flat(), sh.get_primal_flat())
-ms0 = base.native.cp_bench(r["x0"], 480, alpha)
-ms1 = sh.native.cp_bench(r["x0"], 480, alpha)
-print(f"RCCL single-rank shard path OK: traces bit-identical; {480 / ms0 * 1e3:.0f} it/s unsharded, "
-      f"{480 / ms1 * 1e3:.0f} it/s through the shard exchange path")
+for cp3 in ("0", "1"):
+    os.environ["RAOCP_CP3"] = cp3  # the same CP kernels unsharded and sharded
+    base = core.Cache(prob)
+    alpha = 0.999 / base.native.step_size()
+    st0, e0, d0 = base.native.cp_run(r["x0"], 60, 0.0, alpha)
+    sh = core.Cache(prob)
+    sh.native.shard(0, 1)
+    sh.native.comm_init(comm_unique_id(), 0, 1)
+    st1, e1, d1 = sh.native.cp_run(r["x0"], 60, 0.0, alpha)
+    assert st0 == st1 and np.array_equal(e0, e1) and np.array_equal(d0, d1), (np.max(np.abs(e0 - e1)))
+    assert np.array_equal(base.get_primal_flat(), sh.get_primal_flat())
+    ms0 = base.native.cp_bench(r["x0"], 480, alpha)
+    ms1 = sh.native.cp_bench(r["x0"], 480, alpha)
+    print(f"RCCL single-rank shard path OK ({base.native.kernel_info(10)}): traces bit-identical; "
+          f"{480 / ms0 * 1e3:.0f} it/s unsharded, {480 / ms1 * 1e3:.0f} it/s through the shard exchange path")
