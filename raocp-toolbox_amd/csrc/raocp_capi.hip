@@ -63,6 +63,7 @@ struct raocp_ctx {
     raocp::Cp3Tasks cp3_ta{};    // the launch's task list (a shard: its own families + the top)
     raocp::Cp3Tasks cp3_tb{};    // a shard's second launch: the cut's parents, after X1
     int cp3_gridb = 0;
+    double* cp3img = nullptr;    // k_cp3's weight fragments in LDS order (k_cp3_image)
     // per-stage MFMA dynamics (raocp_dyn2.hip): tables, node lists, tile lists per stage
     bool dyn2 = false;           // fp32 contexts always; fp64 opt-in RAOCP_DYN2=1
     const double *W2 = nullptr, *RG2 = nullptr, *KM2 = nullptr, *F2 = nullptr;
@@ -416,8 +417,12 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
     constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
     // LDS: the stage's tables; the backward kernel's slot sums of a cooperative tile after them
     const size_t lb = (size_t)(L::back_n(C) + C * (RU + RX) * 4 * 64) * sizeof(T), lf = (size_t)L::fwd_n(C) * sizeof(T);
-    const int thr = std::max(lb, lf) > 64 * 1024 ? 512 : 256, wpb = thr / 64;
-    const int per_cu = std::max<int>(1, std::min<int>(2048 / thr, (int)(160 * 1024 / std::max(lb, lf))));
+    const size_t lmax = std::max(lb, lf);
+    const int thr = lmax > 64 * 1024 ? 512 : 256, wpb = thr / 64;
+    // (1,024-lane workgroups for the wide stages when the tables allow one workgroup per CU
+    // measured slower at config 5: 215.3 vs 190.9 us per projection, profiles/r03_v3)
+    const int thr_w = thr, wpb_w = thr_w / 64;
+    const int per_cu = std::max<int>(1, std::min<int>(2048 / thr_w, (int)(160 * 1024 / lmax)));
     const int cap = 256 * per_cu;  // one round of resident workgroups; waves loop over tiles
     auto kb = raocp::k_dy3_back<T, NX, NU>;
     auto kf = raocp::k_dy3_fwd<T, NX, NU>;
@@ -430,8 +435,9 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
     auto grid = [&](const raocp::Dy3Stage& st, int t, bool back) {
         const int tiles = (st.i1 - st.i0 + 15) / 16;
         if (coop(t)) return std::max(1, back ? tiles : (tiles * C + wpb - 1) / wpb);
-        return std::max(1, std::min(cap, (tiles + wpb - 1) / wpb));
+        return std::max(1, std::min(cap, (tiles + wpb_w - 1) / wpb_w));
     };
+    auto threads = [&](int t) { return coop(t) ? thr : thr_w; };
     const int N = c->N, S = c->sh_S;  // S > 0: a shard owns the stages >= S partly
     auto stage = [&](int t) -> const raocp::Dy3Stage& { return S > 0 && t >= S ? c->d3own[t] : c->d3st[t]; };
     for (int t = N - 1; t >= 0; --t) {
@@ -442,15 +448,16 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
         raocp::ChkArg ca{};
         if (ck && t == N - 1) ca = *ck;
         const double* img = (const double*)((const char*)c->d3img_b + (size_t)t * L::back_n(C) * sizeof(T));
-        kb<<<grid(st, t, true) + ca.on, thr, lb, c->stream>>>(c->dev, ctl, ca, z, c->Q2, c->Dd2, st, C, img,
-                                                             coop(t) ? 1 : 0);
+        kb<<<grid(st, t, true) + ca.on, threads(t), lb, c->stream>>>(c->dev, ctl, ca, z, c->Q2, c->Dd2, st, C, img,
+                                                                    coop(t) ? 1 : 0);
     }
     if (part == 1) return;
     for (int t = 0; t < N; ++t) {
         const raocp::Dy3Stage& st = stage(t);
         if (st.i1 <= st.i0) continue;
         const double* img = (const double*)((const char*)c->d3img_f + (size_t)t * L::fwd_n(C) * sizeof(T));
-        kf<<<grid(st, t, false), thr, lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, st, C, img, coop(t) ? 1 : 0);
+        kf<<<grid(st, t, false), threads(t), lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, st, C, img,
+                                                               coop(t) ? 1 : 0);
     }
 }
 // LDS bytes of the sweep's larger launch (tables + the slot-parallel sums; launch_dyn3t)
@@ -751,14 +758,36 @@ int cp3_grid_of(long tiles) { return (int)std::max(1L, std::min((tiles + 3) / 4,
 template <bool SH>
 void launch_cp3t(raocp_ctx* c, int g, double* rp, const raocp::Cp3Tasks& tk) {
     const int C = c->unif_C, bx = c->box_mode;
+    const double* im = c->cp3img;
     if (c->f32) {
-        if (c->nx == 20) raocp::k_cp3<float, 20, 8, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
-        else if (c->nx == 32) raocp::k_cp3<float, 32, 12, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
-        else raocp::k_cp3<float, 64, 16, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
+        if (c->nx == 20) raocp::k_cp3<float, 20, 8, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk, im);
+        else if (c->nx == 32) raocp::k_cp3<float, 32, 12, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk, im);
+        else raocp::k_cp3<float, 64, 16, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk, im);
     } else {
-        if (c->nx == 20) raocp::k_cp3<double, 20, 8, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
-        else raocp::k_cp3<double, 32, 12, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk);
+        if (c->nx == 20) raocp::k_cp3<double, 20, 8, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk, im);
+        else raocp::k_cp3<double, 32, 12, SH><<<g, 256, 0, c->stream>>>(c->dev, c->ctl, c->bufs, rp, c->XI2, C, bx, tk, im);
     }
+}
+// k_cp3's weight image (one workgroup, at context creation)
+template <class T, int NX, int NU>
+int cp3_imaget(raocp_ctx* c) {
+    typedef raocp::WL<T, NX, NX> WQ;
+    typedef raocp::WL<T, NU, NU> WR;
+    int rc;
+    if ((rc = c->alloc(&c->cp3img, (size_t)(2 * WQ::N + WR::N) * sizeof(T) / 8))) return rc;
+    raocp::k_cp3_image<T, NX, NU><<<1, 256, 0, c->stream>>>(c->dev, c->cp3img);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return RAOCP_OK;
+}
+int cp3_image(raocp_ctx* c) {
+    if (c->f32) {
+        if (c->nx == 20) return cp3_imaget<float, 20, 8>(c);
+        if (c->nx == 32) return cp3_imaget<float, 32, 12>(c);
+        return cp3_imaget<float, 64, 16>(c);
+    }
+    if (c->nx == 20) return cp3_imaget<double, 20, 8>(c);
+    return cp3_imaget<double, 32, 12>(c);
 }
 void launch_cp3(raocp_ctx* c, int part = 0) {
     if (c->sh_S > 0)
@@ -2265,6 +2294,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                     return bail(fail(RAOCP_ERR_HIP, "memset"));
             }
             c->cp_rows = c->cp3_grid;
+            if ((rc = cp3_image(c))) return bail(rc);
         }
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels

@@ -73,7 +73,8 @@ struct WL {
     const __attribute__((address_space(3))) T* base;
     __device__ __forceinline__ T get(int ro, int s) const { return base[(ro * KS + s) * 64 + (threadIdx.x & 63)]; }
     // every thread of the workgroup takes part (a __syncthreads follows)
-    static __device__ __forceinline__ void fill(__attribute__((address_space(3))) T* dst, const T* tab, int t) {
+    template <class DP>
+    static __device__ __forceinline__ void fill(DP dst, const T* tab, int t) {
         cglbp<T> M = (cglbp<T>)(tab + (size_t)t * R * K);
         for (int q = threadIdx.x; q < N; q += blockDim.x) {
             const int l = q & 63, lo = l & 15, h = l >> 4, s = (q >> 6) % KS, ro = (q >> 6) / KS;
@@ -205,11 +206,25 @@ struct Cp3Tasks {
     int lo[kCp3MaxR], hi[kCp3MaxR], t0[kCp3MaxR + 1];  // t0: first task of each range
 };
 
+// The weight fragments of the launch ([sqrtQ | sqrtR | sqrtPf] in LDS order), laid out once
+// per context: every workgroup copies them by LDS-DMA (one memory round trip in front of its
+// first task; the element-wise gather it replaces sat there too)
+template <class T, int NX, int NU>
+__global__ void __launch_bounds__(256) k_cp3_image(Dev p, double* img) {
+    typedef WL<T, NX, NX> WQ;
+    typedef WL<T, NU, NU> WR;
+    glbp<T> w = (glbp<T>)img;
+    WQ::fill(w, (const T*)p.SQ, p.crec[1].y);  // one table over the children (host check)
+    WR::fill(w + WQ::N, (const T*)p.SR, p.crec[1].z);
+    WQ::fill(w + WQ::N + WR::N, (const T*)p.SP, p.lrec[0].x);  // one over the leaves
+}
+
 // SH: a shard's launches (the xi2 store and ext2 paths compiled in; the unsharded kernel
 // keeps its registers)
 template <class T, int NX, int NU, bool SH>
 __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs bf, double* __restrict__ part,
-                                             double* __restrict__ xi2_, int C, int bx, Cp3Tasks tk) {
+                                             double* __restrict__ xi2_, int C, int bx, Cp3Tasks tk,
+                                             const double* __restrict__ img) {
     typedef typename MF<T>::v4 v4;
     static_assert(NX % 4 == 0 && NU % 4 == 0, "row layout needs nx, nu multiples of 4");
     constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
@@ -217,7 +232,7 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
     typedef WL<T, NU, NU> WR;
     __shared__ KpScratch<T> kps_[4];
     __shared__ double s_red[6][4];
-    __shared__ T wlds_[2 * WQ::N + WR::N];
+    __shared__ __attribute__((aligned(16))) T wlds_[2 * WQ::N + WR::N];
     const int m = p.m;
     const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4, wv = threadIdx.x >> 6;
     const int gw = blockIdx.x * (blockDim.x >> 6) + wv, nwv = gridDim.x * (blockDim.x >> 6);
@@ -230,15 +245,14 @@ __global__ void __launch_bounds__(256) k_cp3(Dev p, Ctl* __restrict__ ctl, Bufs 
     glbp<T> eo = (glbp<T>)bf.e1;    // eta+
     cglbp<T> cond = (cglbp<T>)p.cond;
     double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0, m4 = 0.0, m5 = 0.0;
-    const int done = ctl->done;
-    const T alpha = (T)ctl->alpha, ra = T(1) / alpha;
-    if (done) return;  // uniform over the grid: no barrier is reached
     typedef __attribute__((address_space(3))) T lT;
     lT* wl = (lT*)wlds_;
-    WQ::fill(wl, (const T*)p.SQ, p.crec[1].y);  // one table over the children (host check)
-    WR::fill(wl + WQ::N, (const T*)p.SR, p.crec[1].z);
-    WQ::fill(wl + WQ::N + WR::N, (const T*)p.SP, p.lrec[0].x);  // one over the leaves
+    dma((ldsd*)wlds_, img, (2 * WQ::N + WR::N) * (int)sizeof(T) / 8);  // k_cp3_image (N: multiples of 64)
+    const int done = ctl->done;
+    const T alpha = (T)ctl->alpha, ra = T(1) / alpha;
+    dma_wait();
     __syncthreads();
+    if (done) return;  // uniform over the grid
     const WQ wq{wl};
     const WR wr{wl + WQ::N};
     const WQ wp{wl + WQ::N + WR::N};

@@ -638,6 +638,21 @@ struct TierArg {
     int pl0[kMaxLevels + 1];  // first (kind, class) pair of the parents of level l (absolute)
 };
 
+// level l's node range {lo, hi, off} of this workgroup's subtree: computed from the kernel
+// argument when the tier is regular (wave-uniform arithmetic, no LDS round trip and no
+// barrier before the prologue's row copies are issued), else read from the staged table
+// (after tier_levels and a barrier)
+struct LvR {
+    int lo, hi, off;
+};
+__device__ __forceinline__ LvR lv_of(const Prologue& pl, const TierArg& ta, int l, int off) {
+    if (ta.regular) {
+        const int lo = ta.lo0[l] + (blockIdx.x + ta.boff) * ta.cnt[l];
+        return LvR{lo, lo + ta.cnt[l], off};
+    }
+    return LvR{pl.lo[l], pl.hi[l], pl.off[l]};
+}
+
 __device__ __forceinline__ void tier_levels(Prologue& pl, const TierArg& ta, const Rec* __restrict__ sub_lv, int L) {
     const int l = threadIdx.x;
     if (l > L) return;
@@ -704,27 +719,32 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     }
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
-    lds_sync();
+    if (!ta.regular) lds_sync();
     tstamp(p, pl, 1);
-    const int nall = pl.off[L] + (pl.hi[L] - pl.lo[L]), nnl = pl.off[L];
+    int nnl = 0;
+    for (int l = 0; l < L; ++l) nnl += ta.regular ? ta.cnt[l] : 0;
+    if (!ta.regular) nnl = pl.off[L];
+    const int nall = nnl + (ta.regular ? ta.cnt[L] : pl.hi[L] - pl.lo[L]);
     ldsd* XQ = smem + oXQ;
     ldsd* U = XQ + (size_t)nall * g.KP;
     ldsd* PB = U + (size_t)nnl * g.NUP;
     ldsd* NLd = PB + (FOLD ? 0 : rup(maxch * g.PS, 2));
     ldsd* CHd = NLd + 2 * nnl;
-    for (int l = 0; l <= L; ++l) {
-        const int cnt = pl.hi[l] - pl.lo[l];
+    for (int l = 0, off = 0; l <= L; ++l) {
+        const LvR lv = lv_of(pl, ta, l, off);
+        const int cnt = lv.hi - lv.lo;
+        off += cnt;
         if (l < L || leaves)
-            rows_in_r(dmaok, XQ + (size_t)pl.off[l] * g.KP, g.KP, (const double*)z + p.X0 + (size_t)pl.lo[l] * g.nx,
+            rows_in_r(dmaok, XQ + (size_t)lv.off * g.KP, g.KP, (const double*)z + p.X0 + (size_t)lv.lo * g.nx,
                       g.nx, g.nx, cnt, p.zpage, tid, nthr, rot);
         else  // q rows of the next tier's roots, already padded
-            dma_r(XQ + (size_t)pl.off[l] * g.KP, qbuf_ + (size_t)pl.lo[l] * g.KP, cnt * g.KP, rot);
+            dma_r(XQ + (size_t)lv.off * g.KP, qbuf_ + (size_t)lv.lo * g.KP, cnt * g.KP, rot);
         if (l < L) {
-            rows_in_r(dmaok, U + (size_t)pl.off[l] * g.NUP, g.NUP, (const double*)z + p.U0 + (size_t)pl.lo[l] * g.nu,
+            rows_in_r(dmaok, U + (size_t)lv.off * g.NUP, g.NUP, (const double*)z + p.U0 + (size_t)lv.lo * g.nu,
                       g.nu, g.nu, cnt, p.zpage, tid, nthr, rot);
-            dma_r(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt, rot);
+            dma_r(NLd + 2 * lv.off, (const double*)(p.ninfo + lv.lo), 2 * cnt, rot);
         }
-        if (l > 0) dma_r(CHd + 2 * (pl.off[l] - 1), (const double*)(p.cinfo + pl.lo[l]), 2 * cnt, rot);
+        if (l > 0) dma_r(CHd + 2 * (lv.off - 1), (const double*)(p.cinfo + lv.lo), 2 * cnt, rot);
     }
     if (!FOLD) zero_fill(PB, maxch * g.PS, tid, nthr);
     if (p.dyn_regtab) {
@@ -812,19 +832,24 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     if (FM == 2) dma_r(smem + oF, p.dF + (size_t)ta.pl0[0] * ts.F1, (ta.pl0[1] - ta.pl0[0]) * ts.F1, rot);
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
-    lds_sync();
+    if (!ta.regular) lds_sync();
     tstamp(p, pl, 1);
-    const int nnl = pl.off[L];
-    const int root = pl.lo[0];
+    int nnl = 0;
+    for (int l = 0; l < L; ++l) nnl += ta.regular ? ta.cnt[l] : 0;
+    if (!ta.regular) nnl = pl.off[L];
+    const int root = lv_of(pl, ta, 0, 0).lo;
     ldsd* XD = smem + oXD;
     ldsd* NLd = XD + (size_t)nnl * g.KF;
     ldsd* CHd = NLd + 2 * nnl;
     const double* xroot = (const double*)z + p.X0 + (size_t)root * g.nx;
     const double* zp = p.zpage;
-    for (int l = 0; l < L; ++l) {
-        const int cnt = pl.hi[l] - pl.lo[l];
-        ldsd* xd = XD + (size_t)pl.off[l] * g.KF;
-        const double* dl = dbuf_ + (size_t)pl.lo[l] * g.nu;
+    for (int l = 0, off = 0; l < L; ++l) {
+        const LvR lv = lv_of(pl, ta, l, off);
+        const LvR lc = lv_of(pl, ta, l + 1, off + (lv.hi - lv.lo));
+        const int cnt = lv.hi - lv.lo;
+        off += cnt;
+        ldsd* xd = XD + (size_t)lv.off * g.KF;
+        const double* dl = dbuf_ + (size_t)lv.lo * g.nu;
         if (dmaok) {
             const int cpr = g.KF >> 1, cx = g.nx >> 1, cd = (g.nx + g.nu) >> 1;
             const bool first = l == 0;
@@ -844,9 +869,9 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
                 xd[e] = v;
             }
         }
-        dma_r(NLd + 2 * pl.off[l], (const double*)(p.ninfo + pl.lo[l]), 2 * cnt, rot);
-        const int cc = pl.hi[l + 1] - pl.lo[l + 1];
-        dma_r(CHd + 2 * (pl.off[l + 1] - 1), (const double*)(p.cinfo + pl.lo[l + 1]), 2 * cc, rot);
+        dma_r(NLd + 2 * lv.off, (const double*)(p.ninfo + lv.lo), 2 * cnt, rot);
+        const int cc = lc.hi - lc.lo;
+        dma_r(CHd + 2 * (lc.off - 1), (const double*)(p.cinfo + lc.lo), 2 * cc, rot);
     }
     if (p.dyn_regtab) {
         TabCopy tc;
