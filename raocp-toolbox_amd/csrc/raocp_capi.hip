@@ -110,6 +110,11 @@ struct raocp_ctx {
         raocp::TierArg ta;       // the same, as a kernel argument, when the tier is regular
     };
     std::vector<TierPlan> tiers;
+    bool dyn_fuse = false;       // the tiered sweep in ONE launch (k_dyn_fuse, raocp_dynf.hip)
+    raocp::FuseArg fuse{};       // its plan (tickets / flags in fuse_sync)
+    size_t lds_fuse = 0;
+    bool fuse_st = false;        // its static three-array LDS layout (raocp::FuseStat)
+    unsigned* fuse_sync = nullptr;  // [epoch | error word | per tier: tickets, flags]
     double* x0 = nullptr;
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
     Ctl* ctl = nullptr;
@@ -512,6 +517,35 @@ void launch_dyn3(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* c
     }
 }
 
+// workgroups of k_dyn_fuse per CU at the context's block and LDS size
+// the k_dyn_fuse instantiation of a context (static LDS layout only where FuseStat has one)
+template <int NX, int NU>
+auto fuse_kernel(const raocp_ctx* c) {
+    if constexpr (raocp::FuseStat<NX, NU>::A > 0) {
+        if (c->fuse_st) return raocp::k_dyn_fuse<NX, NU, true, true>;
+    }
+    return raocp::k_dyn_fuse<NX, NU, true, false>;
+}
+struct FuseOcc {
+    template <int NX, int NU>
+    void run(raocp_ctx* c, int* per_cu) {
+        auto kf = fuse_kernel<NX, NU>(c);
+        allow_lds(kf, c->lds_fuse);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)kf, raocp::kFuseBlock, c->lds_fuse) !=
+            hipSuccess)
+            *per_cu = 0;
+    }
+};
+// the static layout's capacities (doubles; 0 where there is none)
+struct FuseStatOf {
+    template <int NX, int NU>
+    void run(int* x, int* a, int* b) {
+        *x = raocp::FuseStat<NX, NU>::X;
+        *a = raocp::FuseStat<NX, NU>::A;
+        *b = raocp::FuseStat<NX, NU>::B;
+    }
+};
+
 struct DynOp {
     // part: 0 whole projection; 1 the tiers' backward sweeps only; 2 the top and the
     // tiers' forward sweeps (a shard exchanges the roots' q rows in between)
@@ -533,6 +567,17 @@ struct DynOp {
             return ta;
         };
         auto tier_blocks = [&](int k) { return sharded ? c->tier_own[k].second : c->tiers[k].nsub; };
+        if (s > 0 && c->dyn_fuse && !sharded && part == 0) {
+            // the whole tiered sweep in one launch (raocp_dynf.hip), one workgroup per subtree
+            // of the deepest tier; it runs the deferred stopping test itself
+            raocp::FuseArg fa = c->fuse;
+            if (ck) fa.ck = *ck;
+            auto kf = fuse_kernel<NX, NU>(c);
+            allow_lds(kf, c->lds_fuse);
+            kf<<<c->tiers.back().nsub, raocp::kFuseBlock, c->lds_fuse, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->x0,
+                                                                                    fa);
+            return;
+        }
         if (s > 0) {
             // tiers below the top, deepest first (backward), the top, then the tiers (forward)
             if (part != 2)
@@ -615,6 +660,17 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
         return;
     }
     dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl, part, ck);
+}
+
+// the fused sweep's error word (a hand-off wait timed out, raocp_dynf.hip): checked after
+// every synchronised run that may have launched it; the context is unusable afterwards
+int fuse_err(raocp_ctx* c) {
+    if (!c->dyn_fuse || !c->fuse_sync) return RAOCP_OK;
+    int e = 0;
+    HIPCHK(hipMemcpy(&e, c->fuse_sync + 1, sizeof(int), hipMemcpyDeviceToHost));
+    if (e) return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dyn_fuse); RAOCP_DYN_FUSE=0 "
+                                        "selects the tier launches");
+    return RAOCP_OK;
 }
 
 // role: 0 all blocks; 1 nonleaf blocks only; 2 leaf blocks only (op_bench timing)
@@ -1012,6 +1068,8 @@ std::string kernel_name(const raocp_ctx* c, int op) {
                 for (int t = 0; t < c->N; ++t) add("k_dy3_fwd<" + T + ", " + nn + ">");
             } else if (c->dyn2) {
                 return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
+            } else if (c->cut > 0 && c->dyn_fuse && c->sh_S == 0) {
+                return "k_dyn_fuse<" + nn + ", true, " + b(c->fuse_st) + "> x1";
             } else if (c->cut > 0) {
                 for (int k = (int)c->tiers.size() - 1; k >= 0; --k)
                     add("k_dyn_bottom_back<" + nn + ", " + b(c->tiers[k].fold) + ">");
@@ -2006,6 +2064,113 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 }
             c->tiers.push_back(tp);
         }
+        // ---- the fused sweep (raocp_dynf.hip): the same tiers in one launch. Needs regular
+        // tiers of >= 2 subtrees per parent subtree, the top's F in LDS, and every workgroup
+        // of the grid co-resident (its waits are for running workgroups only).
+        {
+            c->dyn_fuse = false;
+            bool fz = c->cut > 0 && !c->tiers.empty() && c->tiers.size() <= (size_t)raocp::kFuseTiers && c->f_lds_top;
+            if (const char* e = getenv("RAOCP_DYN_FUSE")) fz = fz && atoi(e) != 0;
+            raocp::FuseArg& fa = c->fuse;
+            memset(&fa, 0, sizeof(fa));
+            // doubles: XD rows | S1 (the deepest tier) | S2 (the tiers above, the top)
+            size_t xd = 0, s1 = 0, s2 = fz ? c->lds_top / 8 : 0;
+            for (size_t k = 0; fz && k < c->tiers.size(); ++k) {
+                const auto& tp = c->tiers[k];
+                const int L = tp.s1 - tp.s0;
+                const int above = k == 0 ? 1 : c->tiers[k - 1].nsub;
+                const int r = tp.nsub / above;
+                const int per_parent = k == 0 ? stage_n(c->cut) : c->tiers[k - 1].ta.cnt[c->tiers[k - 1].s1 - c->tiers[k - 1].s0];
+                fz = fz && tp.ta.regular && tp.fm != 0 && r >= 2 && r * above == tp.nsub && r == per_parent;
+                if (!fz) break;
+                raocp::FuseTier& ft = fa.t[k];
+                size_t nnl = 0;
+                for (int l = 0; l < L; ++l) nnl += tp.ta.cnt[l];
+                const size_t nall = nnl + tp.ta.cnt[L];
+                const int c0 = cp[tp.s0], c1 = cp[tp.s1], p0 = pp[c0], p1 = pp[c1];
+                size_t npl = p1 - p0;
+                if (tp.fm == 2) {
+                    npl = 0;
+                    for (int l = 0; l < L; ++l) npl = std::max<size_t>(npl, tp.ta.pl0[l + 1] - tp.ta.pl0[l]);
+                }
+                ft.s0 = tp.s0;
+                ft.s1 = tp.s1;
+                ft.r = r;
+                ft.c0 = c0;
+                ft.c1 = c1;
+                ft.p0 = p0;
+                ft.p1 = p1;
+                ft.maxch = tp.maxch;
+                ft.fm = tp.fm;
+                ft.fold = tp.fold;
+                ft.nnl = (int)nnl;
+                ft.oXD = (int)xd;
+                ft.ngroups = above;
+                ft.ta = tp.ta;
+                ft.ta.boff = 0;
+                xd += raocp::rup((int)(nnl * KF), 2);
+                const size_t back = (tp.fold ? (size_t)(p1 - p0) * W1 : c->nkind * W1) + (c1 - c0) * RG1 + nall * KP +
+                                    nnl * NUP + (tp.fold ? 0 : raocp::rup(tp.maxch * PS, 2)) + recs(nnl + nall - 1);
+                const size_t fwd = (c1 - c0) * KM1 + npl * F1 + recs(nnl + nall - 1);
+                size_t& reg = k + 1 == c->tiers.size() ? s1 : s2;
+                reg = std::max(reg, std::max(back, fwd));
+            }
+            if (fz) {
+                fa.K = (int)c->tiers.size();
+                fa.nXD = (int)xd;
+                fa.oS1 = (int)xd;
+                // two regions (prefetching, raocp_dynf.hip) when they fit, else one shared
+                bool two = 8 * (xd + s1 + s2) <= kLds;
+                if (const char* e = getenv("RAOCP_FUSE_PREFETCH")) two = two && atoi(e) != 0;
+                fa.oS2 = two ? (int)(xd + s1) : fa.oS1;
+                c->lds_fuse = 8 * (two ? xd + s1 + s2 : xd + std::max(s1, s2));
+                fz = c->lds_fuse <= kLds;
+                // the static layout where the sizes have one and the regions fit it
+                int fx = 0, fa_ = 0, fb = 0;
+                dispatch(nx, nu, FuseStatOf{}, &fx, &fa_, &fb);
+                c->fuse_st = two && fa_ > 0 && xd <= (size_t)fx && s1 <= (size_t)fa_ && s2 <= (size_t)fb;
+                if (const char* e = getenv("RAOCP_FUSE_STATIC")) c->fuse_st = c->fuse_st && atoi(e) != 0;
+                if (c->fuse_st) {
+                    fa.oS1 = fa.oS2 = 0;
+                    c->lds_fuse = 0;
+                    fz = true;
+                }
+            }
+            if (fz) {
+                int per_cu = 0;
+                dispatch(nx, nu, FuseOcc{}, c, &per_cu);
+                fz = per_cu > 0 && (long)c->tiers.back().nsub <= (long)n_cus * per_cu;
+                if (getenv("RAOCP_DYN_VERBOSE"))
+                    fprintf(stderr, "[raocp] fused sweep: %d tiers, LDS %zu B (%s), %d workgroups, %d per CU x %d CUs%s\n",
+                            fa.K, c->lds_fuse, c->fuse_st ? "static" : (fa.oS2 != fa.oS1 ? "two regions" : "one region"), c->tiers.back().nsub, per_cu, n_cus, fz ? "" : " (not co-resident: tier launches)");
+            }
+            if (fz) {
+                size_t words = 2;
+                for (int k = 0; k < fa.K; ++k) words += 2 * (size_t)fa.t[k].ngroups;
+                if ((rc = c->alloc(&c->fuse_sync, words))) return bail(rc);
+                if (hipMemset(c->fuse_sync, 0, words * sizeof(unsigned)) != hipSuccess)
+                    return bail(fail(RAOCP_ERR_HIP, "hipMemset failed"));
+                fa.epoch = c->fuse_sync;
+                fa.err = (int*)(c->fuse_sync + 1);
+                unsigned* w = c->fuse_sync + 2;
+                for (int k = 0; k < fa.K; ++k) {
+                    fa.t[k].cnt = w;
+                    fa.t[k].flag = w + fa.t[k].ngroups;
+                    w += 2 * (size_t)fa.t[k].ngroups;
+                }
+                fa.s = c->cut;
+                fa.T = c->stage_ptr[c->cut];
+                fa.nb = stage_n(c->cut);
+                fa.c1 = cp[c->cut];
+                fa.p1 = pp[fa.c1];
+                fa.maxch_top = c->maxch_top;
+                fa.fold_top = c->fold_top;
+                long long ms = 1000;  // a wait normally lasts tens of microseconds
+                if (const char* e = getenv("RAOCP_FUSE_TIMEOUT_MS")) ms = std::max(1, atoi(e));
+                fa.timeout = ms * 100000LL;  // 100 MHz ticks
+            }
+            c->dyn_fuse = fz;
+        }
         if (getenv("RAOCP_DYN_VERBOSE")) {
             fprintf(stderr, "[raocp] dynamics plan: top stages [0,%d) lds %zu F%s%s", c->cut, c->lds_top,
                     c->f_lds_top ? "(lds)" : "(global)", c->fold_top ? " fold" : "");
@@ -2442,7 +2607,7 @@ int raocp_project_on_dynamics(raocp_ctx* c) {
     launch_dynamics(c, solo, 0, nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipStreamSynchronize(c->stream));
-    return RAOCP_OK;
+    return fuse_err(c);
 }
 
 int raocp_project_on_kernel(raocp_ctx* c) {
@@ -2476,6 +2641,7 @@ int raocp_prox_gconj(raocp_ctx* c, double alpha) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (int fe = fuse_err(c)) return fe;
     if (c->h_ctl->flags & 1) return fail(RAOCP_ERR_NAN_IN_BOX, "Rectangle constraint - 'nan' value cannot be constrained");
     return RAOCP_OK;
 }
@@ -2515,6 +2681,7 @@ int raocp_dual_project(raocp_ctx* c, int which) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    if (int fe = fuse_err(c)) return fe;
     if (c->h_ctl->flags & 1) return fail(RAOCP_ERR_NAN_IN_BOX, "Rectangle constraint - 'nan' value cannot be constrained");
     return RAOCP_OK;
 }
@@ -2674,6 +2841,7 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     c->cur_e = c->E[(fk + 1) % 2];
     if (iters) *iters = fk + 1;
     if (status) *status = fk < max_iters ? 0 : 1;
+    if (int fe = fuse_err(c)) return fe;
     if (c->h_ctl->flags & 1) return fail(RAOCP_ERR_NAN_IN_BOX, "Rectangle constraint - 'nan' value cannot be constrained");
     return RAOCP_OK;
 }
@@ -2984,6 +3152,7 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
     }
     if (iters) *iters = fk + 1;
     if (status) *status = fk < max_iters ? 0 : 1;
+    if (int fe = fuse_err(c)) return fe;
     if (c->h_ctl->flags & 1) return fail(RAOCP_ERR_NAN_IN_BOX, "Rectangle constraint - 'nan' value cannot be constrained");
     return RAOCP_OK;
 }
@@ -3062,7 +3231,7 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
     if (gx) (void)hipGraphExecDestroy(gx);
     HIPCHK(hipGetLastError());
     *ms_per_launch = ms / reps;
-    return RAOCP_OK;
+    return fuse_err(c);
 }
 
 // L (op 0) or L^T (op 1) with the launches cycling over `nsets` input / output buffer pairs:

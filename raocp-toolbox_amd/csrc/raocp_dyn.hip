@@ -322,7 +322,9 @@ __device__ __forceinline__ void back_fold(const Dev& p, const TB& tb, const INF&
 
 // ---- forward: u_i = K x_i + d_i (nodes [b, e)), x_j = F [x_i; d_i] (their children) ---
 // xd(i): padded row [x_i | d_i | 0] (KF); child rows also go to xdo(j) when XOUT.
-template <int KS, int NXc, int NUc, bool XOUT, class TB, class INF, class XDI, class XDO>
+// SCX: the children's x rows are stored write-through (st_sc1): another workgroup of the
+// same launch reads them (the fused sweep, raocp_dynf.hip)
+template <int KS, int NXc, int NUc, bool XOUT, bool SCX, class TB, class INF, class XDI, class XDO>
 __device__ __forceinline__ void fwd_phase_ks(const Dev& p, const TB& tb, const INF& inf, int b, int e, int cb, int ce,
                                              XDI xd, glbd* z, XDO xdo, int tid, int nthr) {
     const Geo<NXc, NUc> g(p);
@@ -350,14 +352,15 @@ __device__ __forceinline__ void fwd_phase_ks(const Dev& p, const TB& tb, const I
             double acc = dot_slice<cKCF>(f, xd(cj.z) + sl * KCF, KCF);
             acc = ks_reduce<KS>(acc);
             if (sl == 0) {
-                z[p.X0 + (size_t)j * g.nx + r] = acc;
+                if constexpr (SCX) st_sc1((double*)(z + p.X0 + (size_t)j * g.nx + r), acc);
+                else z[p.X0 + (size_t)j * g.nx + r] = acc;
                 if (XOUT) xdo(j)[r] = acc;
             }
         }
     }
 }
 
-template <int NXc, int NUc, bool XOUT, class TB, class INF, class XDI, class XDO>
+template <int NXc, int NUc, bool XOUT, bool SCX = false, class TB, class INF, class XDI, class XDO>
 __device__ __forceinline__ void fwd_phase(const Dev& p, const TB& tb, const INF& inf, int b, int e, XDI xd, glbd* z,
                                           XDO xdo, int tid, int nthr) {
     const int nx = NXc ? NXc : p.nx, nu = NUc ? NUc : p.nu;
@@ -365,9 +368,9 @@ __device__ __forceinline__ void fwd_phase(const Dev& p, const TB& tb, const INF&
     const Rec last = inf.nonleaf(e - 1);
     const int ce = last.x + last.y;
     const int items = (e - b) * nu + (ce - cb) * nx;
-    if (items * 4 <= nthr) fwd_phase_ks<4, NXc, NUc, XOUT>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
-    else if (items * 2 <= nthr) fwd_phase_ks<2, NXc, NUc, XOUT>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
-    else fwd_phase_ks<1, NXc, NUc, XOUT>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
+    if (items * 4 <= nthr) fwd_phase_ks<4, NXc, NUc, XOUT, SCX>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
+    else if (items * 2 <= nthr) fwd_phase_ks<2, NXc, NUc, XOUT, SCX>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
+    else fwd_phase_ks<1, NXc, NUc, XOUT, SCX>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
 }
 
 __device__ __forceinline__ glbd* pick3(const Bufs& bf, int k) {
@@ -501,6 +504,7 @@ struct Prologue {
     int lo[kMaxLevels + 1], hi[kMaxLevels + 1], off[kMaxLevels + 1];
     int sp[kMaxTopStages + 2];  // stage_ptr[0 .. s+1] (top)
     unsigned long long ts[64];  // diagnostics (p.stamps != nullptr)
+    int nts;                    // next stamp slot (k_dyn_fuse)
 };
 
 // diagnostics: thread 0 records the 100 MHz clock in LDS; flushed at the end of the kernel

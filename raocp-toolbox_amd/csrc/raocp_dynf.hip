@@ -1,0 +1,534 @@
+// raocp_dynf.hip — the tiered dynamics projection (raocp_dyn.hip) in ONE launch.
+// Included by raocp_kernels.hip after raocp_dyn.hip (inside namespace raocp).
+//
+// Same recursion and level routines as the tier kernels (cache.py:259-288; header of
+// raocp_dyn.hip), same cut into the top (stages [0, s)) and tiers t[0] .. t[K-1] below it
+// (t[K-1] the deepest, whose boundary is the leaves). The tier launches cost ≈ 8 µs each
+// at config 2 before their first level runs (launch gap, prologue, staging: five launches
+// per projection, profiles/r03_v3/stamps_c2.log); here one workgroup per subtree of the
+// deepest tier runs the whole projection:
+//
+//   backward: a workgroup sweeps its deepest-tier subtree, publishes the root's q row and
+//     takes a ticket on its parent subtree (the tier above). The workgroup that draws the
+//     group's last ticket sweeps the parent subtree (its children's q rows are published),
+//     and so on up; the last ticket of tier t[0] runs the top, backward and forward.
+//   forward: every workgroup that stopped at tier k waits for its parent subtree's forward
+//     (a flag), then sweeps its tier-k subtree forward and releases the flags of the tier
+//     below, down to its deepest-tier subtree. The workgroups that climbed do the same
+//     from the highest tier they reached.
+//
+// Nothing waits for a workgroup that has not started: a ticket never waits, and a flag is
+// released by the workgroup that drew the last ticket below it, which is running. The
+// host launches the fused sweep only when every workgroup of the grid is co-resident
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor), and every wait is bounded
+// (FuseArg::timeout): a timed-out workgroup sets the error word and leaves.
+//
+// Hand-offs across workgroups (MI355X: per-XCD L2s are not coherent): the roots' q rows
+// and the boundary x rows are stored write-through (st_sc1) and read with ld_sc1; the
+// storing waves drain (vmcnt 0), a barrier, then one lane takes the ticket / stores the
+// flag. Everything else a workgroup reads it wrote itself: d_i stays in LDS between the
+// backward and the forward sweep of a subtree (the rows XD_k, one region per tier, never
+// go through global memory), the tables and vectors are restaged per tier into a shared
+// scratch region.
+//
+// Tickets count up from 0 and are reset by the workgroup that runs the top (every ticket
+// of the launch has been drawn by then); flags carry the launch's tag (epoch + 1), and the
+// top stores the new epoch, so no host reset runs between launches. A launch that starts
+// with ctl->done set runs the protocol without the arithmetic (the next iterations' CP
+// kernels exit on the flag; the deferred stopping test, run by one waiting workgroup,
+// may set it during the launch: the projected buffer is then never read).
+
+constexpr int kFuseTiers = 4;
+// workgroup size of the fused sweep: at most 512 lanes leaves 256 VGPRs per lane (the tier,
+// top and forward routines inlined into one kernel spill at 1024 lanes' 128)
+constexpr int kFuseBlock = 512;
+
+struct FuseTier {
+    int s0, s1;        // roots at stage s0, levels s0 .. s1-1, boundary nodes at s1
+    int r;             // subtrees of this tier under one subtree of the tier above (or the top)
+    int c0, c1, p0, p1;
+    int maxch;         // widest child level of one subtree (P rows)
+    int fm;            // F rows in the forward sweep: 1 every pair of the tier, 2 per level
+    int fold;          // one-phase backward levels (per-pair WT tables, back_fold)
+    int nnl;           // nonleaf nodes of one subtree (levels 0 .. L-1)
+    int oXD;           // this tier's persistent XD rows (doubles from the LDS base)
+    int ngroups;       // subtrees of the tier above (tickets / flags)
+    TierArg ta;        // regular tier: level sizes and first nodes
+    unsigned* cnt;     // [ngroups] tickets
+    unsigned* flag;    // [ngroups] forward released by the tier above
+};
+
+// Static LDS layout (k_dyn_fuse<..., ST = true>, config 2's sizes): the XD rows, the deepest
+// tier's region S1 and the upper region S2 as three __shared__ arrays. The compiler tracks
+// LDS-DMA copies per LDS object (alias scopes of the module's LDS variables), so the levels
+// reading S1 / XD do not wait for a prefetch into S2 in flight, and the other way round; in
+// one dynamic array every LDS read after a prefetch waits for it (measured: the deepest
+// tier's levels 4.6 -> 9.8 us with the tier above prefetched during them).
+template <int NX, int NU>
+struct FuseStat {
+    static constexpr int X = 0, A = 0, B = 0;  // doubles
+};
+template <>
+struct FuseStat<20, 8> {
+    static constexpr int X = 1024, A = 7168, B = 11264;  // 8 + 56 + 88 KB
+};
+
+struct FuseArg {
+    int K;                          // tiers below the top
+    FuseTier t[kFuseTiers];
+    int s, T, nb, c1, p1, maxch_top; // the top: stages [0, s), nodes [0, T), nb boundary roots
+    int fold_top;                   // the top's backward levels in one phase
+    int oS1, oS2;                   // regions (doubles from the LDS base): the deepest tier, the
+                                    // tiers above and the top (oS2 == oS1: one shared region)
+    int nXD;                        // doubles of the persistent XD regions (zeroed at start)
+    unsigned* epoch;
+    int* err;                       // set to 1 by a workgroup whose wait timed out
+    long long timeout;              // per wait, 100 MHz ticks
+    ChkArg ck;                      // the previous CP iteration's stopping test
+};
+
+// diagnostics: thread 0 stamps the next slot of this workgroup's path (p.stamps != nullptr)
+__device__ __forceinline__ void fz_stamp(const Dev& p, Prologue& pl) {
+    if (p.stamps && threadIdx.x == 0) pl.ts[pl.nts++ & 63] = __builtin_amdgcn_s_memrealtime();
+}
+
+__device__ __forceinline__ unsigned ld_u32_sc1(const unsigned* p) {
+    return __hip_atomic_load((const gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_u32_sc1(unsigned* p, unsigned v) {
+    __hip_atomic_store((gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// level l of subtree `sub` of a regular tier: first node and count
+__device__ __forceinline__ int fz_lo(const TierArg& ta, int l, int sub) { return ta.lo0[l] + sub * ta.cnt[l]; }
+
+__device__ __forceinline__ void fz_levels(Prologue& pl, const TierArg& ta, int L, int sub) {
+    const int l = threadIdx.x;
+    if (l > L) return;
+    int off = 0;
+    for (int k = 0; k < l; ++k) off += ta.cnt[k];
+    pl.lo[l] = fz_lo(ta, l, sub);
+    pl.hi[l] = pl.lo[l] + ta.cnt[l];
+    pl.off[l] = off;
+}
+
+// backward sweep of subtree `sub` of tier tt in two parts: fz_back_stage issues the copies
+// of everything the subtree's own data holds (tables, x / u rows, records), so a workgroup
+// can prefetch a subtree before it knows whether it will sweep it; fz_back_wait copies the
+// boundary q rows other workgroups published (not for the deepest tier, whose boundary is
+// the leaves' x) and waits for every copy in flight; fz_back_levels runs the levels and
+// publishes the root's q row (padded) to qbuf. A prefetch issued between the two overlaps
+// the levels (the waits are vmcnt(0): a prefetch issued before a wait is waited for).
+// region: [W (all kinds) | RG (c0..c1) | XQ (nall, KP) | U (nnl, NUP) | P | NL | CH];
+// fold: W -> WT (pairs p0..p1), no P rows
+template <int NXc, int NUc>
+struct BackLds {
+    ldsd *W, *RG, *XQ, *U, *PB, *NL, *CH;
+    int nall;
+    __device__ __forceinline__ BackLds(const Dev& p, const FuseTier& tt, ldsd* scr) {
+        const Geo<NXc, NUc> g(p);
+        const TabSize<NXc, NUc> ts(g);
+        const int L = tt.s1 - tt.s0;
+        nall = tt.nnl + tt.ta.cnt[L];
+        W = scr;
+        RG = W + (tt.fold ? tt.p1 - tt.p0 : p.nkind) * ts.W1;
+        XQ = RG + (tt.c1 - tt.c0) * ts.RG1;
+        U = XQ + (size_t)nall * g.KP;
+        PB = U + (size_t)tt.nnl * g.NUP;
+        NL = PB + (tt.fold ? 0 : rup(tt.maxch * g.PS, 2));
+        CH = NL + 2 * tt.nnl;
+    }
+};
+
+template <int NXc, int NUc>
+__device__ void fz_back_stage(const Dev& p, const glbd* z, const FuseTier& tt, int sub, bool leaves, ldsd* scr) {
+    const Geo<NXc, NUc> g(p);
+    const TabSize<NXc, NUc> ts(g);
+    const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const TierArg& ta = tt.ta;
+    const int L = tt.s1 - tt.s0;
+    const BackLds<NXc, NUc> ly(p, tt, scr);
+    int rot = p.dyn_rot ? 0 : -1;
+    if (tt.fold) dma_r(ly.W, p.dWT + (size_t)tt.p0 * ts.W1, (tt.p1 - tt.p0) * ts.W1, rot);
+    else dma_r(ly.W, p.dW, p.nkind * ts.W1, rot);
+    dma_r(ly.RG, p.dRG + (size_t)tt.c0 * ts.RG1, (tt.c1 - tt.c0) * ts.RG1, rot);
+    for (int l = 0, off = 0; l <= L; ++l) {
+        const int lo = fz_lo(ta, l, sub), cnt = ta.cnt[l];
+        if (l < L || leaves)
+            rows_in_r(dmaok, ly.XQ + (size_t)off * g.KP, g.KP, (const double*)z + p.X0 + (size_t)lo * g.nx, g.nx, g.nx,
+                      cnt, p.zpage, tid, nthr, rot);
+        if (l < L) {
+            rows_in_r(dmaok, ly.U + (size_t)off * g.NUP, g.NUP, (const double*)z + p.U0 + (size_t)lo * g.nu, g.nu, g.nu,
+                      cnt, p.zpage, tid, nthr, rot);
+            dma_r(ly.NL + 2 * off, (const double*)(p.ninfo + lo), 2 * cnt, rot);
+        }
+        if (l > 0) dma_r(ly.CH + 2 * (off - 1), (const double*)(p.cinfo + lo), 2 * cnt, rot);
+        off += cnt;
+    }
+}
+
+template <int NXc, int NUc>
+__device__ void fz_back_wait(const Dev& p, const double* qbuf_, const FuseTier& tt, int sub, bool leaves, ldsd* scr,
+                             Prologue& pl) {
+    const Geo<NXc, NUc> g(p);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const TierArg& ta = tt.ta;
+    const BackLds<NXc, NUc> ly(p, tt, scr);
+    const int L = tt.s1 - tt.s0;
+    fz_levels(pl, ta, L, sub);
+    // (LDS stores here, not in the stage: a store into a region with LDS-DMA copies in
+    // flight waits for them)
+    if (!tt.fold) zero_fill(ly.PB, tt.maxch * g.PS, tid, nthr);
+    if (!leaves) {  // q rows of the tier below's roots, published by other workgroups (issued last:
+                    // their wait covers the staging copies still in flight)
+        const int lo = fz_lo(ta, L, sub), cnt = ta.cnt[L];
+        for (int e = tid; e < cnt * g.KP; e += nthr)
+            ly.XQ[(size_t)tt.nnl * g.KP + e] = ld_sc1(qbuf_ + (size_t)lo * g.KP + e);
+    }
+    dma_wait();
+    lds_sync();
+    fz_stamp(p, pl);
+}
+
+template <int NXc, int NUc>
+__device__ void fz_back_levels(const Dev& p, double* qbuf_, const FuseTier& tt, int sub, bool leaves, ldsd* smem,
+                               ldsd* scr, Prologue& pl) {
+    const Geo<NXc, NUc> g(p);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const TierArg& ta = tt.ta;
+    const int L = tt.s1 - tt.s0;
+    const BackLds<NXc, NUc> ly(p, tt, scr);
+    const ldsrec* NL = (const ldsrec*)ly.NL;
+    const ldsrec* CH = (const ldsrec*)ly.CH;
+    const TabsT<const ldsd*, const ldsd*> tb{ly.W, ly.RG, nullptr, nullptr, tt.c0, tt.fold ? tt.p0 : 0};
+    ldsd* XD = smem + tt.oXD;
+    for (int l = L - 1; l >= 0; --l) {
+        const InfoT<const ldsrec*> inf{NL + pl.off[l], pl.lo[l], CH + pl.off[l + 1] - 1, pl.lo[l + 1]};
+        const LRows xq_l{ly.XQ + (size_t)pl.off[l] * g.KP, pl.lo[l], g.KP};
+        const LRows xq_c{ly.XQ + (size_t)pl.off[l + 1] * g.KP, pl.lo[l + 1], g.KP};
+        const LRows ur{ly.U + (size_t)pl.off[l] * g.NUP, pl.lo[l], g.NUP};
+        const LRows dl{XD + (size_t)pl.off[l] * g.KF + g.nx, pl.lo[l], g.KF};  // d_i into XD row i, cols nx..
+        const double sign = (l + 1 == L && leaves) ? -1.0 : 1.0;
+        if (tt.fold) {
+            back_fold<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], xq_c, sign, xq_l, ur, xq_l, dl, tid, nthr);
+            lds_sync();
+            continue;
+        }
+        const LRows pr{ly.PB, pl.lo[l + 1], g.PS};
+        back_phase_a<NXc, NUc>(p, tb, inf, pl.lo[l + 1], pl.hi[l + 1], xq_c, sign, pr, tid, nthr);
+        lds_sync();
+        back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, xq_l, dl, tid, nthr);
+        lds_sync();
+    }
+    // the root's q row (XQ row 0, zero tail) for the tier above
+    const int root = fz_lo(ta, 0, sub);
+    if (tid < g.KP) st_sc1(qbuf_ + (size_t)root * g.KP + tid, ly.XQ[tid]);
+}
+
+// forward sweep of subtree `sub` of tier tt, in two parts: fz_fwd_stage issues the table
+// and record copies (a waiting workgroup issues them before its wait), fz_fwd_run takes the
+// root's x row published by the tier above (or the top) and runs the levels. sc: the
+// boundary children's x rows are published (every tier but the deepest).
+// scratch: [KM (c0..c1) | F (fm 1: pairs p0..p1; 2: one level's pairs) | NL | CH]
+template <int NXc, int NUc>
+struct FwdLds {
+    ldsd *KM, *F, *NL, *CH;
+    __device__ __forceinline__ FwdLds(const Dev& p, const FuseTier& tt, ldsd* scr) {
+        const Geo<NXc, NUc> g(p);
+        const TabSize<NXc, NUc> ts(g);
+        const int L = tt.s1 - tt.s0;
+        int npl = tt.p1 - tt.p0;
+        if (tt.fm == 2) {
+            npl = 0;
+            for (int l = 0; l < L; ++l) npl = max(npl, tt.ta.pl0[l + 1] - tt.ta.pl0[l]);
+        }
+        KM = scr;
+        F = KM + (tt.c1 - tt.c0) * ts.KM1;
+        NL = F + npl * ts.F1;
+        CH = NL + 2 * tt.nnl;
+    }
+};
+
+template <int NXc, int NUc>
+__device__ void fz_fwd_stage(const Dev& p, const FuseTier& tt, int sub, ldsd* scr) {
+    const Geo<NXc, NUc> g(p);
+    const TabSize<NXc, NUc> ts(g);
+    const TierArg& ta = tt.ta;
+    const int L = tt.s1 - tt.s0;
+    const FwdLds<NXc, NUc> ly(p, tt, scr);
+    int rot = p.dyn_rot ? 0 : -1;
+    dma_r(ly.KM, p.dKM + (size_t)tt.c0 * ts.KM1, (tt.c1 - tt.c0) * ts.KM1, rot);
+    if (tt.fm == 1) dma_r(ly.F, p.dF + (size_t)tt.p0 * ts.F1, (tt.p1 - tt.p0) * ts.F1, rot);
+    else dma_r(ly.F, p.dF + (size_t)ta.pl0[0] * ts.F1, (ta.pl0[1] - ta.pl0[0]) * ts.F1, rot);
+    for (int l = 0, off = 0; l <= L; ++l) {
+        const int lo = fz_lo(ta, l, sub), cnt = ta.cnt[l];
+        if (l < L) dma_r(ly.NL + 2 * off, (const double*)(p.ninfo + lo), 2 * cnt, rot);
+        if (l > 0) dma_r(ly.CH + 2 * (off - 1), (const double*)(p.cinfo + lo), 2 * cnt, rot);
+        off += cnt;
+    }
+    (void)g;
+}
+
+template <int NXc, int NUc>
+__device__ void fz_fwd_run(const Dev& p, glbd* z, const FuseTier& tt, int sub, bool sc, ldsd* smem, ldsd* scr,
+                           Prologue& pl) {
+    const Geo<NXc, NUc> g(p);
+    const TabSize<NXc, NUc> ts(g);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const TierArg& ta = tt.ta;
+    const int L = tt.s1 - tt.s0;
+    const FwdLds<NXc, NUc> ly(p, tt, scr);
+    ldsd* XD = smem + tt.oXD;
+    const int root = fz_lo(ta, 0, sub);
+    fz_levels(pl, ta, L, sub);
+    if (tid < g.nx) XD[tid] = ld_sc1((const double*)z + p.X0 + (size_t)root * g.nx + tid);
+    dma_wait();
+    lds_sync();
+    fz_stamp(p, pl);
+    const ldsrec* NL = (const ldsrec*)ly.NL;
+    const ldsrec* CH = (const ldsrec*)ly.CH;
+    TabsT<const ldsd*, const ldsd*> tb{nullptr, nullptr, ly.KM, ly.F, tt.c0, tt.fm == 1 ? tt.p0 : ta.pl0[0]};
+    for (int l = 0; l < L; ++l) {
+        if (tt.fm == 2 && l > 0) {  // level l-1's products are done (the barrier that ended it)
+            tb.p0 = ta.pl0[l];
+            dma(ly.F, p.dF + (size_t)ta.pl0[l] * ts.F1, (ta.pl0[l + 1] - ta.pl0[l]) * ts.F1);
+            dma_wait();
+            lds_sync();
+        }
+        const InfoT<const ldsrec*> inf{NL + pl.off[l], pl.lo[l], CH + pl.off[l + 1] - 1, pl.lo[l + 1]};
+        const LRows xd_l{XD + (size_t)pl.off[l] * g.KF, pl.lo[l], g.KF};
+        if (l + 1 < L) {
+            const LRows xd_c{XD + (size_t)pl.off[l + 1] * g.KF, pl.lo[l + 1], g.KF};
+            fwd_phase<NXc, NUc, true>(p, tb, inf, pl.lo[l], pl.hi[l], xd_l, z, xd_c, tid, nthr);
+        } else if (sc) {
+            fwd_phase<NXc, NUc, false, true>(p, tb, inf, pl.lo[l], pl.hi[l], xd_l, z, xd_l, tid, nthr);
+        } else {
+            fwd_phase<NXc, NUc, false>(p, tb, inf, pl.lo[l], pl.hi[l], xd_l, z, xd_l, tid, nthr);
+        }
+        lds_sync();
+    }
+}
+
+// the top (stages [0, s), nodes [0, T)), backward then forward, as k_dyn_top: the boundary
+// q rows come from tier t[0]'s roots (ld_sc1), the boundary x rows are published
+// [W | RG | KM | F (FL) | XQ (T, KP) | QB (nb, KP) | U (T, NUP) | XD (T, KF) | P | NL | CH]
+template <int NXc, int NUc, bool FL>
+__device__ void fz_top(const Dev& p, glbd* z, const double* qbuf_, const double* x0_, const FuseArg& fa, ldsd* scr,
+                       Prologue& pl) {
+    const Geo<NXc, NUc> g(p);
+    const TabSize<NXc, NUc> ts(g);
+    const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int s = fa.s, T = fa.T, nb = fa.nb, c1 = fa.c1, p1 = fa.p1;
+    const bool fold = fa.fold_top;
+    const int nW = (fold ? p1 : p.nkind) * ts.W1;
+    const int oW = 0, oRG = oW + nW, oKM = oRG + c1 * ts.RG1, oF = oKM + c1 * ts.KM1;
+    const int oXQ = oF + (FL ? p1 * ts.F1 : 0), oQB = oXQ + T * g.KP, oU = oQB + nb * g.KP, oXD = oU + T * g.NUP;
+    const int oP = oXD + T * g.KF, oNL = oP + (fold ? 0 : rup(fa.maxch_top * g.PS, 2)), oCH = oNL + 2 * T;
+    int rot = p.dyn_rot ? 0 : -1;
+    dma_r(scr + oW, fold ? p.dWT : p.dW, nW, rot);
+    dma_r(scr + oRG, p.dRG, c1 * ts.RG1, rot);
+    dma_r(scr + oKM, p.dKM, c1 * ts.KM1, rot);
+    if (FL) dma_r(scr + oF, p.dF, p1 * ts.F1, rot);
+    dma_r(scr + oNL, (const double*)p.ninfo, 2 * T, rot);
+    dma_r(scr + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1), rot);
+    if (tid <= s + 1) pl.sp[tid] = p.stage_ptr[tid];
+    rows_in_r(dmaok, scr + oXQ, g.KP, (const double*)z + p.X0, g.nx, g.nx, T, p.zpage, tid, nthr, rot);
+    rows_in_r(dmaok, scr + oU, g.NUP, (const double*)z + p.U0, g.nu, g.nu, T, p.zpage, tid, nthr, rot);
+    zero_fill(scr + oXD, T * g.KF, tid, nthr);
+    if (!fold) zero_fill(scr + oP, fa.maxch_top * g.PS, tid, nthr);
+    // the boundary q rows last: their wait covers the copies above
+    for (int e = tid; e < nb * g.KP; e += nthr) scr[oQB + e] = ld_sc1(qbuf_ + (size_t)T * g.KP + e);
+    dma_wait();
+    lds_sync();
+    fz_stamp(p, pl);
+    typedef typename std::conditional<FL, const ldsd*, const glbd*>::type PF;
+    const TabsT<const ldsd*, PF> tb{scr + oW, scr + oRG, scr + oKM, FL ? (PF)(scr + oF) : (PF)((const glbd*)p.dF), 0, 0};
+    const InfoT<const ldsrec*> inf{(const ldsrec*)(scr + oNL), 0, (const ldsrec*)(scr + oCH), 1};
+    ldsd* XD = scr + oXD;
+    const LRows xq{scr + oXQ, 0, g.KP}, qb{scr + oQB, T, g.KP}, ur{scr + oU, 0, g.NUP}, xd{XD, 0, g.KF};
+    const LRows dlds{XD + g.nx, 0, g.KF};
+    for (int t = s - 1; t >= 0; --t) {
+        const int b = pl.sp[t], e = pl.sp[t + 1];
+        const int cb = e, ce = pl.sp[t + 2];
+        if (fold) {
+            if (t + 1 < s) back_fold<NXc, NUc>(p, tb, inf, b, e, xq, 1.0, xq, ur, xq, dlds, tid, nthr);
+            else back_fold<NXc, NUc>(p, tb, inf, b, e, qb, 1.0, xq, ur, xq, dlds, tid, nthr);
+            lds_sync();
+            continue;
+        }
+        const LRows pr{scr + oP, cb, g.PS};
+        if (t + 1 < s) back_phase_a<NXc, NUc>(p, tb, inf, cb, ce, xq, 1.0, pr, tid, nthr);
+        else back_phase_a<NXc, NUc>(p, tb, inf, cb, ce, qb, 1.0, pr, tid, nthr);
+        lds_sync();
+        back_phase_b<NXc, NUc>(p, tb, inf, b, e, pr, xq, ur, xq, dlds, tid, nthr);
+        lds_sync();
+    }
+    fz_stamp(p, pl);
+    if (tid < g.nx) {
+        const double v = ((const glbd*)x0_)[tid];
+        XD[tid] = v;
+        z[p.X0 + tid] = v;  // x_0 = x0bar (cache.py:282)
+    }
+    lds_sync();
+    for (int t = 0; t < s; ++t) {
+        const int b = pl.sp[t], e = pl.sp[t + 1];
+        if (t + 1 < s) fwd_phase<NXc, NUc, true>(p, tb, inf, b, e, xd, z, xd, tid, nthr);
+        else fwd_phase<NXc, NUc, false, true>(p, tb, inf, b, e, xd, z, xd, tid, nthr);
+        lds_sync();
+    }
+}
+
+// stores of this workgroup drained, then one lane publishes
+__device__ __forceinline__ void fz_drain() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+}
+
+template <int NXc, int NUc, bool FL, bool ST>
+__global__ void __launch_bounds__(kFuseBlock) k_dyn_fuse(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                         double* qbuf_, const double* x0_, FuseArg fa) {
+    extern __shared__ __attribute__((aligned(16))) double smem_[];
+    typedef FuseStat<NXc, NUc> FS;
+    __shared__ __attribute__((aligned(16))) double lx_[ST ? FS::X : 2];
+    __shared__ __attribute__((aligned(16))) double la_[ST ? FS::A : 2];
+    __shared__ __attribute__((aligned(16))) double lb_[ST ? FS::B : 2];
+    __shared__ Prologue pl;
+    __shared__ unsigned s_tk;
+    __shared__ int s_ok;
+    const int tid = threadIdx.x;
+    // regions: XB the XD rows; S1 the deepest tier (backward, then its forward prefetched as
+    // soon as it is free); S2 the tiers above and the top (the tier above the deepest
+    // prefetched while the deepest is swept, all but its boundary q rows). Dynamic layout:
+    // S2 == S1 when both do not fit.
+    ldsd* smem = (ldsd*)smem_;
+    ldsd* XB = ST ? (ldsd*)lx_ : smem;
+    ldsd* S1 = ST ? (ldsd*)la_ : smem + fa.oS1;
+    ldsd* S2 = ST ? (ldsd*)lb_ : smem + fa.oS2;
+    const bool two = ST || fa.oS2 != fa.oS1;
+    glbd* z = dyn_z(bf, zsel, ctl);
+    if (tid == 0) pl.nts = 0;  // diagnostics: stamps of this workgroup's path (fz_stamp)
+    fz_stamp(p, pl);
+    // this workgroup's subtree at tier k: blockIdx.x / (r of every tier below k)
+    auto sub_at = [&](int k) {
+        int b = blockIdx.x;
+        for (int j = fa.K - 1; j > k; --j) b /= fa.t[j].r;
+        return b;
+    };
+    const int D = fa.K - 1;  // the deepest tier
+    // the prologue copies are issued before the epoch and stop flag are read (their loads
+    // wait where the values are used)
+    fz_back_stage<NXc, NUc>(p, z, fa.t[D], blockIdx.x, true, S1);
+    const bool pre2 = two && fa.K >= 2;
+    zero_fill(XB, fa.nXD, tid, blockDim.x);  // XD rows: zero tails (the back sweeps write d, the forward x)
+    const unsigned tag = ld_u32_sc1(fa.epoch) + 1u;
+    const bool work = !ctl_done(ctl);
+    if (tid == 0) s_ok = 1;
+    int k = D, sub = blockIdx.x;
+    bool top = false;
+    // backward, up the tiers while this workgroup draws the last ticket of its group
+    for (;;) {
+        const FuseTier& tt = fa.t[k];
+        ldsd* R = k == D ? S1 : S2;
+        // prefetches overlapping the levels (static layout: the levels' LDS reads do not wait
+        // for them): the subtree of the tier above, all but its boundary q rows, while the
+        // deepest is swept; the deepest tier's forward tables while the tier above it is
+        // swept (S1 is free again). Each region's code path names its region statically.
+        if (work && k == D) {
+            fz_back_wait<NXc, NUc>(p, qbuf_, tt, sub, true, S1, pl);
+            if (pre2) fz_back_stage<NXc, NUc>(p, z, fa.t[D - 1], sub_at(D - 1), false, S2);
+            fz_back_levels<NXc, NUc>(p, qbuf_, tt, sub, true, XB, S1, pl);
+        } else if (work) {
+            if (!(k == D - 1 && pre2)) fz_back_stage<NXc, NUc>(p, z, tt, sub, false, S2);
+            fz_back_wait<NXc, NUc>(p, qbuf_, tt, sub, false, S2, pl);
+            if (k == D - 1 && two) fz_fwd_stage<NXc, NUc>(p, fa.t[D], sub_at(D), S1);
+            fz_back_levels<NXc, NUc>(p, qbuf_, tt, sub, false, XB, S2, pl);
+        }
+        fz_stamp(p, pl);
+        fz_drain();
+        const int grp = sub / tt.r;
+        if (tid == 0) s_tk = __hip_atomic_fetch_add(tt.cnt + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+        const unsigned old = s_tk;
+        fz_stamp(p, pl);
+        // this tier's forward tables: staged now where the region stays free until the forward
+        // (the waiting workgroups always; the deepest tier in S1 also on the way up)
+        const bool last = old + 1u == (unsigned)tt.r;
+        if (work && (!last || (k == D && two && fa.K == 1))) {
+            if (k == D) fz_fwd_stage<NXc, NUc>(p, tt, sub, S1);
+            else fz_fwd_stage<NXc, NUc>(p, tt, sub, S2);
+        }
+        if (!last) {
+            // the deferred stopping test: one waiting workgroup per launch (tt.r >= 2)
+            if (fa.ck.on && k == D && grp == 0 && old == 0u && tid < 64) cp_check_wave(fa.ck);
+            break;
+        }
+        if (k == 0) {
+            top = true;
+            break;
+        }
+        sub = grp;
+        --k;
+    }
+    if (top) {
+        if (work) fz_top<NXc, NUc, FL>(p, z, qbuf_, x0_, fa, S2, pl);
+        fz_stamp(p, pl);
+        // the forward tables of tier t[0] (S2 is free again; S1 holds the deepest tier's
+        // forward when the two differ): issued before the resets, the drain and the flag
+        if (work && (fa.K > 1 || !two)) fz_fwd_stage<NXc, NUc>(p, fa.t[0], sub_at(0), S2);
+        // every ticket of the launch has been drawn: reset them for the next launch
+        for (int kk = 0; kk < fa.K; ++kk)
+            for (int q = tid; q < fa.t[kk].ngroups; q += blockDim.x) st_u32_sc1(fa.t[kk].cnt + q, 0u);
+        fz_drain();
+        if (tid == 0) {
+            st_u32_sc1(fa.epoch, tag);
+            st_u32_sc1(fa.t[0].flag, tag);
+        }
+    } else {
+        // wait for the forward sweep of the parent subtree
+        if (tid == 0) {
+            const unsigned* f = fa.t[k].flag + sub_at(k) / fa.t[k].r;
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            while (ld_u32_sc1(f) != tag) {
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > fa.timeout) {
+                    s_ok = 0;
+                    __hip_atomic_store(fa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();
+        if (!s_ok) return;
+        fz_stamp(p, pl);
+    }
+    // forward, down from tier k to the deepest
+    const int kw = k;  // where this workgroup stopped climbing (0 for the top's)
+    for (; k < fa.K; ++k) {
+        const FuseTier& tt = fa.t[k];
+        const bool deepest = k == D;
+        const int sk = sub_at(k);
+        if (work) {
+            // staged already: the tier it waited at, or t[0] on the top's workgroup (after
+            // the top); the deepest tier whenever S1 is its own region
+            const bool staged = (k == kw && (!top || fa.K > 1 || !two)) || (deepest && two);
+            if (deepest) {
+                if (!staged) fz_fwd_stage<NXc, NUc>(p, tt, sk, S1);
+                fz_fwd_run<NXc, NUc>(p, z, tt, sk, false, XB, S1, pl);
+            } else {
+                if (!staged) fz_fwd_stage<NXc, NUc>(p, tt, sk, S2);
+                fz_fwd_run<NXc, NUc>(p, z, tt, sk, true, XB, S2, pl);
+            }
+        }
+        fz_stamp(p, pl);
+        if (!deepest) {
+            fz_drain();
+            if (tid == 0) st_u32_sc1(fa.t[k + 1].flag + sk, tag);
+        }
+    }
+    // diagnostics: the top's workgroup (the critical path) to slots 0..63, workgroup 0 (a
+    // waiting one, unless it ran the top) to 64..127
+    if (p.stamps && tid == 0 && (top || blockIdx.x == 0))
+        for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(top ? 0 : 64) + q] = pl.ts[q];
+}

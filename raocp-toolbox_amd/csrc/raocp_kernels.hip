@@ -313,6 +313,7 @@ __device__ __forceinline__ GroupIdx group_index(int G, int begin, int end, int b
 }
 
 #include "raocp_dyn.hip"
+#include "raocp_dynf.hip"
 
 // ---- LDS-DMA staging for the CP kernels (see raocp_dyn.hip: dma_gen) ----------------
 // copy nbytes from an arbitrarily aligned global address into LDS at dst (16-B aligned):

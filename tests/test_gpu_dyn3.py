@@ -113,17 +113,20 @@ def test_dyn3_deferred_stopping_test_matches_eager(iters, stop):
 
 def test_kernel_info_lists_the_projection_launches():
     """raocp_kernel_info(9) names every launch of one projection as "name xcount" terms
-    (bench.py sums their PMC traffic): 2 tiers + the top at config 2, one k_dy3_back and
-    one k_dy3_fwd per nonleaf stage with RAOCP_DYN3=1."""
+    (bench.py sums their PMC traffic): the fused sweep (one launch) at config 2, 2 tiers +
+    the top with RAOCP_DYN_FUSE=0, one k_dy3_back and one k_dy3_fwd per nonleaf stage with
+    RAOCP_DYN3=1."""
     import re
     r = recipe_config(2)
     prob = build_problem(r)[1]
-    for env, want in (({}, None), ({"RAOCP_DYN3": "1"}, "dy3")):
+    for env, want in (({}, "fuse"), ({"RAOCP_DYN_FUSE": "0"}, None), ({"RAOCP_DYN3": "1"}, "dy3")):
         cache = _with_env(env, lambda: core.Cache(prob))
         terms = [re.fullmatch(r"(k_\w+<[^>]*>) x(\d+)", t) for t in cache.native.kernel_info(9).split(" + ")]
         assert all(terms), cache.native.kernel_info(9)
         cnt = {m.group(1).split("<")[0]: int(m.group(2)) for m in terms}
         if want == "dy3":
             assert cnt == {"k_dy3_back": 12, "k_dy3_fwd": 12}
+        elif want == "fuse":
+            assert cnt == {"k_dyn_fuse": 1}
         else:
             assert cnt["k_dyn_top"] == 1 and cnt["k_dyn_bottom_back"] == cnt["k_dyn_bottom_fwd"] >= 1

@@ -1,0 +1,113 @@
+"""GPU parity of the fused tiered dynamics sweep k_dyn_fuse (raocp_dynf.hip): the tiers of
+raocp_dyn.hip in one launch, one workgroup per deepest-tier subtree, tickets up the tiers
+and flags down (cache.py:259-288). The default of fp64 trees whose tier plan is regular
+and co-resident (config 2); RAOCP_DYN_FUSE=0 keeps the tier launches.
+
+The fused sweep runs the tier kernels' level routines on the same operands (d_i stays in
+LDS instead of a global round trip); its top runs on 512 lanes where k_dyn_top has 1,024,
+which changes the split-k summation order of the top's dot products. So: against the tier
+launches 1e-13 of the largest entry (projection), 1e-10 per residual entry (CP trace);
+against itself after 1,000 back-to-back launches (the tickets and flags carry over between
+launches without a host reset) bit for bit; against the oracle 1e-12 of the largest entry
+(projection), 1e-8 per residual entry (CP trace).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import raocp.core as core
+from raocp.problems import build_problem, recipe_config, recipe_synthetic
+from helpers import rel_err, trace_rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _recipe(cfg):
+    if cfg == "quad":  # branching 4, tiers of 4-ary subtrees
+        return recipe_synthetic(np.full((4, 4), .25), np.full(4, .25), 6, 6, 20, 8, seed=6)
+    if cfg == "bin10":
+        return recipe_synthetic(np.full((2, 2), .5), np.full(2, .5), 10, 10, 20, 8, seed=4)
+    return recipe_config(int(cfg[1:]))
+
+
+def _pair(prob, env=None):
+    env = env or {}
+    fused = _with_env(env, lambda: core.Cache(prob))
+    tiers = _with_env({**env, "RAOCP_DYN_FUSE": "0"}, lambda: core.Cache(prob))
+    return fused, tiers
+
+
+@pytest.mark.parametrize("env", [{}, {"RAOCP_DYN_FOLD": "1"}, {"RAOCP_FUSE_PREFETCH": "0"}],
+                         ids=["default", "fold", "one_region"])
+@pytest.mark.parametrize("cfg", ["c2", "quad", "bin10"])
+def test_fused_projection_matches_tiers_and_oracle(cfg, env):
+    """fold: one-phase backward levels (per-pair WT tables) in the fused sweep and in the
+    tiers; one_region: no prefetching (the tiers above share the deepest tier's region)."""
+    from oracle.raocp_oracle import OracleProblem
+    r = _recipe(cfg)
+    tree, prob = build_problem(r)
+    fused, tiers = _pair(prob, env)
+    if not fused.native.kernel_info(9).startswith("k_dyn_fuse"):
+        pytest.skip("fused sweep not planned for this tree: " + fused.native.kernel_info(9))
+    assert "k_dyn_fuse" not in tiers.native.kernel_info(9)
+    zz = np.random.default_rng(5).standard_normal(fused.primal_size)
+    out = []
+    for cache in (fused, tiers):
+        cache.cache_initial_state(r["x0"])
+        cache.native.set_primal(zz)
+        cache.native.project_on_dynamics()
+        out.append(cache.native.get_primal())
+    assert rel_err(out[0], out[1]) <= 1e-13
+    assert rel_err(out[0], OracleProblem(prob).project_on_dynamics(zz, r["x0"])) <= 1e-12
+
+
+def test_fused_cp_loop_bit_identical_to_tiers():
+    """30 CP iterations (one full 24-iteration graph batch plus a remainder), tol = 0."""
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    fused, tiers = _pair(prob)
+    assert fused.native.kernel_info(9).startswith("k_dyn_fuse")
+    alpha = 0.999 / fused.native.step_size()
+    out = []
+    for cache in (fused, tiers):
+        st, err, derr = cache.native.cp_run(r["x0"], 30, 0.0, alpha)
+        out.append((st, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
+    (s1, e1, d1, z1, y1), (s2, e2, d2, z2, y2) = out
+    assert s1 == s2 == 1 and e1.shape == e2.shape == (31, 3)
+    assert trace_rel_err(e1, e2) <= 1e-10 and trace_rel_err(d1, d2) <= 1e-10
+    assert rel_err(z1, z2) <= 1e-11 and rel_err(y1, y2) <= 1e-11
+    st_o, err_o, _, z_o, _, _ = OracleProblem(prob).chock(r["x0"], 30, 0.0, alpha=alpha)
+    assert trace_rel_err(out[0][1], err_o) <= 1e-8 and rel_err(out[0][3], z_o) <= 1e-10
+
+
+def test_fused_many_launches_then_projection():
+    """1,000 back-to-back launches (graph-replayed, as in the CP loop): the tickets are reset
+    and the epoch advances inside the kernel; a projection afterwards is still exact."""
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    fused = core.Cache(prob)
+    assert fused.native.kernel_info(9).startswith("k_dyn_fuse")
+    zz = np.random.default_rng(9).standard_normal(fused.primal_size)
+    out = []
+    for rep in range(2):  # (op_bench initialises the CP control block with x0 = 0)
+        fused.cache_initial_state(r["x0"])
+        fused.native.set_primal(zz)
+        fused.native.project_on_dynamics()
+        out.append(fused.native.get_primal())
+        fused.native.op_bench(9, 1000)
+    assert np.array_equal(out[0], out[1])
