@@ -114,6 +114,8 @@ struct raocp_ctx {
     raocp::FuseArg fuse{};       // its plan (tickets / flags in fuse_sync)
     size_t lds_fuse = 0;
     bool fuse_st = false;        // its static three-array LDS layout (raocp::FuseStat)
+    bool dyn_split = false;      // the tiered sweep in TWO launches (k_dyn_up / k_dyn_down)
+    size_t lds_up = 0, lds_down = 0;
     unsigned* fuse_sync = nullptr;  // [epoch | error word | per tier: tickets, flags]
     double* x0 = nullptr;
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
@@ -567,6 +569,22 @@ struct DynOp {
             return ta;
         };
         auto tier_blocks = [&](int k) { return sharded ? c->tier_own[k].second : c->tiers[k].nsub; };
+        if (s > 0 && c->dyn_split && !sharded && part == 0) {
+            // the tiered sweep in two launches (raocp_dynf.hip): one workgroup per subtree of
+            // every tier plus the top; k_dyn_up runs the deferred stopping test in block 0
+            raocp::FuseArg fa = c->fuse;
+            if (ck) fa.ck = *ck;
+            int nsub = 0;
+            for (const auto& tp : c->tiers) nsub += tp.nsub;
+            auto ku = raocp::k_dyn_up<NX, NU>;
+            auto kd = c->f_lds_top ? raocp::k_dyn_down<NX, NU, true> : raocp::k_dyn_down<NX, NU, false>;
+            allow_lds(ku, c->lds_up);
+            allow_lds(kd, c->lds_down);
+            ku<<<nsub + 1 + (fa.ck.on ? 1 : 0), raocp::kFuseBlock, c->lds_up, c->stream>>>(dev_for(), bf, ctl, zsel, c->q,
+                                                                                           c->d, fa);
+            kd<<<nsub + 1, raocp::kFuseBlock, c->lds_down, c->stream>>>(dev_for(), bf, ctl, zsel, c->d, c->x0, fa);
+            return;
+        }
         if (s > 0 && c->dyn_fuse && !sharded && part == 0) {
             // the whole tiered sweep in one launch (raocp_dynf.hip), one workgroup per subtree
             // of the deepest tier; it runs the deferred stopping test itself
@@ -665,11 +683,11 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
 // the fused sweep's error word (a hand-off wait timed out, raocp_dynf.hip): checked after
 // every synchronised run that may have launched it; the context is unusable afterwards
 int fuse_err(raocp_ctx* c) {
-    if (!c->dyn_fuse || !c->fuse_sync) return RAOCP_OK;
+    if (!(c->dyn_fuse || c->dyn_split) || !c->fuse_sync) return RAOCP_OK;
     int e = 0;
     HIPCHK(hipMemcpy(&e, c->fuse_sync + 1, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dyn_fuse); RAOCP_DYN_FUSE=0 "
-                                        "selects the tier launches");
+    if (e) return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dyn_up / k_dyn_down / k_dyn_fuse); "
+                                        "RAOCP_DYN_SPLIT=0 selects the tier launches");
     return RAOCP_OK;
 }
 
@@ -1068,6 +1086,8 @@ std::string kernel_name(const raocp_ctx* c, int op) {
                 for (int t = 0; t < c->N; ++t) add("k_dy3_fwd<" + T + ", " + nn + ">");
             } else if (c->dyn2) {
                 return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
+            } else if (c->cut > 0 && c->dyn_split && c->sh_S == 0) {
+                return "k_dyn_up<" + nn + "> x1 + k_dyn_down<" + nn + ", " + b(c->f_lds_top) + "> x1";
             } else if (c->cut > 0 && c->dyn_fuse && c->sh_S == 0) {
                 return "k_dyn_fuse<" + nn + ", true, " + b(c->fuse_st) + "> x1";
             } else if (c->cut > 0) {
@@ -1891,7 +1911,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         auto level_cost = [&](double P, double C) { return 3.0 + (C * R + P * R + P * nu + C * nx) / 384.0; };
         auto recs = [](size_t cnt) { return 2 * cnt; };  // 16-B records in doubles
         // fold: one-phase backward levels (per-pair WT tables instead of per-kind W, no P rows)
-        bool fold_ok = false;  // measured slower at config 2: opt-in RAOCP_DYN_FOLD=1
+        // the default: config 2's split sweep 47.1 vs 49.5 us, the tier launches 51.4 vs 51.5 us
+        // (profiles/r03_v5/dyn_time.log); RAOCP_DYN_FOLD=0 keeps the two-phase levels
+        bool fold_ok = true;
         if (const char* env = getenv("RAOCP_DYN_FOLD")) fold_ok = atoi(env) != 0;
         auto top_bytes = [&](int s_, int& maxch, bool fl, bool fold) {
             const size_t T = c->stage_ptr[s_], nb = stage_n(s_);
@@ -2070,7 +2092,16 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         {
             c->dyn_fuse = false;
             bool fz = c->cut > 0 && !c->tiers.empty() && c->tiers.size() <= (size_t)raocp::kFuseTiers && c->f_lds_top;
-            if (const char* e = getenv("RAOCP_DYN_FUSE")) fz = fz && atoi(e) != 0;
+            // The same plan serves the split sweep (k_dyn_up / k_dyn_down, two launches, the
+            // default where it applies; RAOCP_DYN_SPLIT=0 keeps the tier launches) and the
+            // fused one (opt-in RAOCP_DYN_FUSE=1: measured 49-56 us per projection at config 2
+            // against the tier launches' 51.5).
+            const char* fe = getenv("RAOCP_DYN_FUSE");
+            const bool want_fuse = fe && atoi(fe) != 0;
+            bool split = true;
+            if (const char* e = getenv("RAOCP_DYN_SPLIT")) split = atoi(e) != 0;
+            c->dyn_split = false;
+            size_t up = 0, down = 0;  // the split sweep's LDS (doubles)
             raocp::FuseArg& fa = c->fuse;
             memset(&fa, 0, sizeof(fa));
             // doubles: XD rows | S1 (the deepest tier) | S2 (the tiers above, the top)
@@ -2114,7 +2145,20 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 const size_t fwd = (c1 - c0) * KM1 + npl * F1 + recs(nnl + nall - 1);
                 size_t& reg = k + 1 == c->tiers.size() ? s1 : s2;
                 reg = std::max(reg, std::max(back, fwd));
+                up = std::max(up, back);
+                down = std::max(down, (size_t)raocp::rup((int)(nnl * KF), 2) + fwd);
             }
+            if (fz) {  // the top's backward (k_dyn_up) and forward (k_dyn_down) layouts
+                const size_t T = c->stage_ptr[c->cut], nb = stage_n(c->cut);
+                const int c1 = cp[c->cut], p1 = pp[c1];
+                up = std::max(up, (c->fold_top ? (size_t)p1 * W1 : c->nkind * W1) + c1 * RG1 + T * KP + nb * KP + T * NUP +
+                                      T * KF + (c->fold_top ? 0 : raocp::rup(c->maxch_top * PS, 2)) + recs(T + T + nb - 1));
+                down = std::max(down, c1 * KM1 + (c->f_lds_top ? (size_t)p1 * F1 : 0) + T * KF + recs(T + T + nb - 1));
+                c->lds_up = 8 * up;
+                c->lds_down = 8 * down;
+                split = split && c->lds_up <= kLds && c->lds_down <= kLds;
+            }
+            const bool elig = fz;
             if (fz) {
                 fa.K = (int)c->tiers.size();
                 fa.nXD = (int)xd;
@@ -2136,6 +2180,10 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                     fz = true;
                 }
             }
+            if (elig && !want_fuse) {  // the split sweep (or the tier launches)
+                c->dyn_split = split;
+                fz = false;
+            }
             if (fz) {
                 int per_cu = 0;
                 dispatch(nx, nu, FuseOcc{}, c, &per_cu);
@@ -2144,7 +2192,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                     fprintf(stderr, "[raocp] fused sweep: %d tiers, LDS %zu B (%s), %d workgroups, %d per CU x %d CUs%s\n",
                             fa.K, c->lds_fuse, c->fuse_st ? "static" : (fa.oS2 != fa.oS1 ? "two regions" : "one region"), c->tiers.back().nsub, per_cu, n_cus, fz ? "" : " (not co-resident: tier launches)");
             }
-            if (fz) {
+            if (fz || c->dyn_split) {
                 size_t words = 2;
                 for (int k = 0; k < fa.K; ++k) words += 2 * (size_t)fa.t[k].ngroups;
                 if ((rc = c->alloc(&c->fuse_sync, words))) return bail(rc);
@@ -2170,6 +2218,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 fa.timeout = ms * 100000LL;  // 100 MHz ticks
             }
             c->dyn_fuse = fz;
+            if (getenv("RAOCP_DYN_VERBOSE") && c->dyn_split)
+                fprintf(stderr, "[raocp] split sweep: %d tiers, LDS %zu / %zu B\n", fa.K, c->lds_up, c->lds_down);
         }
         if (getenv("RAOCP_DYN_VERBOSE")) {
             fprintf(stderr, "[raocp] dynamics plan: top stages [0,%d) lds %zu F%s%s", c->cut, c->lds_top,

@@ -191,9 +191,11 @@ __device__ void fz_back_wait(const Dev& p, const double* qbuf_, const FuseTier& 
     fz_stamp(p, pl);
 }
 
+// d_i goes to the tier's XD rows in LDS (XD; the fused sweep's forward reads them there) or,
+// with dglob, to global rows (the split sweep's forward is the next launch)
 template <int NXc, int NUc>
-__device__ void fz_back_levels(const Dev& p, double* qbuf_, const FuseTier& tt, int sub, bool leaves, ldsd* smem,
-                               ldsd* scr, Prologue& pl) {
+__device__ void fz_back_levels(const Dev& p, double* qbuf_, const FuseTier& tt, int sub, bool leaves, ldsd* XD,
+                               ldsd* scr, Prologue& pl, glbd* dglob = nullptr) {
     const Geo<NXc, NUc> g(p);
     const int tid = threadIdx.x, nthr = blockDim.x;
     const TierArg& ta = tt.ta;
@@ -202,7 +204,7 @@ __device__ void fz_back_levels(const Dev& p, double* qbuf_, const FuseTier& tt, 
     const ldsrec* NL = (const ldsrec*)ly.NL;
     const ldsrec* CH = (const ldsrec*)ly.CH;
     const TabsT<const ldsd*, const ldsd*> tb{ly.W, ly.RG, nullptr, nullptr, tt.c0, tt.fold ? tt.p0 : 0};
-    ldsd* XD = smem + tt.oXD;
+    const GRows dg{dglob, 0, g.nu};
     for (int l = L - 1; l >= 0; --l) {
         const InfoT<const ldsrec*> inf{NL + pl.off[l], pl.lo[l], CH + pl.off[l + 1] - 1, pl.lo[l + 1]};
         const LRows xq_l{ly.XQ + (size_t)pl.off[l] * g.KP, pl.lo[l], g.KP};
@@ -211,14 +213,16 @@ __device__ void fz_back_levels(const Dev& p, double* qbuf_, const FuseTier& tt, 
         const LRows dl{XD + (size_t)pl.off[l] * g.KF + g.nx, pl.lo[l], g.KF};  // d_i into XD row i, cols nx..
         const double sign = (l + 1 == L && leaves) ? -1.0 : 1.0;
         if (tt.fold) {
-            back_fold<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], xq_c, sign, xq_l, ur, xq_l, dl, tid, nthr);
+            if (dglob) back_fold<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], xq_c, sign, xq_l, ur, xq_l, dg, tid, nthr);
+            else back_fold<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], xq_c, sign, xq_l, ur, xq_l, dl, tid, nthr);
             lds_sync();
             continue;
         }
         const LRows pr{ly.PB, pl.lo[l + 1], g.PS};
         back_phase_a<NXc, NUc>(p, tb, inf, pl.lo[l + 1], pl.hi[l + 1], xq_c, sign, pr, tid, nthr);
         lds_sync();
-        back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, xq_l, dl, tid, nthr);
+        if (dglob) back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, xq_l, dg, tid, nthr);
+        else back_phase_b<NXc, NUc>(p, tb, inf, pl.lo[l], pl.hi[l], pr, xq_l, ur, xq_l, dl, tid, nthr);
         lds_sync();
     }
     // the root's q row (XQ row 0, zero tail) for the tier above
@@ -271,7 +275,7 @@ __device__ void fz_fwd_stage(const Dev& p, const FuseTier& tt, int sub, ldsd* sc
 }
 
 template <int NXc, int NUc>
-__device__ void fz_fwd_run(const Dev& p, glbd* z, const FuseTier& tt, int sub, bool sc, ldsd* smem, ldsd* scr,
+__device__ void fz_fwd_run(const Dev& p, glbd* z, const FuseTier& tt, int sub, bool sc, ldsd* XD, ldsd* scr,
                            Prologue& pl) {
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
@@ -279,7 +283,6 @@ __device__ void fz_fwd_run(const Dev& p, glbd* z, const FuseTier& tt, int sub, b
     const TierArg& ta = tt.ta;
     const int L = tt.s1 - tt.s0;
     const FwdLds<NXc, NUc> ly(p, tt, scr);
-    ldsd* XD = smem + tt.oXD;
     const int root = fz_lo(ta, 0, sub);
     fz_levels(pl, ta, L, sub);
     if (tid < g.nx) XD[tid] = ld_sc1((const double*)z + p.X0 + (size_t)root * g.nx + tid);
@@ -313,41 +316,75 @@ __device__ void fz_fwd_run(const Dev& p, glbd* z, const FuseTier& tt, int sub, b
 // the top (stages [0, s), nodes [0, T)), backward then forward, as k_dyn_top: the boundary
 // q rows come from tier t[0]'s roots (ld_sc1), the boundary x rows are published
 // [W | RG | KM | F (FL) | XQ (T, KP) | QB (nb, KP) | U (T, NUP) | XD (T, KF) | P | NL | CH]
+// The top's layout: [W | RG | KM | F (FL) | XQ (T, KP) | QB (nb, KP) | U (T, NUP) | XD (T, KF) | P | NL | CH];
+// bwd (split sweep): backward only (no KM / F), d_i of the top's nodes also stored to
+// global rows for the next launch's forward sweep
 template <int NXc, int NUc, bool FL>
-__device__ void fz_top(const Dev& p, glbd* z, const double* qbuf_, const double* x0_, const FuseArg& fa, ldsd* scr,
-                       Prologue& pl) {
+struct TopLds {
+    int oW, oRG, oKM, oF, oXQ, oQB, oU, oXD, oP, oNL, oCH;
+    __device__ __forceinline__ TopLds(const Dev& p, const FuseArg& fa, bool bwd) {
+        const Geo<NXc, NUc> g(p);
+        const TabSize<NXc, NUc> ts(g);
+        const int T = fa.T, nb = fa.nb, c1 = fa.c1, p1 = fa.p1;
+        const bool fold = fa.fold_top;
+        oW = 0;
+        oRG = oW + (fold ? p1 : p.nkind) * ts.W1;
+        oKM = oRG + c1 * ts.RG1;
+        oF = oKM + (bwd ? 0 : c1 * ts.KM1);
+        oXQ = oF + (FL && !bwd ? p1 * ts.F1 : 0);
+        oQB = oXQ + T * g.KP;
+        oU = oQB + nb * g.KP;
+        oXD = oU + T * g.NUP;
+        oP = oXD + T * g.KF;
+        oNL = oP + (fold ? 0 : rup(fa.maxch_top * g.PS, 2));
+        oCH = oNL + 2 * T;
+    }
+};
+
+// everything but the boundary q rows (issued before a wait for them)
+template <int NXc, int NUc, bool FL>
+__device__ void fz_top_stage(const Dev& p, const glbd* z, const FuseArg& fa, ldsd* scr, Prologue& pl, bool bwd) {
     const Geo<NXc, NUc> g(p);
     const TabSize<NXc, NUc> ts(g);
     const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
     const int tid = threadIdx.x, nthr = blockDim.x;
     const int s = fa.s, T = fa.T, nb = fa.nb, c1 = fa.c1, p1 = fa.p1;
     const bool fold = fa.fold_top;
-    const int nW = (fold ? p1 : p.nkind) * ts.W1;
-    const int oW = 0, oRG = oW + nW, oKM = oRG + c1 * ts.RG1, oF = oKM + c1 * ts.KM1;
-    const int oXQ = oF + (FL ? p1 * ts.F1 : 0), oQB = oXQ + T * g.KP, oU = oQB + nb * g.KP, oXD = oU + T * g.NUP;
-    const int oP = oXD + T * g.KF, oNL = oP + (fold ? 0 : rup(fa.maxch_top * g.PS, 2)), oCH = oNL + 2 * T;
+    const TopLds<NXc, NUc, FL> o(p, fa, bwd);
     int rot = p.dyn_rot ? 0 : -1;
-    dma_r(scr + oW, fold ? p.dWT : p.dW, nW, rot);
-    dma_r(scr + oRG, p.dRG, c1 * ts.RG1, rot);
-    dma_r(scr + oKM, p.dKM, c1 * ts.KM1, rot);
-    if (FL) dma_r(scr + oF, p.dF, p1 * ts.F1, rot);
-    dma_r(scr + oNL, (const double*)p.ninfo, 2 * T, rot);
-    dma_r(scr + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1), rot);
+    dma_r(scr + o.oW, fold ? p.dWT : p.dW, (fold ? p1 : p.nkind) * ts.W1, rot);
+    dma_r(scr + o.oRG, p.dRG, c1 * ts.RG1, rot);
+    if (!bwd) dma_r(scr + o.oKM, p.dKM, c1 * ts.KM1, rot);
+    if (FL && !bwd) dma_r(scr + o.oF, p.dF, p1 * ts.F1, rot);
+    dma_r(scr + o.oNL, (const double*)p.ninfo, 2 * T, rot);
+    dma_r(scr + o.oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1), rot);
     if (tid <= s + 1) pl.sp[tid] = p.stage_ptr[tid];
-    rows_in_r(dmaok, scr + oXQ, g.KP, (const double*)z + p.X0, g.nx, g.nx, T, p.zpage, tid, nthr, rot);
-    rows_in_r(dmaok, scr + oU, g.NUP, (const double*)z + p.U0, g.nu, g.nu, T, p.zpage, tid, nthr, rot);
-    zero_fill(scr + oXD, T * g.KF, tid, nthr);
-    if (!fold) zero_fill(scr + oP, fa.maxch_top * g.PS, tid, nthr);
-    // the boundary q rows last: their wait covers the copies above
-    for (int e = tid; e < nb * g.KP; e += nthr) scr[oQB + e] = ld_sc1(qbuf_ + (size_t)T * g.KP + e);
+    rows_in_r(dmaok, scr + o.oXQ, g.KP, (const double*)z + p.X0, g.nx, g.nx, T, p.zpage, tid, nthr, rot);
+    rows_in_r(dmaok, scr + o.oU, g.NUP, (const double*)z + p.U0, g.nu, g.nu, T, p.zpage, tid, nthr, rot);
+}
+
+template <int NXc, int NUc, bool FL>
+__device__ void fz_top_run(const Dev& p, glbd* z, const double* qbuf_, const double* x0_, const FuseArg& fa, ldsd* scr,
+                           Prologue& pl, glbd* dglob) {
+    const Geo<NXc, NUc> g(p);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int s = fa.s, T = fa.T, nb = fa.nb;
+    const bool fold = fa.fold_top;
+    const bool bwd = dglob != nullptr;
+    const TopLds<NXc, NUc, FL> o(p, fa, bwd);
+    zero_fill(scr + o.oXD, T * g.KF, tid, nthr);
+    if (!fold) zero_fill(scr + o.oP, fa.maxch_top * g.PS, tid, nthr);
+    // the boundary q rows last: their wait covers the copies still in flight
+    for (int e = tid; e < nb * g.KP; e += nthr) scr[o.oQB + e] = ld_sc1(qbuf_ + (size_t)T * g.KP + e);
     dma_wait();
     lds_sync();
     fz_stamp(p, pl);
     typedef typename std::conditional<FL, const ldsd*, const glbd*>::type PF;
-    const TabsT<const ldsd*, PF> tb{scr + oW, scr + oRG, scr + oKM, FL ? (PF)(scr + oF) : (PF)((const glbd*)p.dF), 0, 0};
-    const InfoT<const ldsrec*> inf{(const ldsrec*)(scr + oNL), 0, (const ldsrec*)(scr + oCH), 1};
-    ldsd* XD = scr + oXD;
-    const LRows xq{scr + oXQ, 0, g.KP}, qb{scr + oQB, T, g.KP}, ur{scr + oU, 0, g.NUP}, xd{XD, 0, g.KF};
+    const TabsT<const ldsd*, PF> tb{scr + o.oW, scr + o.oRG, scr + o.oKM,
+                                    FL ? (PF)(scr + o.oF) : (PF)((const glbd*)p.dF), 0, 0};
+    const InfoT<const ldsrec*> inf{(const ldsrec*)(scr + o.oNL), 0, (const ldsrec*)(scr + o.oCH), 1};
+    ldsd* XD = scr + o.oXD;
+    const LRows xq{scr + o.oXQ, 0, g.KP}, qb{scr + o.oQB, T, g.KP}, ur{scr + o.oU, 0, g.NUP}, xd{XD, 0, g.KF};
     const LRows dlds{XD + g.nx, 0, g.KF};
     for (int t = s - 1; t >= 0; --t) {
         const int b = pl.sp[t], e = pl.sp[t + 1];
@@ -358,7 +395,7 @@ __device__ void fz_top(const Dev& p, glbd* z, const double* qbuf_, const double*
             lds_sync();
             continue;
         }
-        const LRows pr{scr + oP, cb, g.PS};
+        const LRows pr{scr + o.oP, cb, g.PS};
         if (t + 1 < s) back_phase_a<NXc, NUc>(p, tb, inf, cb, ce, xq, 1.0, pr, tid, nthr);
         else back_phase_a<NXc, NUc>(p, tb, inf, cb, ce, qb, 1.0, pr, tid, nthr);
         lds_sync();
@@ -366,6 +403,13 @@ __device__ void fz_top(const Dev& p, glbd* z, const double* qbuf_, const double*
         lds_sync();
     }
     fz_stamp(p, pl);
+    if (bwd) {  // d of the top's nodes for the next launch's forward sweep
+        for (int e = tid; e < T * g.nu; e += nthr) {
+            const int i = e / g.nu, c = e - i * g.nu;
+            dglob[(size_t)i * g.nu + c] = XD[(size_t)i * g.KF + g.nx + c];
+        }
+        return;
+    }
     if (tid < g.nx) {
         const double v = ((const glbd*)x0_)[tid];
         XD[tid] = v;
@@ -378,6 +422,15 @@ __device__ void fz_top(const Dev& p, glbd* z, const double* qbuf_, const double*
         else fwd_phase<NXc, NUc, false, true>(p, tb, inf, b, e, xd, z, xd, tid, nthr);
         lds_sync();
     }
+}
+
+// the top (stages [0, s), nodes [0, T)), backward then forward, as k_dyn_top: the boundary
+// q rows come from tier t[0]'s roots (ld_sc1), the boundary x rows are published
+template <int NXc, int NUc, bool FL>
+__device__ void fz_top(const Dev& p, glbd* z, const double* qbuf_, const double* x0_, const FuseArg& fa, ldsd* scr,
+                       Prologue& pl) {
+    fz_top_stage<NXc, NUc, FL>(p, z, fa, scr, pl, false);
+    fz_top_run<NXc, NUc, FL>(p, z, qbuf_, x0_, fa, scr, pl, nullptr);
 }
 
 // stores of this workgroup drained, then one lane publishes
@@ -438,12 +491,12 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_fuse(Dev p, Bufs bf, const C
         if (work && k == D) {
             fz_back_wait<NXc, NUc>(p, qbuf_, tt, sub, true, S1, pl);
             if (pre2) fz_back_stage<NXc, NUc>(p, z, fa.t[D - 1], sub_at(D - 1), false, S2);
-            fz_back_levels<NXc, NUc>(p, qbuf_, tt, sub, true, XB, S1, pl);
+            fz_back_levels<NXc, NUc>(p, qbuf_, tt, sub, true, XB + tt.oXD, S1, pl);
         } else if (work) {
             if (!(k == D - 1 && pre2)) fz_back_stage<NXc, NUc>(p, z, tt, sub, false, S2);
             fz_back_wait<NXc, NUc>(p, qbuf_, tt, sub, false, S2, pl);
             if (k == D - 1 && two) fz_fwd_stage<NXc, NUc>(p, fa.t[D], sub_at(D), S1);
-            fz_back_levels<NXc, NUc>(p, qbuf_, tt, sub, false, XB, S2, pl);
+            fz_back_levels<NXc, NUc>(p, qbuf_, tt, sub, false, XB + tt.oXD, S2, pl);
         }
         fz_stamp(p, pl);
         fz_drain();
@@ -515,10 +568,10 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_fuse(Dev p, Bufs bf, const C
             const bool staged = (k == kw && (!top || fa.K > 1 || !two)) || (deepest && two);
             if (deepest) {
                 if (!staged) fz_fwd_stage<NXc, NUc>(p, tt, sk, S1);
-                fz_fwd_run<NXc, NUc>(p, z, tt, sk, false, XB, S1, pl);
+                fz_fwd_run<NXc, NUc>(p, z, tt, sk, false, XB + tt.oXD, S1, pl);
             } else {
                 if (!staged) fz_fwd_stage<NXc, NUc>(p, tt, sk, S2);
-                fz_fwd_run<NXc, NUc>(p, z, tt, sk, true, XB, S2, pl);
+                fz_fwd_run<NXc, NUc>(p, z, tt, sk, true, XB + tt.oXD, S2, pl);
             }
         }
         fz_stamp(p, pl);
@@ -531,4 +584,209 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_fuse(Dev p, Bufs bf, const C
     // waiting one, unless it ran the top) to 64..127
     if (p.stamps && tid == 0 && (top || blockIdx.x == 0))
         for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(top ? 0 : 64) + q] = pl.ts[q];
+}
+
+// ==============================================================================
+// The split sweep (default where the fused plan applies): the same tiers in TWO launches,
+// one workgroup per subtree of every tier plus the top, each with ONE role fixed by its
+// block index, so every workgroup stages its tables and vectors at its start and only the
+// dependent rows (the children's q, the parent's x) wait for a hand-off:
+//   k_dyn_up:   [deferred stopping test] [deepest subtrees] [tier D-1] .. [tier 0] [top]
+//               a tier-k workgroup waits until its r children subtrees have published
+//               their q rows (a counter of arrivals), sweeps backward, publishes its
+//               root's q row and arrives at its parent's counter; the top sweeps backward
+//               and bumps the epoch. d_i goes to global rows.
+//   k_dyn_down: [top] [tier 0] .. [deepest]: the top sweeps forward and releases tier 0;
+//               a tier-k workgroup waits for its parent's flag (the launch's epoch),
+//               sweeps forward, publishes its boundary x rows and releases its children.
+// A workgroup waits only for workgroups with lower block indices in k_dyn_down and higher
+// ones' producers ... precisely: in k_dyn_up for the deepest tiers' (lower indices), in
+// k_dyn_down for its parents' (lower indices), which are dispatched first and never wait
+// for it, so no co-residency is needed. Counters are reset by their one consumer after its
+// wait; flags carry the epoch, which k_dyn_up's top advances once per projection.
+
+// spin (one lane) until *f == v, bounded; false on a timeout (error word set)
+__device__ __forceinline__ bool fz_wait_eq(const unsigned* f, unsigned v, const FuseArg& fa, int& ok) {
+    if (threadIdx.x == 0) {
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        while (ld_u32_sc1(f) != v) {
+            if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > fa.timeout) {
+                ok = 0;
+                __hip_atomic_store(fa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
+template <int NXc, int NUc>
+__global__ void __launch_bounds__(kFuseBlock) k_dyn_up(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                       double* qbuf_, double* dbuf_, FuseArg fa) {
+    extern __shared__ __attribute__((aligned(16))) double smem_[];
+    __shared__ Prologue pl;
+    __shared__ int s_ok;
+    const int tid = threadIdx.x;
+    if (fa.ck.on && blockIdx.x == 0) {  // the previous CP iteration's stopping test
+        if (tid < 64) cp_check_wave(fa.ck);
+        return;
+    }
+    ldsd* smem = (ldsd*)smem_;
+    glbd* z = dyn_z(bf, zsel, ctl);
+    if (tid == 0) {
+        pl.nts = 0;
+        s_ok = 1;
+    }
+    fz_stamp(p, pl);
+    const int D = fa.K - 1;
+    int b = (int)blockIdx.x - (fa.ck.on ? 1 : 0), k = D;
+    for (; k >= 0 && b >= fa.t[k].ngroups * fa.t[k].r; --k) b -= fa.t[k].ngroups * fa.t[k].r;
+    if (k >= 0) {  // subtree b of tier k
+        const FuseTier& tt = fa.t[k];
+        fz_back_stage<NXc, NUc>(p, z, tt, b, k == D, smem);
+        const bool work = !ctl_done(ctl);
+        if (k < D && !fz_wait_eq(fa.t[k + 1].cnt + b, (unsigned)fa.t[k + 1].r, fa, s_ok)) return;
+        if (k < D && tid == 0) st_u32_sc1(fa.t[k + 1].cnt + b, 0u);
+        fz_stamp(p, pl);
+        if (work) {
+            fz_back_wait<NXc, NUc>(p, qbuf_, tt, b, k == D, smem, pl);
+            fz_back_levels<NXc, NUc>(p, qbuf_, tt, b, k == D, nullptr, smem, pl, (glbd*)dbuf_);
+        }
+        fz_stamp(p, pl);
+        fz_drain();
+        if (tid == 0) __hip_atomic_fetch_add(tt.cnt + b / tt.r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fz_stamp(p, pl);
+        if (p.stamps && tid == 0 && b == 0 && (k == 0 || k == D))  // diagnostics: tier 0 / deepest, subtree 0
+            for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
+    } else {  // the top
+        fz_top_stage<NXc, NUc, false>(p, z, fa, smem, pl, true);
+        const unsigned e = ld_u32_sc1(fa.epoch);
+        const bool work = !ctl_done(ctl);
+        if (!fz_wait_eq(fa.t[0].cnt, (unsigned)fa.t[0].r, fa, s_ok)) return;
+        if (tid == 0) st_u32_sc1(fa.t[0].cnt, 0u);
+        fz_stamp(p, pl);
+        if (work) fz_top_run<NXc, NUc, false>(p, z, qbuf_, nullptr, fa, smem, pl, (glbd*)dbuf_);
+        fz_stamp(p, pl);
+        fz_drain();
+        if (tid == 0) st_u32_sc1(fa.epoch, e + 1u);
+        if (p.stamps && tid == 0)
+            for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[q] = pl.ts[q];
+    }
+}
+
+// the top's forward sweep (k_dyn_down's block 0):
+// [KM (0..c1) | F (pairs 0..p1, FL) | XD (T, KF) = [x | d | 0] | NL (T) | CH (T + nb - 1)]
+template <int NXc, int NUc, bool FL>
+__device__ void fz_top_fwd(const Dev& p, glbd* z, const double* dbuf_, const double* x0_, const FuseArg& fa,
+                           ldsd* scr, Prologue& pl) {
+    const Geo<NXc, NUc> g(p);
+    const TabSize<NXc, NUc> ts(g);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int s = fa.s, T = fa.T, nb = fa.nb, c1 = fa.c1, p1 = fa.p1;
+    const int oKM = 0, oF = oKM + c1 * ts.KM1, oXD = oF + (FL ? p1 * ts.F1 : 0), oNL = oXD + T * g.KF, oCH = oNL + 2 * T;
+    int rot = p.dyn_rot ? 0 : -1;
+    dma_r(scr + oKM, p.dKM, c1 * ts.KM1, rot);
+    if (FL) dma_r(scr + oF, p.dF, p1 * ts.F1, rot);
+    dma_r(scr + oNL, (const double*)p.ninfo, 2 * T, rot);
+    dma_r(scr + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1), rot);
+    if (tid <= s + 1) pl.sp[tid] = p.stage_ptr[tid];
+    for (int e = tid; e < T * g.KF; e += nthr) {  // [x0 (row 0) or 0 | d | 0]
+        const int i = e / g.KF, c = e - i * g.KF;
+        double v = 0.0;
+        if (c < g.nx) v = i == 0 ? ((const glbd*)x0_)[c] : 0.0;
+        else if (c < g.nx + g.nu) v = ((const glbd*)dbuf_)[(size_t)i * g.nu + c - g.nx];
+        scr[oXD + e] = v;
+    }
+    if (tid < g.nx) z[p.X0 + tid] = ((const glbd*)x0_)[tid];  // x_0 = x0bar (cache.py:282)
+    dma_wait();
+    lds_sync();
+    typedef typename std::conditional<FL, const ldsd*, const glbd*>::type PF;
+    const TabsT<const ldsd*, PF> tb{nullptr, nullptr, scr + oKM, FL ? (PF)(scr + oF) : (PF)((const glbd*)p.dF), 0, 0};
+    const InfoT<const ldsrec*> inf{(const ldsrec*)(scr + oNL), 0, (const ldsrec*)(scr + oCH), 1};
+    const LRows xd{scr + oXD, 0, g.KF};
+    for (int t = 0; t < s; ++t) {
+        const int b = pl.sp[t], e = pl.sp[t + 1];
+        if (t + 1 < s) fwd_phase<NXc, NUc, true>(p, tb, inf, b, e, xd, z, xd, tid, nthr);
+        else fwd_phase<NXc, NUc, false, true>(p, tb, inf, b, e, xd, z, xd, tid, nthr);
+        lds_sync();
+    }
+}
+
+// a tier's XD rows for the forward sweep: [0 | d (global rows) | 0]; the root's x arrives later
+template <int NXc, int NUc>
+__device__ void fz_xd_stage(const Dev& p, const double* dbuf_, const FuseTier& tt, int sub, ldsd* XD) {
+    const Geo<NXc, NUc> g(p);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    const int L = tt.s1 - tt.s0;
+    const bool dmaok = (g.nx % 2 == 0) && (g.nu % 2 == 0);
+    const double* zp = p.zpage;
+    for (int l = 0, off = 0; l < L; ++l) {
+        const int lo = fz_lo(tt.ta, l, sub), cnt = tt.ta.cnt[l];
+        ldsd* xd = XD + (size_t)off * g.KF;
+        const double* dl = dbuf_ + (size_t)lo * g.nu;
+        if (dmaok) {
+            const int cpr = g.KF >> 1, cx = g.nx >> 1, cd = (g.nx + g.nu) >> 1;
+            dma_gen(xd, cnt * cpr, [=](int ch) {
+                const int r = ch / cpr, c = ch - r * cpr;
+                return (c >= cx && c < cd) ? dl + (size_t)r * g.nu + 2 * (c - cx) : zp;
+            });
+        } else {
+            for (int e = tid; e < cnt * g.KF; e += nthr) {
+                const int r = e / g.KF, c = e - r * g.KF;
+                xd[e] = (c >= g.nx && c < g.nx + g.nu) ? ((const glbd*)dl)[(size_t)r * g.nu + c - g.nx] : 0.0;
+            }
+        }
+        off += cnt;
+    }
+}
+
+template <int NXc, int NUc, bool FL>
+__global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                         const double* dbuf_, const double* x0_, FuseArg fa) {
+    extern __shared__ __attribute__((aligned(16))) double smem_[];
+    __shared__ Prologue pl;
+    __shared__ int s_ok;
+    const int tid = threadIdx.x;
+    ldsd* smem = (ldsd*)smem_;
+    glbd* z = dyn_z(bf, zsel, ctl);
+    if (tid == 0) {
+        pl.nts = 0;
+        s_ok = 1;
+    }
+    fz_stamp(p, pl);
+    const int D = fa.K - 1;
+    if (blockIdx.x == 0) {  // the top
+        const unsigned tag = ld_u32_sc1(fa.epoch);
+        if (!ctl_done(ctl)) fz_top_fwd<NXc, NUc, FL>(p, z, dbuf_, x0_, fa, smem, pl);
+        fz_stamp(p, pl);
+        fz_drain();
+        if (tid == 0) st_u32_sc1(fa.t[0].flag, tag);
+        if (p.stamps && tid == 0)
+            for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[q] = pl.ts[q];
+        return;
+    }
+    int b = (int)blockIdx.x - 1, k = 0;
+    for (; k < D && b >= fa.t[k].ngroups * fa.t[k].r; ++k) b -= fa.t[k].ngroups * fa.t[k].r;
+    const FuseTier& tt = fa.t[k];
+    // [XD (nnl, KF) | KM | F | NL | CH]
+    ldsd* XD = smem;
+    ldsd* scr = smem + rup(tt.nnl * Geo<NXc, NUc>(p).KF, 2);
+    const bool work = !ctl_done(ctl);
+    if (work) {
+        fz_fwd_stage<NXc, NUc>(p, tt, b, scr);
+        fz_xd_stage<NXc, NUc>(p, dbuf_, tt, b, XD);
+    }
+    const unsigned tag = ld_u32_sc1(fa.epoch);
+    if (!fz_wait_eq(tt.flag + b / tt.r, tag, fa, s_ok)) return;
+    fz_stamp(p, pl);
+    if (work) fz_fwd_run<NXc, NUc>(p, z, tt, b, k < D, XD, scr, pl);
+    fz_stamp(p, pl);
+    if (k < D) {
+        fz_drain();
+        if (tid == 0) st_u32_sc1(fa.t[k + 1].flag + b, tag);
+    }
+    if (p.stamps && tid == 0 && b == 0)  // diagnostics: tier 0 / deepest, subtree 0
+        for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
 }

@@ -1,7 +1,10 @@
-"""GPU parity of the fused tiered dynamics sweep k_dyn_fuse (raocp_dynf.hip): the tiers of
-raocp_dyn.hip in one launch, one workgroup per deepest-tier subtree, tickets up the tiers
-and flags down (cache.py:259-288). The default of fp64 trees whose tier plan is regular
-and co-resident (config 2); RAOCP_DYN_FUSE=0 keeps the tier launches.
+"""GPU parity of the tiered dynamics sweep in fewer launches (raocp_dynf.hip; cache.py:259-288):
+- the split sweep k_dyn_up + k_dyn_down (the default of fp64 trees with a regular tier plan,
+  config 2): one workgroup per subtree of every tier plus the top, counters of arrivals up
+  the tiers, epoch flags down;
+- the fused sweep k_dyn_fuse (opt-in RAOCP_DYN_FUSE=1): one launch, one workgroup per
+  deepest-tier subtree, tickets up the tiers and flags down;
+against the tier launches (RAOCP_DYN_SPLIT=0).
 
 The fused sweep runs the tier kernels' level routines on the same operands (d_i stays in
 LDS instead of a global round trip); its top runs on 512 lanes where k_dyn_top has 1,024,
@@ -44,26 +47,35 @@ def _recipe(cfg):
     return recipe_config(int(cfg[1:]))
 
 
-def _pair(prob, env=None):
+FUSE = {"RAOCP_DYN_FUSE": "1"}
+SPLIT = {}
+TIERS = {"RAOCP_DYN_SPLIT": "0"}
+
+
+def _pair(prob, env=None, mode=FUSE):
     env = env or {}
-    fused = _with_env(env, lambda: core.Cache(prob))
-    tiers = _with_env({**env, "RAOCP_DYN_FUSE": "0"}, lambda: core.Cache(prob))
+    fused = _with_env({**env, **mode}, lambda: core.Cache(prob))
+    tiers = _with_env({**env, **TIERS}, lambda: core.Cache(prob))
     return fused, tiers
 
 
-@pytest.mark.parametrize("env", [{}, {"RAOCP_DYN_FOLD": "1"}, {"RAOCP_FUSE_PREFETCH": "0"}],
-                         ids=["default", "fold", "one_region"])
+@pytest.mark.parametrize("env", [{}, {"RAOCP_DYN_FOLD": "0"}, {"RAOCP_FUSE_PREFETCH": "0"}],
+                         ids=["default", "two_phase", "one_region"])
+@pytest.mark.parametrize("mode", ["split", "fused"])
 @pytest.mark.parametrize("cfg", ["c2", "quad", "bin10"])
-def test_fused_projection_matches_tiers_and_oracle(cfg, env):
-    """fold: one-phase backward levels (per-pair WT tables) in the fused sweep and in the
-    tiers; one_region: no prefetching (the tiers above share the deepest tier's region)."""
+def test_fused_projection_matches_tiers_and_oracle(cfg, mode, env):
+    """default: one-phase backward levels (per-pair WT tables) in the sweep and in the tiers;
+    two_phase: the two-phase levels (per-kind W, child products through LDS); one_region:
+    the fused sweep without prefetching (the tiers above share the deepest
+    tier's region)."""
     from oracle.raocp_oracle import OracleProblem
     r = _recipe(cfg)
     tree, prob = build_problem(r)
-    fused, tiers = _pair(prob, env)
-    if not fused.native.kernel_info(9).startswith("k_dyn_fuse"):
-        pytest.skip("fused sweep not planned for this tree: " + fused.native.kernel_info(9))
-    assert "k_dyn_fuse" not in tiers.native.kernel_info(9)
+    fused, tiers = _pair(prob, env, FUSE if mode == "fused" else SPLIT)
+    name = "k_dyn_fuse" if mode == "fused" else "k_dyn_up"
+    if not fused.native.kernel_info(9).startswith(name):
+        pytest.skip(f"{mode} sweep not planned for this tree: " + fused.native.kernel_info(9))
+    assert "k_dyn_fuse" not in tiers.native.kernel_info(9) and "k_dyn_up" not in tiers.native.kernel_info(9)
     zz = np.random.default_rng(5).standard_normal(fused.primal_size)
     out = []
     for cache in (fused, tiers):
@@ -75,13 +87,14 @@ def test_fused_projection_matches_tiers_and_oracle(cfg, env):
     assert rel_err(out[0], OracleProblem(prob).project_on_dynamics(zz, r["x0"])) <= 1e-12
 
 
-def test_fused_cp_loop_bit_identical_to_tiers():
+@pytest.mark.parametrize("mode", ["split", "fused"])
+def test_fused_cp_loop_matches_tiers(mode):
     """30 CP iterations (one full 24-iteration graph batch plus a remainder), tol = 0."""
     from oracle.raocp_oracle import OracleProblem
     r = recipe_config(2)
     tree, prob = build_problem(r)
-    fused, tiers = _pair(prob)
-    assert fused.native.kernel_info(9).startswith("k_dyn_fuse")
+    fused, tiers = _pair(prob, None, FUSE if mode == "fused" else SPLIT)
+    assert fused.native.kernel_info(9).startswith("k_dyn_fuse" if mode == "fused" else "k_dyn_up")
     alpha = 0.999 / fused.native.step_size()
     out = []
     for cache in (fused, tiers):
@@ -95,13 +108,15 @@ def test_fused_cp_loop_bit_identical_to_tiers():
     assert trace_rel_err(out[0][1], err_o) <= 1e-8 and rel_err(out[0][3], z_o) <= 1e-10
 
 
-def test_fused_many_launches_then_projection():
-    """1,000 back-to-back launches (graph-replayed, as in the CP loop): the tickets are reset
-    and the epoch advances inside the kernel; a projection afterwards is still exact."""
+@pytest.mark.parametrize("mode", ["split", "fused"])
+def test_fused_many_launches_then_projection(mode):
+    """1,000 back-to-back launches (graph-replayed, as in the CP loop): the tickets / counters
+    are reset and the epoch advances inside the kernels; a projection afterwards is the same
+    bit for bit."""
     r = recipe_config(2)
     tree, prob = build_problem(r)
-    fused = core.Cache(prob)
-    assert fused.native.kernel_info(9).startswith("k_dyn_fuse")
+    fused = _with_env(FUSE if mode == "fused" else SPLIT, lambda: core.Cache(prob))
+    assert fused.native.kernel_info(9).startswith("k_dyn_fuse" if mode == "fused" else "k_dyn_up")
     zz = np.random.default_rng(9).standard_normal(fused.primal_size)
     out = []
     for rep in range(2):  # (op_bench initialises the CP control block with x0 = 0)
