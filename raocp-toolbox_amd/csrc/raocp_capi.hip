@@ -1905,7 +1905,10 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             return v >= 64 && v <= 1024 && v % 64 == 0 ? v : def;
         };
         c->dyn_block = wg_env("RAOCP_DYN_BLOCK", 512);
-        c->dyn_top_block = wg_env("RAOCP_DYN_TOP_BLOCK", 1024);
+        // the top on 512 lanes like the split sweep's top workgroups (kFuseBlock): the level
+        // routines pick their split-k width from the lane count, so a sharded solve (tier
+        // launches) reproduces the unsharded one (split sweep) bit for bit
+        c->dyn_top_block = wg_env("RAOCP_DYN_TOP_BLOCK", raocp::kFuseBlock);
         if (R * raocp::kKS > c->dyn_block) c->dyn_block = 1024;  // a child's split-k rows in one workgroup
         const long wg_per_cu = 2;
         auto level_cost = [&](double P, double C) { return 3.0 + (C * R + P * R + P * nu + C * nx) / 384.0; };
