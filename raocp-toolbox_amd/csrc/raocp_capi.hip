@@ -116,6 +116,9 @@ struct raocp_ctx {
     bool fuse_st = false;        // its static three-array LDS layout (raocp::FuseStat)
     bool dyn_split = false;      // the tiered sweep in TWO launches (k_dyn_up / k_dyn_down)
     size_t lds_up = 0, lds_down = 0;
+    bool dyn_one = false;        // ... in ONE launch with the same roles (k_dyn_one)
+    bool one_fl = false;         // k_dyn_one's top holds its F rows in LDS
+    size_t lds_one = 0;
     unsigned* fuse_sync = nullptr;  // [epoch | error word | per tier: tickets, flags]
     double* x0 = nullptr;
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
@@ -538,6 +541,15 @@ struct FuseOcc {
             *per_cu = 0;
     }
 };
+struct OneOcc {
+    template <int NX, int NU>
+    void run(raocp_ctx* c, bool fl, size_t lds, int* per_cu) {
+        auto k = fl ? raocp::k_dyn_one<NX, NU, true> : raocp::k_dyn_one<NX, NU, false>;
+        allow_lds(k, lds);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)k, raocp::kFuseBlock, lds) != hipSuccess)
+            *per_cu = 0;
+    }
+};
 // the static layout's capacities (doubles; 0 where there is none)
 struct FuseStatOf {
     template <int NX, int NU>
@@ -569,6 +581,19 @@ struct DynOp {
             return ta;
         };
         auto tier_blocks = [&](int k) { return sharded ? c->tier_own[k].second : c->tiers[k].nsub; };
+        if (s > 0 && c->dyn_one && !sharded && part == 0) {
+            // the split sweep in one launch (raocp_dynf.hip, k_dyn_one): block 0 runs the
+            // deferred stopping test when there is one
+            raocp::FuseArg fa = c->fuse;
+            if (ck) fa.ck = *ck;
+            int nsub = 0;
+            for (const auto& tp : c->tiers) nsub += tp.nsub;
+            auto k1 = c->one_fl ? raocp::k_dyn_one<NX, NU, true> : raocp::k_dyn_one<NX, NU, false>;
+            allow_lds(k1, c->lds_one);
+            k1<<<nsub + 1 + (fa.ck.on ? 1 : 0), raocp::kFuseBlock, c->lds_one, c->stream>>>(dev_for(), bf, ctl, zsel, c->q,
+                                                                                            c->x0, fa);
+            return;
+        }
         if (s > 0 && c->dyn_split && !sharded && part == 0) {
             // the tiered sweep in two launches (raocp_dynf.hip): one workgroup per subtree of
             // every tier plus the top; k_dyn_up runs the deferred stopping test in block 0
@@ -683,7 +708,7 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
 // the fused sweep's error word (a hand-off wait timed out, raocp_dynf.hip): checked after
 // every synchronised run that may have launched it; the context is unusable afterwards
 int fuse_err(raocp_ctx* c) {
-    if (!(c->dyn_fuse || c->dyn_split) || !c->fuse_sync) return RAOCP_OK;
+    if (!(c->dyn_fuse || c->dyn_split || c->dyn_one) || !c->fuse_sync) return RAOCP_OK;
     int e = 0;
     HIPCHK(hipMemcpy(&e, c->fuse_sync + 1, sizeof(int), hipMemcpyDeviceToHost));
     if (e) return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dyn_up / k_dyn_down / k_dyn_fuse); "
@@ -1086,6 +1111,8 @@ std::string kernel_name(const raocp_ctx* c, int op) {
                 for (int t = 0; t < c->N; ++t) add("k_dy3_fwd<" + T + ", " + nn + ">");
             } else if (c->dyn2) {
                 return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
+            } else if (c->cut > 0 && c->dyn_one && c->sh_S == 0) {
+                return "k_dyn_one<" + nn + ", " + b(c->one_fl) + "> x1";
             } else if (c->cut > 0 && c->dyn_split && c->sh_S == 0) {
                 return "k_dyn_up<" + nn + "> x1 + k_dyn_down<" + nn + ", " + b(c->f_lds_top) + "> x1";
             } else if (c->cut > 0 && c->dyn_fuse && c->sh_S == 0) {
@@ -2104,7 +2131,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             bool split = true;
             if (const char* e = getenv("RAOCP_DYN_SPLIT")) split = atoi(e) != 0;
             c->dyn_split = false;
-            size_t up = 0, down = 0;  // the split sweep's LDS (doubles)
+            size_t up = 0, down = 0, one = 0;  // the split sweeps' LDS (doubles)
             raocp::FuseArg& fa = c->fuse;
             memset(&fa, 0, sizeof(fa));
             // doubles: XD rows | S1 (the deepest tier) | S2 (the tiers above, the top)
@@ -2150,6 +2177,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 reg = std::max(reg, std::max(back, fwd));
                 up = std::max(up, back);
                 down = std::max(down, (size_t)raocp::rup((int)(nnl * KF), 2) + fwd);
+                one = std::max(one, (size_t)raocp::rup((int)(nnl * KF), 2) + std::max(back, fwd));
             }
             if (fz) {  // the top's backward (k_dyn_up) and forward (k_dyn_down) layouts
                 const size_t T = c->stage_ptr[c->cut], nb = stage_n(c->cut);
@@ -2186,6 +2214,32 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             if (elig && !want_fuse) {  // the split sweep (or the tier launches)
                 c->dyn_split = split;
                 fz = false;
+                // ... in one launch when the whole grid is co-resident: the top's F rows in
+                // LDS if that keeps it so, else read from L2
+                const char* e1 = getenv("RAOCP_DYN_ONE");  // opt-in (RAOCP_DYN_ONE=1), DESIGN.md 4.2
+                const bool on1 = split && e1 && atoi(e1) != 0;
+                const long grid1 = [&] {
+                    long g = 2;  // the top and the deferred stopping test
+                    for (const auto& tp : c->tiers) g += tp.nsub;
+                    return g;
+                }();
+                const size_t T = c->stage_ptr[c->cut], nb = stage_n(c->cut);
+                const int c1 = cp[c->cut], p1 = pp[c1];
+                for (int fl = 1; on1 && fl >= 0 && !c->dyn_one; --fl) {
+                    if (fl && !c->f_lds_top) continue;
+                    const size_t top = (c->fold_top ? (size_t)p1 * W1 : c->nkind * W1) + c1 * RG1 + c1 * KM1 +
+                                       (fl ? (size_t)p1 * F1 : 0) + T * KP + nb * KP + T * NUP + T * KF +
+                                       (c->fold_top ? 0 : raocp::rup(c->maxch_top * PS, 2)) + recs(T + T + nb - 1);
+                    const size_t lds = 8 * std::max(one, top);
+                    if (lds > kLds) continue;
+                    int per_cu = 0;
+                    dispatch(nx, nu, OneOcc{}, c, fl != 0, lds, &per_cu);
+                    if (per_cu > 0 && grid1 <= (long)n_cus * per_cu) {
+                        c->dyn_one = true;
+                        c->one_fl = fl != 0;
+                        c->lds_one = lds;
+                    }
+                }
             }
             if (fz) {
                 int per_cu = 0;
@@ -2222,7 +2276,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             }
             c->dyn_fuse = fz;
             if (getenv("RAOCP_DYN_VERBOSE") && c->dyn_split)
-                fprintf(stderr, "[raocp] split sweep: %d tiers, LDS %zu / %zu B\n", fa.K, c->lds_up, c->lds_down);
+                fprintf(stderr, "[raocp] split sweep: %d tiers, LDS %zu / %zu B; one launch: %s (LDS %zu B, top F %s)\n", fa.K,
+                        c->lds_up, c->lds_down, c->dyn_one ? "yes" : "no", c->lds_one, c->one_fl ? "LDS" : "L2");
         }
         if (getenv("RAOCP_DYN_VERBOSE")) {
             fprintf(stderr, "[raocp] dynamics plan: top stages [0,%d) lds %zu F%s%s", c->cut, c->lds_top,

@@ -790,3 +790,87 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const C
     if (p.stamps && tid == 0 && b == 0)  // diagnostics: tier 0 / deepest, subtree 0
         for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
 }
+
+// ==============================================================================
+// The split sweep in ONE launch (k_dyn_one, the default where its grid is co-resident): the
+// roles of k_dyn_up ([deferred stopping test] [deepest subtrees] .. [tier 0] [top]), and
+// every subtree workgroup then sweeps its own subtree forward too: it keeps d_i in LDS (its
+// XD rows), stages its forward tables while it waits for its parent's flag, and releases
+// its children's. The top sweeps backward and forward (its F rows in LDS or, to keep two
+// workgroups per CU, read from L2). A subtree workgroup now waits after its own backward
+// sweep for workgroups that may not have started, so the host launches it only when the
+// whole grid is co-resident (hipOccupancyMaxActiveBlocksPerMultiprocessor), and every wait
+// stays bounded. The epoch is read by every workgroup at its start and advanced by the top
+// after the last arrival (so after every read).
+template <int NXc, int NUc, bool FL>
+// two workgroups per CU (<= 128 VGPRs, 4 waves per SIMD): the grid (272 + 2 workgroups at
+// config 2) must be co-resident on 256 CUs
+__global__ void __launch_bounds__(kFuseBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) k_dyn_one(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+                                                        double* qbuf_, const double* x0_, FuseArg fa) {
+    extern __shared__ __attribute__((aligned(16))) double smem_[];
+    __shared__ Prologue pl;
+    __shared__ int s_ok;
+    const int tid = threadIdx.x;
+    if (fa.ck.on && blockIdx.x == 0) {  // the previous CP iteration's stopping test
+        if (tid < 64) cp_check_wave(fa.ck);
+        return;
+    }
+    ldsd* smem = (ldsd*)smem_;
+    glbd* z = dyn_z(bf, zsel, ctl);
+    if (tid == 0) {
+        pl.nts = 0;
+        s_ok = 1;
+    }
+    fz_stamp(p, pl);
+    const int D = fa.K - 1;
+    int b = (int)blockIdx.x - (fa.ck.on ? 1 : 0), k = D;
+    for (; k >= 0 && b >= fa.t[k].ngroups * fa.t[k].r; --k) b -= fa.t[k].ngroups * fa.t[k].r;
+    if (k < 0) {  // the top: backward and forward
+        fz_top_stage<NXc, NUc, FL>(p, z, fa, smem, pl, false);
+        const unsigned tag = ld_u32_sc1(fa.epoch) + 1u;
+        const bool work = !ctl_done(ctl);
+        if (!fz_wait_eq(fa.t[0].cnt, (unsigned)fa.t[0].r, fa, s_ok)) return;
+        if (tid == 0) st_u32_sc1(fa.t[0].cnt, 0u);
+        fz_stamp(p, pl);
+        if (work) fz_top_run<NXc, NUc, FL>(p, z, qbuf_, x0_, fa, smem, pl, nullptr);
+        fz_stamp(p, pl);
+        fz_drain();
+        if (tid == 0) {
+            st_u32_sc1(fa.epoch, tag);
+            st_u32_sc1(fa.t[0].flag, tag);
+        }
+        if (p.stamps && tid == 0)
+            for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[q] = pl.ts[q];
+        return;
+    }
+    // subtree b of tier k: [XD (nnl, KF) | backward, then forward region]
+    const FuseTier& tt = fa.t[k];
+    ldsd* XD = smem;
+    ldsd* scr = smem + rup(tt.nnl * Geo<NXc, NUc>(p).KF, 2);
+    // (LDS stores before the LDS-DMA copies: a store after them would wait for them)
+    zero_fill(XD, tt.nnl * Geo<NXc, NUc>(p).KF, tid, blockDim.x);  // x (root: later) / d / zero tail
+    fz_back_stage<NXc, NUc>(p, z, tt, b, k == D, scr);
+    const unsigned tag = ld_u32_sc1(fa.epoch) + 1u;
+    const bool work = !ctl_done(ctl);
+    if (k < D && !fz_wait_eq(fa.t[k + 1].cnt + b, (unsigned)fa.t[k + 1].r, fa, s_ok)) return;
+    if (k < D && tid == 0) st_u32_sc1(fa.t[k + 1].cnt + b, 0u);
+    fz_stamp(p, pl);
+    if (work) {
+        fz_back_wait<NXc, NUc>(p, qbuf_, tt, b, k == D, scr, pl);
+        fz_back_levels<NXc, NUc>(p, qbuf_, tt, b, k == D, XD, scr, pl);
+    }
+    fz_stamp(p, pl);
+    fz_drain();
+    if (tid == 0) __hip_atomic_fetch_add(tt.cnt + b / tt.r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (work) fz_fwd_stage<NXc, NUc>(p, tt, b, scr);  // the backward region is free
+    if (!fz_wait_eq(tt.flag + b / tt.r, tag, fa, s_ok)) return;
+    fz_stamp(p, pl);
+    if (work) fz_fwd_run<NXc, NUc>(p, z, tt, b, k < D, XD, scr, pl);
+    fz_stamp(p, pl);
+    if (k < D) {
+        fz_drain();
+        if (tid == 0) st_u32_sc1(fa.t[k + 1].flag + b, tag);
+    }
+    if (p.stamps && tid == 0 && b == 0)  // diagnostics: tier 0 / deepest, subtree 0
+        for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
+}

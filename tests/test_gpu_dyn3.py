@@ -113,14 +113,14 @@ def test_dyn3_deferred_stopping_test_matches_eager(iters, stop):
 
 def test_kernel_info_lists_the_projection_launches():
     """raocp_kernel_info(9) names every launch of one projection as "name xcount" terms
-    (bench.py sums their PMC traffic): the split sweep (k_dyn_up + k_dyn_down) at config 2,
-    2 tiers + the top with RAOCP_DYN_SPLIT=0, the fused sweep (one launch) with
+    (bench.py sums their PMC traffic): the split sweep (k_dyn_up + k_dyn_down) at config 2, in
+    one launch (k_dyn_one) with RAOCP_DYN_ONE=1, 2 tiers + the top with RAOCP_DYN_SPLIT=0, the fused sweep (one launch) with
     RAOCP_DYN_FUSE=1, one k_dy3_back and one k_dy3_fwd per nonleaf stage with RAOCP_DYN3=1."""
     import re
     r = recipe_config(2)
     prob = build_problem(r)[1]
-    for env, want in (({}, "split"), ({"RAOCP_DYN_SPLIT": "0"}, None), ({"RAOCP_DYN_FUSE": "1"}, "fuse"),
-                      ({"RAOCP_DYN3": "1"}, "dy3")):
+    for env, want in (({}, "split"), ({"RAOCP_DYN_ONE": "1"}, "one"), ({"RAOCP_DYN_SPLIT": "0"}, None),
+                      ({"RAOCP_DYN_FUSE": "1"}, "fuse"), ({"RAOCP_DYN3": "1"}, "dy3")):
         cache = _with_env(env, lambda: core.Cache(prob))
         terms = [re.fullmatch(r"(k_\w+<[^>]*>) x(\d+)", t) for t in cache.native.kernel_info(9).split(" + ")]
         assert all(terms), cache.native.kernel_info(9)
@@ -131,5 +131,7 @@ def test_kernel_info_lists_the_projection_launches():
             assert cnt == {"k_dyn_fuse": 1}
         elif want == "split":
             assert cnt == {"k_dyn_up": 1, "k_dyn_down": 1}
+        elif want == "one":
+            assert cnt == {"k_dyn_one": 1}
         else:
             assert cnt["k_dyn_top"] == 1 and cnt["k_dyn_bottom_back"] == cnt["k_dyn_bottom_fwd"] >= 1

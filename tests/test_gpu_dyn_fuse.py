@@ -1,7 +1,8 @@
 """GPU parity of the tiered dynamics sweep in fewer launches (raocp_dynf.hip; cache.py:259-288):
-- the split sweep k_dyn_up + k_dyn_down (the default of fp64 trees with a regular tier plan,
-  config 2): one workgroup per subtree of every tier plus the top, counters of arrivals up
-  the tiers, epoch flags down;
+- the split sweep: one workgroup per subtree of every tier plus the top, counters of
+  arrivals up the tiers, epoch flags down; in two launches (k_dyn_up + k_dyn_down, the
+  default of fp64 trees with a regular tier plan, config 2) or one (k_dyn_one, opt-in
+  RAOCP_DYN_ONE=1 where the grid is co-resident);
 - the fused sweep k_dyn_fuse (opt-in RAOCP_DYN_FUSE=1): one launch, one workgroup per
   deepest-tier subtree, tickets up the tiers and flags down;
 against the tier launches (RAOCP_DYN_SPLIT=0).
@@ -49,7 +50,9 @@ def _recipe(cfg):
 
 FUSE = {"RAOCP_DYN_FUSE": "1"}
 SPLIT = {}
+ONE = {"RAOCP_DYN_ONE": "1"}
 TIERS = {"RAOCP_DYN_SPLIT": "0"}
+MODES = {"fused": (FUSE, "k_dyn_fuse"), "split": (SPLIT, "k_dyn_up"), "one": (ONE, "k_dyn_one")}
 
 
 def _pair(prob, env=None, mode=FUSE):
@@ -61,7 +64,7 @@ def _pair(prob, env=None, mode=FUSE):
 
 @pytest.mark.parametrize("env", [{}, {"RAOCP_DYN_FOLD": "0"}, {"RAOCP_FUSE_PREFETCH": "0"}],
                          ids=["default", "two_phase", "one_region"])
-@pytest.mark.parametrize("mode", ["split", "fused"])
+@pytest.mark.parametrize("mode", ["one", "split", "fused"])
 @pytest.mark.parametrize("cfg", ["c2", "quad", "bin10"])
 def test_fused_projection_matches_tiers_and_oracle(cfg, mode, env):
     """default: one-phase backward levels (per-pair WT tables) in the sweep and in the tiers;
@@ -71,11 +74,11 @@ def test_fused_projection_matches_tiers_and_oracle(cfg, mode, env):
     from oracle.raocp_oracle import OracleProblem
     r = _recipe(cfg)
     tree, prob = build_problem(r)
-    fused, tiers = _pair(prob, env, FUSE if mode == "fused" else SPLIT)
-    name = "k_dyn_fuse" if mode == "fused" else "k_dyn_up"
+    fused, tiers = _pair(prob, env, MODES[mode][0])
+    name = MODES[mode][1]
     if not fused.native.kernel_info(9).startswith(name):
         pytest.skip(f"{mode} sweep not planned for this tree: " + fused.native.kernel_info(9))
-    assert "k_dyn_fuse" not in tiers.native.kernel_info(9) and "k_dyn_up" not in tiers.native.kernel_info(9)
+    assert not any(n in tiers.native.kernel_info(9) for _, n in MODES.values())
     zz = np.random.default_rng(5).standard_normal(fused.primal_size)
     out = []
     for cache in (fused, tiers):
@@ -87,14 +90,14 @@ def test_fused_projection_matches_tiers_and_oracle(cfg, mode, env):
     assert rel_err(out[0], OracleProblem(prob).project_on_dynamics(zz, r["x0"])) <= 1e-12
 
 
-@pytest.mark.parametrize("mode", ["split", "fused"])
+@pytest.mark.parametrize("mode", ["one", "split", "fused"])
 def test_fused_cp_loop_matches_tiers(mode):
     """30 CP iterations (one full 24-iteration graph batch plus a remainder), tol = 0."""
     from oracle.raocp_oracle import OracleProblem
     r = recipe_config(2)
     tree, prob = build_problem(r)
-    fused, tiers = _pair(prob, None, FUSE if mode == "fused" else SPLIT)
-    assert fused.native.kernel_info(9).startswith("k_dyn_fuse" if mode == "fused" else "k_dyn_up")
+    fused, tiers = _pair(prob, None, MODES[mode][0])
+    assert fused.native.kernel_info(9).startswith(MODES[mode][1])
     alpha = 0.999 / fused.native.step_size()
     out = []
     for cache in (fused, tiers):
@@ -108,15 +111,15 @@ def test_fused_cp_loop_matches_tiers(mode):
     assert trace_rel_err(out[0][1], err_o) <= 1e-8 and rel_err(out[0][3], z_o) <= 1e-10
 
 
-@pytest.mark.parametrize("mode", ["split", "fused"])
+@pytest.mark.parametrize("mode", ["one", "split", "fused"])
 def test_fused_many_launches_then_projection(mode):
     """1,000 back-to-back launches (graph-replayed, as in the CP loop): the tickets / counters
     are reset and the epoch advances inside the kernels; a projection afterwards is the same
     bit for bit."""
     r = recipe_config(2)
     tree, prob = build_problem(r)
-    fused = _with_env(FUSE if mode == "fused" else SPLIT, lambda: core.Cache(prob))
-    assert fused.native.kernel_info(9).startswith("k_dyn_fuse" if mode == "fused" else "k_dyn_up")
+    fused = _with_env(MODES[mode][0], lambda: core.Cache(prob))
+    assert fused.native.kernel_info(9).startswith(MODES[mode][1])
     zz = np.random.default_rng(9).standard_normal(fused.primal_size)
     out = []
     for rep in range(2):  # (op_bench initialises the CP control block with x0 = 0)

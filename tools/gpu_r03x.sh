@@ -1,0 +1,12 @@
+# k_dyn_one at four waves per SIMD: timing against the two-launch split sweep, the dynamics tests.
+export TMPDIR=/tmp
+set -o pipefail
+mkdir -p gpurun_out
+RAOCP_DYN_VERBOSE=1 timeout -k 10 300 python -u tools/dyn_time.py 2 default RAOCP_DYN_ONE=0 RAOCP_DYN_SPLIT=0 > gpurun_out/dyn_time.log 2>&1 || { cat gpurun_out/dyn_time.log; exit 1; }
+cat gpurun_out/dyn_time.log
+timeout -k 10 120 python3 tools/stamps.py 2 > gpurun_out/stamps_c2.log 2>&1 || { tail -5 gpurun_out/stamps_c2.log; exit 1; }
+cat gpurun_out/stamps_c2.log
+timeout -k 10 600 python -u -m pytest -m gpu -x -q tests/test_gpu_dyn_fuse.py tests/test_gpu_dyn3.py tests/test_gpu_variants.py --timeout 120 --timeout-method thread > gpurun_out/pytest_dyn.log 2>&1 || { tail -60 gpurun_out/pytest_dyn.log; exit 1; }
+tail -2 gpurun_out/pytest_dyn.log
+timeout -k 10 600 python -u tools/cp3_time.py 2 > gpurun_out/cp3_time.log 2>&1 || { cat gpurun_out/cp3_time.log; exit 1; }
+cat gpurun_out/cp3_time.log

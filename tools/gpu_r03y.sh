@@ -1,0 +1,8 @@
+# k_dyn_one at four waves per SIMD (the one-launch default build): timing and stamps only.
+export TMPDIR=/tmp
+set -o pipefail
+mkdir -p gpurun_out
+RAOCP_DYN_VERBOSE=1 timeout -k 10 300 python -u tools/dyn_time.py 2 default RAOCP_DYN_ONE=0 RAOCP_DYN_SPLIT=0 > gpurun_out/dyn_time.log 2>&1 || { cat gpurun_out/dyn_time.log; exit 1; }
+cat gpurun_out/dyn_time.log
+timeout -k 10 120 python3 tools/stamps.py 2 > gpurun_out/stamps_c2.log 2>&1 || { tail -5 gpurun_out/stamps_c2.log; exit 1; }
+cat gpurun_out/stamps_c2.log
