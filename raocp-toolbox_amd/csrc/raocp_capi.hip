@@ -4,6 +4,7 @@
 // raocp_kernels.hip and replays the CP iteration as a captured hipGraph.
 
 #include "raocp_kernels.hip"
+#include "raocp_dynr.h"
 #include "../../include/raocp_hip.h"
 
 #include <dlfcn.h>
@@ -110,16 +111,20 @@ struct raocp_ctx {
         raocp::TierArg ta;       // the same, as a kernel argument, when the tier is regular
     };
     std::vector<TierPlan> tiers;
-    bool dyn_fuse = false;       // the tiered sweep in ONE launch (k_dyn_fuse, raocp_dynf.hip)
-    raocp::FuseArg fuse{};       // its plan (tickets / flags in fuse_sync)
-    size_t lds_fuse = 0;
-    bool fuse_st = false;        // its static three-array LDS layout (raocp::FuseStat)
+    raocp::FuseArg fuse{};       // the split sweep's plan (counters / flags in fuse_sync)
     bool dyn_split = false;      // the tiered sweep in TWO launches (k_dyn_up / k_dyn_down)
     size_t lds_up = 0, lds_down = 0;
-    bool dyn_one = false;        // ... in ONE launch with the same roles (k_dyn_one)
-    bool one_fl = false;         // k_dyn_one's top holds its F rows in LDS
-    size_t lds_one = 0;
-    unsigned* fuse_sync = nullptr;  // [epoch | error word | per tier: tickets, flags]
+    unsigned* fuse_sync = nullptr;  // [epoch | error word | per tier: counters, flags]
+    size_t fuse_words = 0;
+    // the regular-tree sweep (raocp_dynr.hip): two launches, one workgroup per subtree of
+    // every tier; the default for fp64 regular trees of the compiled sizes (RAOCP_DR=0: off)
+    bool reg_ok = false;            // uniform branching, one class per stage, one pair per slot
+    int reg_C = 0;
+    std::vector<raocp::Dy3Stage> reg_st;
+    bool dr = false;
+    raocp::DrPlan drp{};
+    int dr_block = 512;
+    size_t dr_lds_up = 0, dr_lds_dn = 0;
     double* x0 = nullptr;
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
     Ctl* ctl = nullptr;
@@ -169,8 +174,6 @@ struct raocp_ctx {
     int n_ph = 0;
     bool has_x0 = false;
     std::vector<double> h_x0;
-    unsigned* ticket = nullptr;  // k_cpp blocks done (fused stopping test)
-    bool no_fuse_check = true;   // RAOCP_FUSE_CHECK=1: the stopping test inside k_cpp's last block
     bool no_defer_check = false; // RAOCP_DEFER_CHECK=0: k_cp_check after every iteration (defer_check)
                                  // (measured slower than its own launch: DESIGN.md)
     // captured CP iterations
@@ -522,41 +525,18 @@ void launch_dyn3(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* c
     }
 }
 
-// workgroups of k_dyn_fuse per CU at the context's block and LDS size
-// the k_dyn_fuse instantiation of a context (static LDS layout only where FuseStat has one)
-template <int NX, int NU>
-auto fuse_kernel(const raocp_ctx* c) {
-    if constexpr (raocp::FuseStat<NX, NU>::A > 0) {
-        if (c->fuse_st) return raocp::k_dyn_fuse<NX, NU, true, true>;
-    }
-    return raocp::k_dyn_fuse<NX, NU, true, false>;
-}
-struct FuseOcc {
+// workgroups per CU of the split sweep's two kernels at their LDS sizes (co-residency)
+struct SplitOcc {
     template <int NX, int NU>
-    void run(raocp_ctx* c, int* per_cu) {
-        auto kf = fuse_kernel<NX, NU>(c);
-        allow_lds(kf, c->lds_fuse);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)kf, raocp::kFuseBlock, c->lds_fuse) !=
-            hipSuccess)
-            *per_cu = 0;
-    }
-};
-struct OneOcc {
-    template <int NX, int NU>
-    void run(raocp_ctx* c, bool fl, size_t lds, int* per_cu) {
-        auto k = fl ? raocp::k_dyn_one<NX, NU, true> : raocp::k_dyn_one<NX, NU, false>;
-        allow_lds(k, lds);
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(per_cu, (const void*)k, raocp::kFuseBlock, lds) != hipSuccess)
-            *per_cu = 0;
-    }
-};
-// the static layout's capacities (doubles; 0 where there is none)
-struct FuseStatOf {
-    template <int NX, int NU>
-    void run(int* x, int* a, int* b) {
-        *x = raocp::FuseStat<NX, NU>::X;
-        *a = raocp::FuseStat<NX, NU>::A;
-        *b = raocp::FuseStat<NX, NU>::B;
+    void run(raocp_ctx* c, int* pu, int* pd) {
+        auto ku = raocp::k_dyn_up<NX, NU>;
+        auto kd = c->f_lds_top ? raocp::k_dyn_down<NX, NU, true> : raocp::k_dyn_down<NX, NU, false>;
+        allow_lds(ku, c->lds_up);
+        allow_lds(kd, c->lds_down);
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(pu, (const void*)ku, raocp::kFuseBlock, c->lds_up) != hipSuccess)
+            *pu = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(pd, (const void*)kd, raocp::kFuseBlock, c->lds_down) != hipSuccess)
+            *pd = 0;
     }
 };
 
@@ -581,19 +561,6 @@ struct DynOp {
             return ta;
         };
         auto tier_blocks = [&](int k) { return sharded ? c->tier_own[k].second : c->tiers[k].nsub; };
-        if (s > 0 && c->dyn_one && !sharded && part == 0) {
-            // the split sweep in one launch (raocp_dynf.hip, k_dyn_one): block 0 runs the
-            // deferred stopping test when there is one
-            raocp::FuseArg fa = c->fuse;
-            if (ck) fa.ck = *ck;
-            int nsub = 0;
-            for (const auto& tp : c->tiers) nsub += tp.nsub;
-            auto k1 = c->one_fl ? raocp::k_dyn_one<NX, NU, true> : raocp::k_dyn_one<NX, NU, false>;
-            allow_lds(k1, c->lds_one);
-            k1<<<nsub + 1 + (fa.ck.on ? 1 : 0), raocp::kFuseBlock, c->lds_one, c->stream>>>(dev_for(), bf, ctl, zsel, c->q,
-                                                                                            c->x0, fa);
-            return;
-        }
         if (s > 0 && c->dyn_split && !sharded && part == 0) {
             // the tiered sweep in two launches (raocp_dynf.hip): one workgroup per subtree of
             // every tier plus the top; k_dyn_up runs the deferred stopping test in block 0
@@ -608,17 +575,6 @@ struct DynOp {
             ku<<<nsub + 1 + (fa.ck.on ? 1 : 0), raocp::kFuseBlock, c->lds_up, c->stream>>>(dev_for(), bf, ctl, zsel, c->q,
                                                                                            c->d, fa);
             kd<<<nsub + 1, raocp::kFuseBlock, c->lds_down, c->stream>>>(dev_for(), bf, ctl, zsel, c->d, c->x0, fa);
-            return;
-        }
-        if (s > 0 && c->dyn_fuse && !sharded && part == 0) {
-            // the whole tiered sweep in one launch (raocp_dynf.hip), one workgroup per subtree
-            // of the deepest tier; it runs the deferred stopping test itself
-            raocp::FuseArg fa = c->fuse;
-            if (ck) fa.ck = *ck;
-            auto kf = fuse_kernel<NX, NU>(c);
-            allow_lds(kf, c->lds_fuse);
-            kf<<<c->tiers.back().nsub, raocp::kFuseBlock, c->lds_fuse, c->stream>>>(dev_for(), bf, ctl, zsel, c->q, c->x0,
-                                                                                    fa);
             return;
         }
         if (s > 0) {
@@ -691,6 +647,15 @@ struct DynOp {
 // launch (only where defer_check(c) holds)
 void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int part = 0,
                      const raocp::ChkArg* ck = nullptr) {
+    if (c->dr && c->sh_S == 0 && part == 0) {  // the regular-tree sweep (raocp_dynr.hip)
+        raocp::DrPlan p = c->drp;
+        if (c->dev.stamps) p.stamps = c->dev.stamps;
+        raocp::dr_launch_up(p, c->nx, c->nu, c->dr_block, c->dr_lds_up, bf, zsel, ctl,
+                            ck ? *ck : raocp::ChkArg{nullptr, nullptr, nullptr, 0, 0}, c->stream);
+        if (c->dev.stamps) p.stamps = c->dev.stamps + 64;
+        raocp::dr_launch_down(p, c->nx, c->nu, c->dr_block, c->dr_lds_dn, bf, zsel, ctl, c->stream);
+        return;
+    }
     if (c->dyn3) {
         double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
         launch_dyn3(c, z, ctl, ck, part);
@@ -708,11 +673,182 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
 // the fused sweep's error word (a hand-off wait timed out, raocp_dynf.hip): checked after
 // every synchronised run that may have launched it; the context is unusable afterwards
 int fuse_err(raocp_ctx* c) {
-    if (!(c->dyn_fuse || c->dyn_split || c->dyn_one) || !c->fuse_sync) return RAOCP_OK;
+    if (c->dr && c->sh_S == 0) {
+        unsigned e = 0;
+        HIPCHK(hipMemcpy(&e, c->drp.sync + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+        if (e) {
+            // clear every counter, flag, the epoch and the error word: the next projection
+            // starts from a clean protocol state
+            HIPCHK(hipMemset(c->drp.sync, 0, (2 + 2 * (size_t)c->drp.S) * sizeof(unsigned)));
+            return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dr_up / k_dr_down); "
+                                         "RAOCP_DR=0 selects the tiered sweep");
+        }
+        return RAOCP_OK;
+    }
+    if (!c->dyn_split || !c->fuse_sync) return RAOCP_OK;
     int e = 0;
     HIPCHK(hipMemcpy(&e, c->fuse_sync + 1, sizeof(int), hipMemcpyDeviceToHost));
-    if (e) return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dyn_up / k_dyn_down / k_dyn_fuse); "
+    if (e) HIPCHK(hipMemset(c->fuse_sync, 0, c->fuse_words * sizeof(unsigned)));  // clean protocol state
+    if (e) return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dyn_up / k_dyn_down); "
                                         "RAOCP_DYN_SPLIT=0 selects the tier launches");
+    return RAOCP_OK;
+}
+
+// ---- the regular-tree sweep (raocp_dynr.hip) -----------------------------------------------
+// Tables in the kernels' LDS order, per nonleaf stage t (its class and the pairs of its child
+// slots, c->reg_st[t]):
+//   backward [R rows][KS slots][SX]: WT = [-Rinv B' ; A' - G B'] of slot k's pair (zero rows for
+//            k >= C), then [R rows][NUP]: RG = [Rinv ; G] of the class (zero tail);
+//   forward  [C slots][nx rows][SF]: [Abar_k | B_k], then [nu rows][SX]: K of the class.
+// The tier plan minimises a cost model of the critical path (us: per level a barrier and the
+// lane work of the backward and forward passes, per tier boundary one hand-off each way) over
+// cut lists of at most kDrMaxTiers tiers, with the whole grid (one workgroup per subtree of
+// every tier) within the CU count: every workgroup of a launch is then resident at once, so no
+// wait depends on the dispatch order. RAOCP_DR_CUTS="s1,s2,.." forces the cuts.
+int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::vector<double>& RG, int SNU,
+             const std::vector<double>& KM, const std::vector<double>& F, int SKF, int n_cus) {
+    const int nx = c->nx, nu = c->nu, C = c->reg_C, N = c->N, R = nx + nu;
+    const int KS = raocp::dr_ks(C), SX = raocp::dr_stride(nx), SF = raocp::dr_stride(nx + nu), NUP = raocp::dr_nup(nu, C);
+    const int nb = raocp::dr_back_n(nx, nu, C), nf = raocp::dr_fwd_n(nx, nu, C);
+    auto npow = [&](int e) {
+        long v = 1;
+        for (int i = 0; i < e; ++i) v *= C;
+        return v;
+    };
+    const size_t kLds = 160 * 1024 - 1024;  // minus the kernels' static LDS
+    // cost (us) of a cut list s = {0, s1, .., N}; 1e300 where it does not fit
+    int best_block = 512;
+    auto eval = [&](const std::vector<int>& s, int* block) -> double {
+        const int T = (int)s.size() - 1;
+        if (T < 1 || T > raocp::kDrMaxTiers) return 1e300;
+        long wgs = 0, maxitems = 0;
+        for (int k = 0; k < T; ++k) {
+            const int L = s[k + 1] - s[k];
+            if (L < 1 || L > raocp::kDrMaxLevels) return 1e300;
+            wgs += npow(s[k]);
+            if (raocp::dr_lds_up(nx, nu, C, L, k == T - 1) > kLds || raocp::dr_lds_down(nx, nu, C, L) > kLds) return 1e300;
+            maxitems = std::max(maxitems, npow(L - 1) * std::max<long>(R * KS, C * nx + nu));
+        }
+        if (wgs > n_cus) return 1e300;
+        const int B = maxitems > 512 ? 1024 : 512;
+        if (block) *block = B;
+        double cost = 4.0 * (T - 1);
+        for (int k = 0; k < T; ++k)
+            for (int l = 0; l < s[k + 1] - s[k]; ++l) {
+                const long ib = npow(l) * R * KS, inf = npow(l) * (C * nx + nu);
+                cost += 0.24 + 0.05 * (double)((ib + B - 1) / B + (inf + B - 1) / B) + 4e-4 * ib + 6e-4 * inf;
+            }
+        return cost;
+    };
+    std::vector<int> cuts;
+    if (const char* e = getenv("RAOCP_DR_CUTS")) {
+        cuts.push_back(0);
+        for (const char* p = e; *p;) {
+            char* q = nullptr;
+            const long v = strtol(p, &q, 10);
+            if (q == p) break;
+            if (v > 0 && v < N) cuts.push_back((int)v);
+            p = *q ? q + 1 : q;
+        }
+        cuts.push_back(N);
+        if (!std::is_sorted(cuts.begin(), cuts.end()) || eval(cuts, &best_block) >= 1e299)
+            return fail(RAOCP_ERR_ARG, std::string("RAOCP_DR_CUTS=") + e + ": not a valid tier plan for this tree");
+    } else {
+        double best = 1e300;
+        std::vector<int> s{0};
+        // every increasing cut list of at most kDrMaxTiers tiers
+        auto rec = [&](auto&& self, int from) -> void {
+            s.push_back(N);
+            int B = 512;
+            const double v = eval(s, &B);
+            if (v < best) {
+                best = v;
+                cuts = s;
+                best_block = B;
+            }
+            s.pop_back();
+            if ((int)s.size() >= raocp::kDrMaxTiers) return;
+            for (int a = from; a < N; ++a) {
+                s.push_back(a);
+                self(self, a + 1);
+                s.pop_back();
+            }
+        };
+        rec(rec, 1);
+        if (best >= 1e299) return RAOCP_OK;  // no plan: the sweep stays off
+    }
+    std::vector<double> bimg((size_t)N * nb, 0.0), fimg((size_t)N * nf, 0.0);
+    for (int t = 0; t < N; ++t) {
+        const raocp::Dy3Stage& st = c->reg_st[t];
+        double* b = &bimg[(size_t)t * nb];
+        for (int r = 0; r < R; ++r) {
+            for (int k = 0; k < C; ++k)
+                for (int e = 0; e < nx; ++e) b[((size_t)r * KS + k) * SX + e] = WT[((size_t)st.pair[k] * R + r) * SKP + e];
+            for (int e = 0; e < nu; ++e)
+                b[(size_t)R * KS * SX + (size_t)r * NUP + e] = RG[((size_t)st.cls * R + r) * SNU + e];
+        }
+        double* f = &fimg[(size_t)t * nf];
+        for (int k = 0; k < C; ++k)
+            for (int r = 0; r < nx; ++r)
+                for (int e = 0; e < nx + nu; ++e)
+                    f[((size_t)k * nx + r) * SF + e] = F[((size_t)st.pair[k] * nx + r) * SKF + e];
+        for (int r = 0; r < nu; ++r)
+            for (int e = 0; e < nx; ++e) f[(size_t)C * nx * SF + (size_t)r * SX + e] = KM[((size_t)st.cls * nu + r) * SKP + e];
+    }
+    raocp::DrPlan& p = c->drp;
+    memset(&p, 0, sizeof(p));
+    const int T = (int)cuts.size() - 1;
+    p.T = T;
+    p.C = C;
+    p.N = N;
+    int w = 0, bup = 0;
+    for (int k = T - 1; k >= 0; --k) {  // k_dr_up: the deepest tier first
+        p.t[k].bup = bup;
+        bup += (int)npow(cuts[k]);
+    }
+    for (int k = 0; k < T; ++k) {
+        raocp::DrTier& tt = p.t[k];
+        tt.s0 = cuts[k];
+        tt.L = cuts[k + 1] - cuts[k];
+        tt.nsub = (int)npow(cuts[k]);
+        tt.bdn = w;  // k_dr_down: the top first
+        tt.w0 = w;
+        w += tt.nsub;
+        c->dr_lds_up = std::max(c->dr_lds_up, raocp::dr_lds_up(nx, nu, C, tt.L, k == T - 1));
+        c->dr_lds_dn = std::max(c->dr_lds_dn, raocp::dr_lds_down(nx, nu, C, tt.L));
+    }
+    p.nblk = w;
+    p.S = w;
+    p.X0 = c->dev.X0;
+    p.U0 = c->dev.U0;
+    c->dr_block = best_block;
+    if (const char* e = getenv("RAOCP_DR_BLOCK")) c->dr_block = atoi(e) > 512 ? 1024 : 512;
+    // diagnostics (tests/test_gpu_dynr.py): RAOCP_DR_FAULT=1 makes the deepest tier's first
+    // subtree skip its arrival, so its parent's wait times out
+    if (const char* e = getenv("RAOCP_DR_FAULT")) p.fault = atoi(e);
+    int rc;
+    const double *bi = nullptr, *fi = nullptr;
+    double *qb = nullptr, *db = nullptr;
+    unsigned* sy = nullptr;
+    if ((rc = c->upload_vec(&bi, bimg)) || (rc = c->upload_vec(&fi, fimg)) || (rc = c->alloc(&qb, (size_t)c->n * nx)) ||
+        (rc = c->alloc(&db, (size_t)c->m * nu)) || (rc = c->alloc(&sy, 2 + 2 * (size_t)w)))
+        return rc;
+    HIPCHK(hipMemset(sy, 0, (2 + 2 * (size_t)w) * sizeof(unsigned)));
+    HIPCHK(hipMemset(qb, 0, (size_t)c->n * nx * sizeof(double)));
+    p.bimg = bi;
+    p.fimg = fi;
+    p.qbuf = qb;
+    p.dbuf = db;
+    p.sync = sy;
+    long long ms = 1000;  // a wait normally lasts microseconds
+    if (const char* e = getenv("RAOCP_FUSE_TIMEOUT_MS")) ms = std::max(1, atoi(e));
+    p.timeout = ms * 100000LL;  // 100 MHz ticks
+    c->dr = true;
+    if (getenv("RAOCP_DYN_VERBOSE")) {
+        fprintf(stderr, "[raocp] regular sweep: %d tiers,", T);
+        for (int k = 0; k < T; ++k) fprintf(stderr, " [%d,%d) x%d", p.t[k].s0, p.t[k].s0 + p.t[k].L, p.t[k].nsub);
+        fprintf(stderr, "; %d lanes, LDS %zu / %zu B\n", c->dr_block, c->dr_lds_up, c->dr_lds_dn);
+    }
     return RAOCP_OK;
 }
 
@@ -802,13 +938,12 @@ struct CpdOp {
 };
 template <class T>
 struct CppOp {
-    // fuse: the stopping test rides on the launch's last block (the CP iteration only)
     template <int NX, int NU>
-    void run(raocp_ctx* c, bool fuse) {
+    void run(raocp_ctx* c) {
         auto k = raocp::k_cpp<T, NX, NU>;
         allow_lds(k, c->lds_cpp);
         k<<<c->cp_nbF + c->cp_nbL, kBlock, c->lds_cpp, c->stream>>>(c->dev, c->ctl, c->bufs, c->XI2, c->redpart,
-                                                                     c->cp_nbF, c->hist, fuse ? c->ticket : nullptr);
+                                                                     c->cp_nbF);
     }
 };
 void launch_cpd(raocp_ctx* c) {
@@ -817,10 +952,10 @@ void launch_cpd(raocp_ctx* c) {
     else if (c->cp_v1) dispatch(c->nx, c->nu, CpdOp<double>{}, c);
     else dispatch_rt(c->nx, c->nu, Cpd2Op<double>{}, c);
 }
-void launch_cpp(raocp_ctx* c, bool fuse = false) {
-    if (c->f32 && c->cp_v1) CppOp<float>{}.run<0, 0>(c, fuse);
+void launch_cpp(raocp_ctx* c) {
+    if (c->f32 && c->cp_v1) CppOp<float>{}.run<0, 0>(c);
     else if (c->f32) dispatch_rt(c->nx, c->nu, Cpp2Op<float>{}, c);
-    else if (c->cp_v1 || fuse) dispatch(c->nx, c->nu, CppOp<double>{}, c, fuse);
+    else if (c->cp_v1) dispatch(c->nx, c->nu, CppOp<double>{}, c);
     else dispatch_rt(c->nx, c->nu, Cpp2Op<double>{}, c);
 }
 // the fused CP iteration (raocp_cp3.hip): compile-time sizes of the benchmark configs
@@ -829,7 +964,8 @@ bool cp3_sizes(bool f32, int nx, int nu) {
     return (nx == 20 && nu == 8) || (nx == 32 && nu == 12) || (f32 && nx == 64 && nu == 16);
 }
 // a k_cp3 task list: split leaf tiles [l0, l1), then the parent ranges in order; returns
-// the tiles
+// the tiles, or -1 when the nonempty ranges exceed the kernel argument's kCp3MaxR slots (the
+// caller must not launch it: a dropped range would leave its parents uncomputed)
 long cp3_tasks(raocp::Cp3Tasks& tk, const std::vector<std::pair<int, int>>& ranges, int l0, int l1, int split,
                int mL) {
     tk = raocp::Cp3Tasks{};
@@ -839,7 +975,8 @@ long cp3_tasks(raocp::Cp3Tasks& tk, const std::vector<std::pair<int, int>>& rang
     tk.mL = mL;
     long tiles = (tk.l1 - tk.l0 + 15) / 16;
     for (const auto& r : ranges) {
-        if (r.second <= r.first || tk.nr >= raocp::kCp3MaxR) continue;
+        if (r.second <= r.first) continue;
+        if (tk.nr >= raocp::kCp3MaxR) return -1;
         tk.lo[tk.nr] = r.first;
         tk.hi[tk.nr] = r.second;
         tk.t0[tk.nr + 1] = tk.t0[tk.nr] + (r.second - r.first + 15) / 16;
@@ -908,8 +1045,6 @@ void launch_first_half(raocp_ctx* c) {
     launch_cpp(c);
     c->bufs = keep;
 }
-// RAOCP_FUSE_CHECK=1: the unsharded CP iteration runs its stopping test inside k_cpp
-bool fuse_check(const raocp_ctx* c) { return !c->comm && c->sh_R == 1 && !c->no_fuse_check; }
 // Deferred stopping test (default for the tiered dynamics; RAOCP_DEFER_CHECK=0 disables):
 // iteration k's test runs in an extra workgroup of iteration k + 1's first dynamics launch
 // instead of its own k_cp_check launch after k_cpp, and a batch ends with one k_cp_check
@@ -918,8 +1053,9 @@ bool fuse_check(const raocp_ctx* c) { return !c->comm && c->sh_R == 1 && !c->no_
 // z+_k = Z[k % 3] or eta+_k = E[k % 2]), and every later kernel exits on ctl->done, so the
 // result and the history are those of the eager test.
 bool defer_check(const raocp_ctx* c) {
-    if (c->dyn3 && c->sh_S == 0) return !(c->comm || c->sh_R != 1 || fuse_check(c) || c->no_defer_check || c->N < 1);
-    if (c->comm || c->sh_R != 1 || fuse_check(c) || c->dyn2 || c->cut <= 0 || c->tiers.empty() || c->no_defer_check)
+    if (c->dr && c->sh_S == 0) return !(c->comm || c->sh_R != 1 || c->no_defer_check);
+    if (c->dyn3 && c->sh_S == 0) return !(c->comm || c->sh_R != 1 || c->no_defer_check || c->N < 1);
+    if (c->comm || c->sh_R != 1 || c->dyn2 || c->cut <= 0 || c->tiers.empty() || c->no_defer_check)
         return false;
     return c->tiers.back().nsub > 0;
 }
@@ -1059,15 +1195,14 @@ int enqueue_cp_iteration(raocp_ctx* c, int it) {
     const bool defer = defer_check(c);
     const raocp::ChkArg ck{c->ctl, c->hist, c->redpart, c->cp_rows, 1};
     launch_dynamics(c, c->bufs, 1, c->ctl, 0, defer && it > 0 ? &ck : nullptr);
-    const bool fuse = !c->cp3 && fuse_check(c);
     if (c->cp3) {
         launch_cp3(c);
     } else {
         launch_cpd(c);
-        launch_cpp(c, fuse);
+        launch_cpp(c);
     }
     c->bufs = keep;
-    if (!fuse && !defer) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
+    if (!defer) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
     return RAOCP_OK;
 }
 // the kernel the default selection launches for op (raocp_op_bench numbering: 0 L, 1 L^T,
@@ -1106,17 +1241,15 @@ std::string kernel_name(const raocp_ctx* c, int op) {
                 terms.push_back({k, 1});
             };
             auto b = [](bool v) { return std::string(v ? "true" : "false"); };
-            if (c->dyn3) {  // one backward and one forward launch per nonleaf stage
+            if (c->dr && c->sh_S == 0) {
+                return std::string(raocp::dr_name_up(c->nx, c->nu)) + " x1 + " + raocp::dr_name_down(c->nx, c->nu) + " x1";
+            } else if (c->dyn3) {  // one backward and one forward launch per nonleaf stage
                 for (int t = 0; t < c->N; ++t) add("k_dy3_back<" + T + ", " + nn + ">");
                 for (int t = 0; t < c->N; ++t) add("k_dy3_fwd<" + T + ", " + nn + ">");
             } else if (c->dyn2) {
                 return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
-            } else if (c->cut > 0 && c->dyn_one && c->sh_S == 0) {
-                return "k_dyn_one<" + nn + ", " + b(c->one_fl) + "> x1";
             } else if (c->cut > 0 && c->dyn_split && c->sh_S == 0) {
                 return "k_dyn_up<" + nn + "> x1 + k_dyn_down<" + nn + ", " + b(c->f_lds_top) + "> x1";
-            } else if (c->cut > 0 && c->dyn_fuse && c->sh_S == 0) {
-                return "k_dyn_fuse<" + nn + ", true, " + b(c->fuse_st) + "> x1";
             } else if (c->cut > 0) {
                 for (int k = (int)c->tiers.size() - 1; k >= 0; --k)
                     add("k_dyn_bottom_back<" + nn + ", " + b(c->tiers[k].fold) + ">");
@@ -1803,6 +1936,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 }
                 sts.push_back(d);
             }
+            c->reg_ok = ok && C >= 2;
+            c->reg_C = C;
+            c->reg_st = sts;
             // default: fp32, and fp64 trees of >= 64k nodes (config 4: 118 vs 143 us for the
             // tiers; config 2 keeps the tiers, whose few launches win on small trees)
             c->dyn3 = ok && (c->f32 || n >= 65536);
@@ -1874,6 +2010,17 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 (rc = c->alloc(&c->Dd2, (size_t)m * nu)))
                 return bail(rc);
             c->dyn32 = c->f32;
+        }
+        // the regular-tree sweep (raocp_dynr.hip): fp64 regular trees of the compiled sizes
+        c->dr = false;
+        // (RAOCP_DYN3=1 / RAOCP_DYN2=1 keep the per-stage sweeps they ask for)
+        if (c->reg_ok && !c->f32 && !c->dyn3 && !c->dyn2 && raocp::dr_supported(nx, nu, c->reg_C) && N >= 2) {
+            bool want = true;
+            if (const char* e = getenv("RAOCP_DR")) want = atoi(e) != 0;
+            int n_cus = 0;
+            if (hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || n_cus <= 0)
+                n_cus = 256;
+            if (want && (rc = dr_setup(c, WT, SKP, RG, SNU, KM, F, SKF, n_cus))) return bail(rc);
         }
         std::vector<raocp::Rec> ninfo(m), cinfo(n);
         for (int i = 0; i < m; ++i) ninfo[i] = raocp::Rec{t->ch_start[i], t->nch[i], pr->i_k[i], t->stage[i]};
@@ -2116,26 +2263,19 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 }
             c->tiers.push_back(tp);
         }
-        // ---- the fused sweep (raocp_dynf.hip): the same tiers in one launch. Needs regular
-        // tiers of >= 2 subtrees per parent subtree, the top's F in LDS, and every workgroup
-        // of the grid co-resident (its waits are for running workgroups only).
+        // ---- the split sweep (raocp_dynf.hip): the same tiers in TWO launches, one workgroup
+        // per subtree of every tier plus the top, for regular tiers of >= 2 subtrees per parent
+        // subtree with the top's F in LDS (RAOCP_DYN_SPLIT=0 keeps the tier launches). Its
+        // waits are for workgroups of the same launch, so it runs only where the whole grid is
+        // co-resident (the occupancy query): no wait then depends on the dispatch order.
         {
-            c->dyn_fuse = false;
+            c->dyn_split = false;
             bool fz = c->cut > 0 && !c->tiers.empty() && c->tiers.size() <= (size_t)raocp::kFuseTiers && c->f_lds_top;
-            // The same plan serves the split sweep (k_dyn_up / k_dyn_down, two launches, the
-            // default where it applies; RAOCP_DYN_SPLIT=0 keeps the tier launches) and the
-            // fused one (opt-in RAOCP_DYN_FUSE=1: measured 49-56 us per projection at config 2
-            // against the tier launches' 51.5).
-            const char* fe = getenv("RAOCP_DYN_FUSE");
-            const bool want_fuse = fe && atoi(fe) != 0;
             bool split = true;
             if (const char* e = getenv("RAOCP_DYN_SPLIT")) split = atoi(e) != 0;
-            c->dyn_split = false;
-            size_t up = 0, down = 0, one = 0;  // the split sweeps' LDS (doubles)
+            size_t up = 0, down = 0;  // doubles
             raocp::FuseArg& fa = c->fuse;
             memset(&fa, 0, sizeof(fa));
-            // doubles: XD rows | S1 (the deepest tier) | S2 (the tiers above, the top)
-            size_t xd = 0, s1 = 0, s2 = fz ? c->lds_top / 8 : 0;
             for (size_t k = 0; fz && k < c->tiers.size(); ++k) {
                 const auto& tp = c->tiers[k];
                 const int L = tp.s1 - tp.s0;
@@ -2165,19 +2305,14 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 ft.fm = tp.fm;
                 ft.fold = tp.fold;
                 ft.nnl = (int)nnl;
-                ft.oXD = (int)xd;
                 ft.ngroups = above;
                 ft.ta = tp.ta;
                 ft.ta.boff = 0;
-                xd += raocp::rup((int)(nnl * KF), 2);
                 const size_t back = (tp.fold ? (size_t)(p1 - p0) * W1 : c->nkind * W1) + (c1 - c0) * RG1 + nall * KP +
                                     nnl * NUP + (tp.fold ? 0 : raocp::rup(tp.maxch * PS, 2)) + recs(nnl + nall - 1);
                 const size_t fwd = (c1 - c0) * KM1 + npl * F1 + recs(nnl + nall - 1);
-                size_t& reg = k + 1 == c->tiers.size() ? s1 : s2;
-                reg = std::max(reg, std::max(back, fwd));
                 up = std::max(up, back);
                 down = std::max(down, (size_t)raocp::rup((int)(nnl * KF), 2) + fwd);
-                one = std::max(one, (size_t)raocp::rup((int)(nnl * KF), 2) + std::max(back, fwd));
             }
             if (fz) {  // the top's backward (k_dyn_up) and forward (k_dyn_down) layouts
                 const size_t T = c->stage_ptr[c->cut], nb = stage_n(c->cut);
@@ -2189,72 +2324,24 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 c->lds_down = 8 * down;
                 split = split && c->lds_up <= kLds && c->lds_down <= kLds;
             }
-            const bool elig = fz;
-            if (fz) {
+            if (fz && split) {
                 fa.K = (int)c->tiers.size();
-                fa.nXD = (int)xd;
-                fa.oS1 = (int)xd;
-                // two regions (prefetching, raocp_dynf.hip) when they fit, else one shared
-                bool two = 8 * (xd + s1 + s2) <= kLds;
-                if (const char* e = getenv("RAOCP_FUSE_PREFETCH")) two = two && atoi(e) != 0;
-                fa.oS2 = two ? (int)(xd + s1) : fa.oS1;
-                c->lds_fuse = 8 * (two ? xd + s1 + s2 : xd + std::max(s1, s2));
-                fz = c->lds_fuse <= kLds;
-                // the static layout where the sizes have one and the regions fit it
-                int fx = 0, fa_ = 0, fb = 0;
-                dispatch(nx, nu, FuseStatOf{}, &fx, &fa_, &fb);
-                c->fuse_st = two && fa_ > 0 && xd <= (size_t)fx && s1 <= (size_t)fa_ && s2 <= (size_t)fb;
-                if (const char* e = getenv("RAOCP_FUSE_STATIC")) c->fuse_st = c->fuse_st && atoi(e) != 0;
-                if (c->fuse_st) {
-                    fa.oS1 = fa.oS2 = 0;
-                    c->lds_fuse = 0;
-                    fz = true;
-                }
-            }
-            if (elig && !want_fuse) {  // the split sweep (or the tier launches)
-                c->dyn_split = split;
-                fz = false;
-                // ... in one launch when the whole grid is co-resident: the top's F rows in
-                // LDS if that keeps it so, else read from L2
-                const char* e1 = getenv("RAOCP_DYN_ONE");  // opt-in (RAOCP_DYN_ONE=1), DESIGN.md 4.2
-                const bool on1 = split && e1 && atoi(e1) != 0;
-                const long grid1 = [&] {
-                    long g = 2;  // the top and the deferred stopping test
-                    for (const auto& tp : c->tiers) g += tp.nsub;
-                    return g;
-                }();
-                const size_t T = c->stage_ptr[c->cut], nb = stage_n(c->cut);
-                const int c1 = cp[c->cut], p1 = pp[c1];
-                for (int fl = 1; on1 && fl >= 0 && !c->dyn_one; --fl) {
-                    if (fl && !c->f_lds_top) continue;
-                    const size_t top = (c->fold_top ? (size_t)p1 * W1 : c->nkind * W1) + c1 * RG1 + c1 * KM1 +
-                                       (fl ? (size_t)p1 * F1 : 0) + T * KP + nb * KP + T * NUP + T * KF +
-                                       (c->fold_top ? 0 : raocp::rup(c->maxch_top * PS, 2)) + recs(T + T + nb - 1);
-                    const size_t lds = 8 * std::max(one, top);
-                    if (lds > kLds) continue;
-                    int per_cu = 0;
-                    dispatch(nx, nu, OneOcc{}, c, fl != 0, lds, &per_cu);
-                    if (per_cu > 0 && grid1 <= (long)n_cus * per_cu) {
-                        c->dyn_one = true;
-                        c->one_fl = fl != 0;
-                        c->lds_one = lds;
-                    }
-                }
-            }
-            if (fz) {
-                int per_cu = 0;
-                dispatch(nx, nu, FuseOcc{}, c, &per_cu);
-                fz = per_cu > 0 && (long)c->tiers.back().nsub <= (long)n_cus * per_cu;
+                long grid = 2;  // the top and the deferred stopping test's workgroup
+                for (const auto& tp : c->tiers) grid += tp.nsub;
+                int pu = 0, pd = 0;
+                dispatch(nx, nu, SplitOcc{}, c, &pu, &pd);
+                c->dyn_split = pu > 0 && pd > 0 && grid <= (long)n_cus * std::min(pu, pd);
                 if (getenv("RAOCP_DYN_VERBOSE"))
-                    fprintf(stderr, "[raocp] fused sweep: %d tiers, LDS %zu B (%s), %d workgroups, %d per CU x %d CUs%s\n",
-                            fa.K, c->lds_fuse, c->fuse_st ? "static" : (fa.oS2 != fa.oS1 ? "two regions" : "one region"), c->tiers.back().nsub, per_cu, n_cus, fz ? "" : " (not co-resident: tier launches)");
+                    fprintf(stderr, "[raocp] split sweep: %d tiers, %ld workgroups, %d / %d per CU x %d CUs%s\n", fa.K, grid, pu,
+                            pd, n_cus, c->dyn_split ? "" : " (not co-resident: tier launches)");
             }
-            if (fz || c->dyn_split) {
+            if (c->dyn_split) {
                 size_t words = 2;
                 for (int k = 0; k < fa.K; ++k) words += 2 * (size_t)fa.t[k].ngroups;
                 if ((rc = c->alloc(&c->fuse_sync, words))) return bail(rc);
                 if (hipMemset(c->fuse_sync, 0, words * sizeof(unsigned)) != hipSuccess)
                     return bail(fail(RAOCP_ERR_HIP, "hipMemset failed"));
+                c->fuse_words = words;
                 fa.epoch = c->fuse_sync;
                 fa.err = (int*)(c->fuse_sync + 1);
                 unsigned* w = c->fuse_sync + 2;
@@ -2274,10 +2361,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 if (const char* e = getenv("RAOCP_FUSE_TIMEOUT_MS")) ms = std::max(1, atoi(e));
                 fa.timeout = ms * 100000LL;  // 100 MHz ticks
             }
-            c->dyn_fuse = fz;
-            if (getenv("RAOCP_DYN_VERBOSE") && c->dyn_split)
-                fprintf(stderr, "[raocp] split sweep: %d tiers, LDS %zu / %zu B; one launch: %s (LDS %zu B, top F %s)\n", fa.K,
-                        c->lds_up, c->lds_down, c->dyn_one ? "yes" : "no", c->lds_one, c->one_fl ? "LDS" : "L2");
         }
         if (getenv("RAOCP_DYN_VERBOSE")) {
             fprintf(stderr, "[raocp] dynamics plan: top stages [0,%d) lds %zu F%s%s", c->cut, c->lds_top,
@@ -2486,16 +2569,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     c->cur_z = c->Z[0];
     c->cur_e = c->E[0];
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
-    c->dev.dyn_regtab = 0;  // RAOCP_DYN_REGTAB=1: dynamics tables by vector loads instead of LDS-DMA
-    if (const char* e = getenv("RAOCP_DYN_REGTAB")) c->dev.dyn_regtab = atoi(e) != 0;
     c->dev.dyn_rot = 1;  // RAOCP_DYN_ROT=0: every staged range starts at wave 0
     if (const char* e = getenv("RAOCP_DYN_ROT")) c->dev.dyn_rot = atoi(e) != 0;
 
-    // RAOCP_CP_PACK=1: the CP / L^T kernels pack their staged regions into shared LDS-DMA
-    // instructions (StgTable). Measured neutral at config 2 and 4-6 % slower at configs 3-5
-    // (the slot map costs two more barriers per block), so one pass per region is the default.
-    c->dev.cp_pack = 0;
-    if (const char* e = getenv("RAOCP_CP_PACK")) c->dev.cp_pack = atoi(e) != 0;
     {
         // L by streaming wave tasks (raocp_ell3.hip): compile-time sizes, and one sqrtQ / sqrtR
         // table over all children and one sqrtPf over all leaves (the waves keep them in registers)
@@ -2558,6 +2634,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             // leaf-parent tiles first (heavier), then the rest
             const long tiles = cp3_tasks(c->cp3_ta, {{c->cp3_mL, m}, {0, c->cp3_mL}}, m, c->cp3_split ? n : m,
                                          c->cp3_split, c->cp3_mL);
+            if (tiles < 0) return bail(fail(RAOCP_ERR_ARG, "k_cp3 task list exceeds its parent-range slots"));
             c->cp3_grid = cp3_grid_of(tiles);
             if (const char* e = getenv("RAOCP_CP3_GRID")) c->cp3_grid = std::max(1, atoi(e));
             if (c->cp3_grid > c->red_rows) {
@@ -2572,12 +2649,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels
     if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = atoi(e);
-    c->dev.regstage = 0;  // RAOCP_REGSTAGE=1: k_ell's gather by vector loads (measured slower)
-    if (const char* e = getenv("RAOCP_REGSTAGE")) c->dev.regstage = atoi(e) != 0;
-    if ((rc = c->alloc(&c->ticket, 64))) return bail(rc);
-    if (hipMemset(c->ticket, 0, 64 * sizeof(unsigned)) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "memset"));
-    if (const char* e = getenv("RAOCP_FUSE_CHECK")) c->no_fuse_check = atoi(e) == 0;
     if (const char* e = getenv("RAOCP_DEFER_CHECK")) c->no_defer_check = atoi(e) == 0;
+    c->drp.zpage = c->dev.zpage;
+    c->drp.x0 = c->x0;
     *out = c;
     return RAOCP_OK;
 }
@@ -3003,6 +3077,7 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     HIPCHK(hipEventSynchronize(e1));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
     HIPCHK(hipMemcpy(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
+    if (int fe = fuse_err(c)) return fe;  // a timed-out hand-off skipped its arithmetic
     if (c->h_ctl->final_k != iters - 1) return fail(RAOCP_ERR_STATE, "bench did not run the requested iterations");
     c->cur_z = c->Z[iters % 3];
     c->cur_e = c->E[iters % 2];
@@ -3130,6 +3205,9 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
         c->cp3_ta.xlo = c->own_first;
         c->cp3_ta.xhi = c->own_first + c->own_cnt;
         const long tb = cp3_tasks(c->cp3_tb, {{c->stage_ptr[S - 1], c->stage_ptr[S]}}, 0, 0, c->cp3_split, c->cp3_mL);
+        if (ta < 0 || tb < 0)
+            return fail(RAOCP_ERR_ARG, "shard's k_cp3 task list exceeds its " + std::to_string(raocp::kCp3MaxR) +
+                                           " parent-range slots (too many stages below the cut)");
         c->cp3_tb.ext2 = 1;
         c->cp3_grid = cp3_grid_of(ta);
         c->cp3_gridb = cp3_grid_of(tb);

@@ -55,7 +55,7 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
     glbp<T> eo = (glbp<T>)bf.e1;               // eta+
     glbp<T> xi2 = (glbp<T>)xi2_;
     const int bid = blockIdx.x;
-    Stg st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
+    Stg st{(ldsd*)smem_, 0, stg_table()};
     double m2 = 0.0, m5 = 0.0;
     auto finish = [&](int e, T dv, T v, T pv, T b) {
         const T ep = alpha * (v - pv);
@@ -310,44 +310,9 @@ __global__ void __launch_bounds__(kBlock) k_cpd(Dev p, Ctl* __restrict__ ctl, Bu
 //   delta0 = delta1 + L^T(d - eta+)
 // Buffers: p = z0, z+ = z1, out = z2, d = e0, eta+ = e1.
 // ==============================================================================
-// block-wide max of non-negative doubles, returned in every thread
-__device__ __forceinline__ double block_max_val(double v, double* s_red) {
-    for (int off = 32; off > 0; off >>= 1) v = nmax(v, __shfl_xor(v, off, 64));
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) s_red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    double b = s_red[0];
-    for (int i = 1; i < (int)(blockDim.x >> 6); ++i) b = nmax(b, s_red[i]);
-    return b;
-}
-
-// k_cp_check run by the k_cpp block that drew the last ticket: every block's maxima row
-// (this launch's by sc1 stores, k_cpd's from the previous launch) -> history row k,
-// stopping test (solver.py:137-161); re-arms the ticket for the next iteration
-__device__ void cp_check_last(Ctl* ctl, double* hist, const double* part, int rows, unsigned* ticket, double* s_red) {
-    double m[6] = {0, 0, 0, 0, 0, 0};
-    for (int r = threadIdx.x; r < rows; r += blockDim.x)
-        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], ld_sc1(part + (size_t)r * 6 + q));
-    double M[6];
-    _Pragma("unroll") for (int q = 0; q < 6; ++q) M[q] = block_max_val(m[q], s_red);
-    if (threadIdx.x != 0) return;
-    const int k = ctl->k;
-    for (int q = 0; q < 6; ++q) hist[(size_t)k * 6 + q] = M[q];
-    const double err = nmax(nmax(M[0], M[1]), M[2]);
-    if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
-        ctl->done = 1;
-        ctl->final_k = k;
-    } else {
-        ctl->k = k + 1;
-    }
-    __hip_atomic_store((gu32*)ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ticket != nullptr: the stopping test is fused (the launch's last block runs k_cp_check)
 template <class T, int NXc, int NUc>
 __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bufs bf, const double* __restrict__ xi2_,
-                                                double* __restrict__ part, int nbF, double* __restrict__ hist,
-                                                unsigned* __restrict__ ticket) {
+                                                double* __restrict__ part, int nbF) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ T s_x[kBlock];
     __shared__ double s_red[4][kBlock / 64];
@@ -361,7 +326,7 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
     cglbp<T> dA = (cglbp<T>)bf.e1;   // eta+
     cglbp<T> xg = (cglbp<T>)xi2_;
     const int bid = blockIdx.x;
-    Stg st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
+    Stg st{(ldsd*)smem_, 0, stg_table()};
     double m0 = 0.0, m1 = 0.0, m3 = 0.0, m4 = 0.0;
     stamp(p, 0);
     // residual terms of one primal entry: pp = p, zz = z+, w = L^T(d - eta+), lc = L^T xi2
@@ -610,29 +575,9 @@ __global__ void __launch_bounds__(kBlock) k_cpp(Dev p, Ctl* __restrict__ ctl, Bu
         }
     }
     double* prow = part + (size_t)bid * 6;
-    if (!ticket) {
-        block_max_store(m0, prow + 0, s_red[0]);
-        block_max_store(m1, prow + 1, s_red[1]);
-        block_max_store(m3, prow + 3, s_red[2]);
-        block_max_store(m4, prow + 4, s_red[3]);
-        stamp(p, 10);
-        return;
-    }
-    // fused stopping test: this block's row goes out write-through (sc1), drained, then one
-    // ticket per block (agent-scope atomic); the block holding the last ticket reduces
-    const double v0 = block_max_val(m0, s_red[0]), v1 = block_max_val(m1, s_red[1]);
-    const double v3 = block_max_val(m3, s_red[2]), v4 = block_max_val(m4, s_red[3]);
-    __shared__ int s_last;
-    if (threadIdx.x == 0) {
-        st_sc1(prow + 0, v0);
-        st_sc1(prow + 1, v1);
-        st_sc1(prow + 3, v3);
-        st_sc1(prow + 4, v4);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned t = __hip_atomic_fetch_add((gu32*)ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = t == gridDim.x - 1;
-    }
-    __syncthreads();
+    block_max_store(m0, prow + 0, s_red[0]);
+    block_max_store(m1, prow + 1, s_red[1]);
+    block_max_store(m3, prow + 3, s_red[2]);
+    block_max_store(m4, prow + 4, s_red[3]);
     stamp(p, 10);
-    if (s_last) cp_check_last(ctl, hist, part, gridDim.x, ticket, s_red[0]);
 }

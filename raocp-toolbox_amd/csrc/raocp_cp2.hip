@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
     const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int lo = lane & 15, h = lane >> 4;
     const crec4* tab = (const crec4*)p.cp2_tab;
-    StgB st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
+    StgB st{(ldsd*)smem_, 0, stg_table()};
     double m2 = 0.0, m5 = 0.0;
     T alpha = T(0), ra = T(0);  // alpha and 1 / alpha (products instead of divisions: 1 ulp)
     auto finish = [&](int e, T dv, T v, T pv, T b) {
@@ -540,7 +540,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
     const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int lo = lane & 15, h = lane >> 4;
     const crec4* tab = (const crec4*)p.cp2_tab;
-    StgB st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
+    StgB st{(ldsd*)smem_, 0, stg_table()};
     double m0 = 0.0, m1 = 0.0, m3 = 0.0, m4 = 0.0;
     T alpha = T(0), ra = T(0);
     // residual terms of one primal entry: pp = p, zz = z+, w = L^T(d - eta+), lc = L^T xi2

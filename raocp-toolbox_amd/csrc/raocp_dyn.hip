@@ -373,10 +373,6 @@ __device__ __forceinline__ void fwd_phase(const Dev& p, const TB& tb, const INF&
     else fwd_phase_ks<1, NXc, NUc, XOUT, SCX>(p, tb, inf, b, e, cb, ce, xd, z, xdo, tid, nthr);
 }
 
-__device__ __forceinline__ glbd* pick3(const Bufs& bf, int k) {
-    const int w = k % 3;
-    return (glbd*)(w == 0 ? bf.z0 : (w == 1 ? bf.z1 : bf.z2));
-}
 
 // the iterate the sweep projects: buffers arrive rotated for the iteration, so no ctl read
 __device__ __forceinline__ glbd* dyn_z(const Bufs& bf, int zsel, const Ctl*) { return pick3(bf, zsel); }
@@ -504,7 +500,7 @@ struct Prologue {
     int lo[kMaxLevels + 1], hi[kMaxLevels + 1], off[kMaxLevels + 1];
     int sp[kMaxTopStages + 2];  // stage_ptr[0 .. s+1] (top)
     unsigned long long ts[64];  // diagnostics (p.stamps != nullptr)
-    int nts;                    // next stamp slot (k_dyn_fuse)
+    int nts;                    // next stamp slot (the split sweep)
 };
 
 // diagnostics: thread 0 records the 100 MHz clock in LDS; flushed at the end of the kernel
@@ -548,47 +544,6 @@ __device__ __forceinline__ void dma_rows(ldsd* dst, int w, const double* src, in
         return c < cc ? src + (size_t)r * sstride + 2 * c : zp;
     });
 }
-// Matrix tables by vector loads instead of LDS-DMA (Dev::dyn_regtab): up to four regions
-// (n[k] doubles, even, 16-B aligned) copied in one pass — every thread issues all its
-// 16-B loads first, then writes them to LDS, so the regions cost one memory round trip
-// and no LDS-DMA issue slots (the tables are the same for every workgroup of a launch).
-struct TabCopy {
-    // four fixed slots (dynamically indexed arrays would live in scratch). Region bases are
-    // pre-shifted by the region's first chunk, so chunk c of the concatenation is
-    // base + 2 c for the region holding it.
-    ldsd *d0 = nullptr, *d1 = nullptr, *d2 = nullptr, *d3 = nullptr;
-    const glbd *s0 = nullptr, *s1 = nullptr, *s2 = nullptr, *s3 = nullptr;
-    int e0 = 0, e1 = 0, e2 = 0, e3 = 0;  // cumulative chunk ends
-    int cnt = 0;
-    __device__ __forceinline__ void add(ldsd* d, const double* src, int nd) {
-        const int beg = e3, end = e3 + (nd >> 1);
-        const glbd* sg = (const glbd*)src - 2 * beg;
-        ldsd* dg = d - 2 * beg;
-        if (cnt == 0) { d0 = dg; s0 = sg; e0 = e1 = e2 = e3 = end; }
-        else if (cnt == 1) { d1 = dg; s1 = sg; e1 = e2 = e3 = end; }
-        else if (cnt == 2) { d2 = dg; s2 = sg; e2 = e3 = end; }
-        else { d3 = dg; s3 = sg; e3 = end; }
-        ++cnt;
-    }
-    __device__ __forceinline__ void run() const {
-        constexpr int U = 8;
-        const int tid = threadIdx.x, nthr = blockDim.x;
-        for (int base = 0; base < e3; base += U * nthr) {
-            d2v v[U];
-            _Pragma("unroll") for (int u = 0; u < U; ++u) {
-                const int c = base + u * nthr + tid;
-                const glbd* sp = c < e0 ? s0 : (c < e1 ? s1 : (c < e2 ? s2 : s3));
-                if (c < e3) v[u] = ld2(sp + 2 * c);
-            }
-            _Pragma("unroll") for (int u = 0; u < U; ++u) {
-                const int c = base + u * nthr + tid;
-                ldsd* dp = c < e0 ? d0 : (c < e1 ? d1 : (c < e2 ? d2 : d3));
-                if (c < e3) *(lds2*)(dp + 2 * c) = v[u];
-            }
-        }
-    }
-};
-
 __device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // The CP stop flag, read by a kernel AFTER it has issued its prologue loads: the flag was
 // written by the previous launch (another XCD's L2), so the load costs a memory round trip,
@@ -717,10 +672,8 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
     const double* srcW = FOLD ? p.dWT + (size_t)p0 * ts.W1 : p.dW;
     const double* srcRG = p.dRG + (size_t)c0 * ts.RG1;
     int rot = p.dyn_rot ? 0 : -1;
-    if (!p.dyn_regtab) {
-        dma_r(smem + oW, srcW, nW, rot);
-        dma_r(smem + oRG, srcRG, (c1 - c0) * ts.RG1, rot);
-    }
+    dma_r(smem + oW, srcW, nW, rot);
+    dma_r(smem + oRG, srcRG, (c1 - c0) * ts.RG1, rot);
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
     if (!ta.regular) lds_sync();
@@ -751,12 +704,6 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
         if (l > 0) dma_r(CHd + 2 * (lv.off - 1), (const double*)(p.cinfo + lv.lo), 2 * cnt, rot);
     }
     if (!FOLD) zero_fill(PB, maxch * g.PS, tid, nthr);
-    if (p.dyn_regtab) {
-        TabCopy tc;
-        tc.add(smem + oW, srcW, nW);
-        tc.add(smem + oRG, srcRG, (c1 - c0) * ts.RG1);
-        tc.run();
-    }
     const int done = ctl_done(ctl);
     dma_wait();
     lds_sync();
@@ -829,10 +776,8 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
     }
     const int oKM = 0, oF = oKM + (c1 - c0) * ts.KM1, oXD = oF + (FL ? npl * ts.F1 : 0);
     int rot = p.dyn_rot ? 0 : -1;
-    if (!p.dyn_regtab) {
-        dma_r(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1, rot);
-        if (FM == 1) dma_r(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1, rot);
-    }
+    dma_r(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1, rot);
+    if (FM == 1) dma_r(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1, rot);
     if (FM == 2) dma_r(smem + oF, p.dF + (size_t)ta.pl0[0] * ts.F1, (ta.pl0[1] - ta.pl0[0]) * ts.F1, rot);
     tier_levels(pl, ta, sub_lv, L);
     glbd* z = dyn_z(bf, zsel, ctl);
@@ -876,12 +821,6 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
         dma_r(NLd + 2 * lv.off, (const double*)(p.ninfo + lv.lo), 2 * cnt, rot);
         const int cc = lc.hi - lc.lo;
         dma_r(CHd + 2 * (lc.off - 1), (const double*)(p.cinfo + lc.lo), 2 * cc, rot);
-    }
-    if (p.dyn_regtab) {
-        TabCopy tc;
-        tc.add(smem + oKM, p.dKM + (size_t)c0 * ts.KM1, (c1 - c0) * ts.KM1);
-        if (FM == 1) tc.add(smem + oF, p.dF + (size_t)p0 * ts.F1, (p1 - p0) * ts.F1);
-        tc.run();
     }
     const int done = ctl_done(ctl);
     dma_wait();
@@ -939,12 +878,10 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl
     const int oXQ = oF + (FL ? p1 * ts.F1 : 0), oQB = oXQ + T * g.KP, oU = oQB + nb * g.KP, oXD = oU + T * g.NUP;
     const int oP = oXD + T * g.KF, oNL = oP + (FOLD ? 0 : rup(maxch * g.PS, 2)), oCH = oNL + 2 * T;
     int rot = p.dyn_rot ? 0 : -1;
-    if (!p.dyn_regtab) {
-        dma_r(smem + oW, FOLD ? p.dWT : p.dW, nW, rot);
-        dma_r(smem + oRG, p.dRG, c1 * ts.RG1, rot);
-        dma_r(smem + oKM, p.dKM, c1 * ts.KM1, rot);
-        if (FL) dma_r(smem + oF, p.dF, p1 * ts.F1, rot);
-    }
+    dma_r(smem + oW, FOLD ? p.dWT : p.dW, nW, rot);
+    dma_r(smem + oRG, p.dRG, c1 * ts.RG1, rot);
+    dma_r(smem + oKM, p.dKM, c1 * ts.KM1, rot);
+    if (FL) dma_r(smem + oF, p.dF, p1 * ts.F1, rot);
     dma_r(smem + oNL, (const double*)p.ninfo, 2 * T, rot);
     dma_r(smem + oCH, (const double*)(p.cinfo + 1), 2 * (T + nb - 1), rot);
     if (tid <= s + 1) pl.sp[tid] = p.stage_ptr[tid];
@@ -958,14 +895,6 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl
     rows_in_r(dmaok, smem + oU, g.NUP, (const double*)z + p.U0, g.nu, g.nu, T, p.zpage, tid, nthr, rot);
     zero_fill(smem + oXD, T * g.KF, tid, nthr);
     if (!FOLD) zero_fill(smem + oP, maxch * g.PS, tid, nthr);
-    if (p.dyn_regtab) {
-        TabCopy tc;
-        tc.add(smem + oW, FOLD ? p.dWT : p.dW, nW);
-        tc.add(smem + oRG, p.dRG, c1 * ts.RG1);
-        tc.add(smem + oKM, p.dKM, c1 * ts.KM1);
-        if (FL) tc.add(smem + oF, p.dF, p1 * ts.F1);
-        tc.run();
-    }
     const int done = ctl_done(ctl);
     dma_wait();
     lds_sync();

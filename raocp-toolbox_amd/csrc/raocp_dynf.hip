@@ -1,42 +1,22 @@
-// raocp_dynf.hip — the tiered dynamics projection (raocp_dyn.hip) in ONE launch.
-// Included by raocp_kernels.hip after raocp_dyn.hip (inside namespace raocp).
+// raocp_dynf.hip — the tiered dynamics projection (raocp_dyn.hip) in TWO launches: the
+// split sweep k_dyn_up / k_dyn_down. Included by raocp_kernels.hip after raocp_dyn.hip
+// (inside namespace raocp). The fallback of trees the regular-tree sweep (raocp_dynr.hip)
+// does not take but whose tier plan is regular (every subtree of a tier the same shape, ids
+// consecutive): e.g. Markov trees with uniform branching (BASELINE configs[2]).
 //
 // Same recursion and level routines as the tier kernels (cache.py:259-288; header of
-// raocp_dyn.hip), same cut into the top (stages [0, s)) and tiers t[0] .. t[K-1] below it
-// (t[K-1] the deepest, whose boundary is the leaves). The tier launches cost ≈ 8 µs each
-// at config 2 before their first level runs (launch gap, prologue, staging: five launches
-// per projection, profiles/r03_v3/stamps_c2.log); here one workgroup per subtree of the
-// deepest tier runs the whole projection:
-//
-//   backward: a workgroup sweeps its deepest-tier subtree, publishes the root's q row and
-//     takes a ticket on its parent subtree (the tier above). The workgroup that draws the
-//     group's last ticket sweeps the parent subtree (its children's q rows are published),
-//     and so on up; the last ticket of tier t[0] runs the top, backward and forward.
-//   forward: every workgroup that stopped at tier k waits for its parent subtree's forward
-//     (a flag), then sweeps its tier-k subtree forward and releases the flags of the tier
-//     below, down to its deepest-tier subtree. The workgroups that climbed do the same
-//     from the highest tier they reached.
-//
-// Nothing waits for a workgroup that has not started: a ticket never waits, and a flag is
-// released by the workgroup that drew the last ticket below it, which is running. The
-// host launches the fused sweep only when every workgroup of the grid is co-resident
-// (hipOccupancyMaxActiveBlocksPerMultiprocessor), and every wait is bounded
-// (FuseArg::timeout): a timed-out workgroup sets the error word and leaves.
+// raocp_dyn.hip), same cut into the top (stages [0, s)) and tiers t[0] .. t[K-1] below it,
+// one workgroup per subtree of every tier plus one for the top, each with ONE role fixed by
+// its block index, so every workgroup stages its tables and vectors at its start and only
+// the dependent rows (the children's q, the parent's x) wait for a hand-off (below).
 //
 // Hand-offs across workgroups (MI355X: per-XCD L2s are not coherent): the roots' q rows
 // and the boundary x rows are stored write-through (st_sc1) and read with ld_sc1; the
-// storing waves drain (vmcnt 0), a barrier, then one lane takes the ticket / stores the
-// flag. Everything else a workgroup reads it wrote itself: d_i stays in LDS between the
-// backward and the forward sweep of a subtree (the rows XD_k, one region per tier, never
-// go through global memory), the tables and vectors are restaged per tier into a shared
-// scratch region.
-//
-// Tickets count up from 0 and are reset by the workgroup that runs the top (every ticket
-// of the launch has been drawn by then); flags carry the launch's tag (epoch + 1), and the
-// top stores the new epoch, so no host reset runs between launches. A launch that starts
-// with ctl->done set runs the protocol without the arithmetic (the next iterations' CP
-// kernels exit on the flag; the deferred stopping test, run by one waiting workgroup,
-// may set it during the launch: the projected buffer is then never read).
+// storing waves drain (vmcnt 0), a barrier, then one lane arrives / stores the flag. The
+// host launches the sweep only where the whole grid is co-resident
+// (hipOccupancyMaxActiveBlocksPerMultiprocessor), so no wait depends on the dispatch order;
+// every wait is bounded (FuseArg::timeout) and a timed-out workgroup sets the error word,
+// which every workgroup of a later launch reads at its start and then leaves at once.
 
 constexpr int kFuseTiers = 4;
 // workgroup size of the fused sweep: at most 512 lanes leaves 256 VGPRs per lane (the tier,
@@ -51,26 +31,10 @@ struct FuseTier {
     int fm;            // F rows in the forward sweep: 1 every pair of the tier, 2 per level
     int fold;          // one-phase backward levels (per-pair WT tables, back_fold)
     int nnl;           // nonleaf nodes of one subtree (levels 0 .. L-1)
-    int oXD;           // this tier's persistent XD rows (doubles from the LDS base)
     int ngroups;       // subtrees of the tier above (tickets / flags)
     TierArg ta;        // regular tier: level sizes and first nodes
     unsigned* cnt;     // [ngroups] tickets
     unsigned* flag;    // [ngroups] forward released by the tier above
-};
-
-// Static LDS layout (k_dyn_fuse<..., ST = true>, config 2's sizes): the XD rows, the deepest
-// tier's region S1 and the upper region S2 as three __shared__ arrays. The compiler tracks
-// LDS-DMA copies per LDS object (alias scopes of the module's LDS variables), so the levels
-// reading S1 / XD do not wait for a prefetch into S2 in flight, and the other way round; in
-// one dynamic array every LDS read after a prefetch waits for it (measured: the deepest
-// tier's levels 4.6 -> 9.8 us with the tier above prefetched during them).
-template <int NX, int NU>
-struct FuseStat {
-    static constexpr int X = 0, A = 0, B = 0;  // doubles
-};
-template <>
-struct FuseStat<20, 8> {
-    static constexpr int X = 1024, A = 7168, B = 11264;  // 8 + 56 + 88 KB
 };
 
 struct FuseArg {
@@ -78,9 +42,6 @@ struct FuseArg {
     FuseTier t[kFuseTiers];
     int s, T, nb, c1, p1, maxch_top; // the top: stages [0, s), nodes [0, T), nb boundary roots
     int fold_top;                   // the top's backward levels in one phase
-    int oS1, oS2;                   // regions (doubles from the LDS base): the deepest tier, the
-                                    // tiers above and the top (oS2 == oS1: one shared region)
-    int nXD;                        // doubles of the persistent XD regions (zeroed at start)
     unsigned* epoch;
     int* err;                       // set to 1 by a workgroup whose wait timed out
     long long timeout;              // per wait, 100 MHz ticks
@@ -424,173 +385,14 @@ __device__ void fz_top_run(const Dev& p, glbd* z, const double* qbuf_, const dou
     }
 }
 
-// the top (stages [0, s), nodes [0, T)), backward then forward, as k_dyn_top: the boundary
-// q rows come from tier t[0]'s roots (ld_sc1), the boundary x rows are published
-template <int NXc, int NUc, bool FL>
-__device__ void fz_top(const Dev& p, glbd* z, const double* qbuf_, const double* x0_, const FuseArg& fa, ldsd* scr,
-                       Prologue& pl) {
-    fz_top_stage<NXc, NUc, FL>(p, z, fa, scr, pl, false);
-    fz_top_run<NXc, NUc, FL>(p, z, qbuf_, x0_, fa, scr, pl, nullptr);
-}
-
 // stores of this workgroup drained, then one lane publishes
 __device__ __forceinline__ void fz_drain() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 }
 
-template <int NXc, int NUc, bool FL, bool ST>
-__global__ void __launch_bounds__(kFuseBlock) k_dyn_fuse(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
-                                                         double* qbuf_, const double* x0_, FuseArg fa) {
-    extern __shared__ __attribute__((aligned(16))) double smem_[];
-    typedef FuseStat<NXc, NUc> FS;
-    __shared__ __attribute__((aligned(16))) double lx_[ST ? FS::X : 2];
-    __shared__ __attribute__((aligned(16))) double la_[ST ? FS::A : 2];
-    __shared__ __attribute__((aligned(16))) double lb_[ST ? FS::B : 2];
-    __shared__ Prologue pl;
-    __shared__ unsigned s_tk;
-    __shared__ int s_ok;
-    const int tid = threadIdx.x;
-    // regions: XB the XD rows; S1 the deepest tier (backward, then its forward prefetched as
-    // soon as it is free); S2 the tiers above and the top (the tier above the deepest
-    // prefetched while the deepest is swept, all but its boundary q rows). Dynamic layout:
-    // S2 == S1 when both do not fit.
-    ldsd* smem = (ldsd*)smem_;
-    ldsd* XB = ST ? (ldsd*)lx_ : smem;
-    ldsd* S1 = ST ? (ldsd*)la_ : smem + fa.oS1;
-    ldsd* S2 = ST ? (ldsd*)lb_ : smem + fa.oS2;
-    const bool two = ST || fa.oS2 != fa.oS1;
-    glbd* z = dyn_z(bf, zsel, ctl);
-    if (tid == 0) pl.nts = 0;  // diagnostics: stamps of this workgroup's path (fz_stamp)
-    fz_stamp(p, pl);
-    // this workgroup's subtree at tier k: blockIdx.x / (r of every tier below k)
-    auto sub_at = [&](int k) {
-        int b = blockIdx.x;
-        for (int j = fa.K - 1; j > k; --j) b /= fa.t[j].r;
-        return b;
-    };
-    const int D = fa.K - 1;  // the deepest tier
-    // the prologue copies are issued before the epoch and stop flag are read (their loads
-    // wait where the values are used)
-    fz_back_stage<NXc, NUc>(p, z, fa.t[D], blockIdx.x, true, S1);
-    const bool pre2 = two && fa.K >= 2;
-    zero_fill(XB, fa.nXD, tid, blockDim.x);  // XD rows: zero tails (the back sweeps write d, the forward x)
-    const unsigned tag = ld_u32_sc1(fa.epoch) + 1u;
-    const bool work = !ctl_done(ctl);
-    if (tid == 0) s_ok = 1;
-    int k = D, sub = blockIdx.x;
-    bool top = false;
-    // backward, up the tiers while this workgroup draws the last ticket of its group
-    for (;;) {
-        const FuseTier& tt = fa.t[k];
-        ldsd* R = k == D ? S1 : S2;
-        // prefetches overlapping the levels (static layout: the levels' LDS reads do not wait
-        // for them): the subtree of the tier above, all but its boundary q rows, while the
-        // deepest is swept; the deepest tier's forward tables while the tier above it is
-        // swept (S1 is free again). Each region's code path names its region statically.
-        if (work && k == D) {
-            fz_back_wait<NXc, NUc>(p, qbuf_, tt, sub, true, S1, pl);
-            if (pre2) fz_back_stage<NXc, NUc>(p, z, fa.t[D - 1], sub_at(D - 1), false, S2);
-            fz_back_levels<NXc, NUc>(p, qbuf_, tt, sub, true, XB + tt.oXD, S1, pl);
-        } else if (work) {
-            if (!(k == D - 1 && pre2)) fz_back_stage<NXc, NUc>(p, z, tt, sub, false, S2);
-            fz_back_wait<NXc, NUc>(p, qbuf_, tt, sub, false, S2, pl);
-            if (k == D - 1 && two) fz_fwd_stage<NXc, NUc>(p, fa.t[D], sub_at(D), S1);
-            fz_back_levels<NXc, NUc>(p, qbuf_, tt, sub, false, XB + tt.oXD, S2, pl);
-        }
-        fz_stamp(p, pl);
-        fz_drain();
-        const int grp = sub / tt.r;
-        if (tid == 0) s_tk = __hip_atomic_fetch_add(tt.cnt + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();
-        const unsigned old = s_tk;
-        fz_stamp(p, pl);
-        // this tier's forward tables: staged now where the region stays free until the forward
-        // (the waiting workgroups always; the deepest tier in S1 also on the way up)
-        const bool last = old + 1u == (unsigned)tt.r;
-        if (work && (!last || (k == D && two && fa.K == 1))) {
-            if (k == D) fz_fwd_stage<NXc, NUc>(p, tt, sub, S1);
-            else fz_fwd_stage<NXc, NUc>(p, tt, sub, S2);
-        }
-        if (!last) {
-            // the deferred stopping test: one waiting workgroup per launch (tt.r >= 2)
-            if (fa.ck.on && k == D && grp == 0 && old == 0u && tid < 64) cp_check_wave(fa.ck);
-            break;
-        }
-        if (k == 0) {
-            top = true;
-            break;
-        }
-        sub = grp;
-        --k;
-    }
-    if (top) {
-        if (work) fz_top<NXc, NUc, FL>(p, z, qbuf_, x0_, fa, S2, pl);
-        fz_stamp(p, pl);
-        // the forward tables of tier t[0] (S2 is free again; S1 holds the deepest tier's
-        // forward when the two differ): issued before the resets, the drain and the flag
-        if (work && (fa.K > 1 || !two)) fz_fwd_stage<NXc, NUc>(p, fa.t[0], sub_at(0), S2);
-        // every ticket of the launch has been drawn: reset them for the next launch
-        for (int kk = 0; kk < fa.K; ++kk)
-            for (int q = tid; q < fa.t[kk].ngroups; q += blockDim.x) st_u32_sc1(fa.t[kk].cnt + q, 0u);
-        fz_drain();
-        if (tid == 0) {
-            st_u32_sc1(fa.epoch, tag);
-            st_u32_sc1(fa.t[0].flag, tag);
-        }
-    } else {
-        // wait for the forward sweep of the parent subtree
-        if (tid == 0) {
-            const unsigned* f = fa.t[k].flag + sub_at(k) / fa.t[k].r;
-            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-            while (ld_u32_sc1(f) != tag) {
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > fa.timeout) {
-                    s_ok = 0;
-                    __hip_atomic_store(fa.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        __syncthreads();
-        if (!s_ok) return;
-        fz_stamp(p, pl);
-    }
-    // forward, down from tier k to the deepest
-    const int kw = k;  // where this workgroup stopped climbing (0 for the top's)
-    for (; k < fa.K; ++k) {
-        const FuseTier& tt = fa.t[k];
-        const bool deepest = k == D;
-        const int sk = sub_at(k);
-        if (work) {
-            // staged already: the tier it waited at, or t[0] on the top's workgroup (after
-            // the top); the deepest tier whenever S1 is its own region
-            const bool staged = (k == kw && (!top || fa.K > 1 || !two)) || (deepest && two);
-            if (deepest) {
-                if (!staged) fz_fwd_stage<NXc, NUc>(p, tt, sk, S1);
-                fz_fwd_run<NXc, NUc>(p, z, tt, sk, false, XB + tt.oXD, S1, pl);
-            } else {
-                if (!staged) fz_fwd_stage<NXc, NUc>(p, tt, sk, S2);
-                fz_fwd_run<NXc, NUc>(p, z, tt, sk, true, XB + tt.oXD, S2, pl);
-            }
-        }
-        fz_stamp(p, pl);
-        if (!deepest) {
-            fz_drain();
-            if (tid == 0) st_u32_sc1(fa.t[k + 1].flag + sk, tag);
-        }
-    }
-    // diagnostics: the top's workgroup (the critical path) to slots 0..63, workgroup 0 (a
-    // waiting one, unless it ran the top) to 64..127
-    if (p.stamps && tid == 0 && (top || blockIdx.x == 0))
-        for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(top ? 0 : 64) + q] = pl.ts[q];
-}
-
 // ==============================================================================
-// The split sweep (default where the fused plan applies): the same tiers in TWO launches,
-// one workgroup per subtree of every tier plus the top, each with ONE role fixed by its
-// block index, so every workgroup stages its tables and vectors at its start and only the
-// dependent rows (the children's q, the parent's x) wait for a hand-off:
+// The split sweep:
 //   k_dyn_up:   [deferred stopping test] [deepest subtrees] [tier D-1] .. [tier 0] [top]
 //               a tier-k workgroup waits until its r children subtrees have published
 //               their q rows (a counter of arrivals), sweeps backward, publishes its
@@ -599,11 +401,8 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_fuse(Dev p, Bufs bf, const C
 //   k_dyn_down: [top] [tier 0] .. [deepest]: the top sweeps forward and releases tier 0;
 //               a tier-k workgroup waits for its parent's flag (the launch's epoch),
 //               sweeps forward, publishes its boundary x rows and releases its children.
-// A workgroup waits only for workgroups with lower block indices in k_dyn_down and higher
-// ones' producers ... precisely: in k_dyn_up for the deepest tiers' (lower indices), in
-// k_dyn_down for its parents' (lower indices), which are dispatched first and never wait
-// for it, so no co-residency is needed. Counters are reset by their one consumer after its
-// wait; flags carry the epoch, which k_dyn_up's top advances once per projection.
+// Counters are reset by their one consumer after its wait; flags carry the epoch, which
+// k_dyn_up's top advances once per projection.
 
 // spin (one lane) until *f == v, bounded; false on a timeout (error word set)
 __device__ __forceinline__ bool fz_wait_eq(const unsigned* f, unsigned v, const FuseArg& fa, int& ok) {
@@ -633,6 +432,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_up(Dev p, Bufs bf, const Ctl
         if (tid < 64) cp_check_wave(fa.ck);
         return;
     }
+    if (ld_u32_sc1((const unsigned*)fa.err)) return;  // an earlier hand-off timed out: the host resets
     ldsd* smem = (ldsd*)smem_;
     glbd* z = dyn_z(bf, zsel, ctl);
     if (tid == 0) {
@@ -749,6 +549,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const C
     __shared__ Prologue pl;
     __shared__ int s_ok;
     const int tid = threadIdx.x;
+    if (ld_u32_sc1((const unsigned*)fa.err)) return;  // an earlier hand-off timed out: the host resets
     ldsd* smem = (ldsd*)smem_;
     glbd* z = dyn_z(bf, zsel, ctl);
     if (tid == 0) {
@@ -779,90 +580,6 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const C
         fz_xd_stage<NXc, NUc>(p, dbuf_, tt, b, XD);
     }
     const unsigned tag = ld_u32_sc1(fa.epoch);
-    if (!fz_wait_eq(tt.flag + b / tt.r, tag, fa, s_ok)) return;
-    fz_stamp(p, pl);
-    if (work) fz_fwd_run<NXc, NUc>(p, z, tt, b, k < D, XD, scr, pl);
-    fz_stamp(p, pl);
-    if (k < D) {
-        fz_drain();
-        if (tid == 0) st_u32_sc1(fa.t[k + 1].flag + b, tag);
-    }
-    if (p.stamps && tid == 0 && b == 0)  // diagnostics: tier 0 / deepest, subtree 0
-        for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
-}
-
-// ==============================================================================
-// The split sweep in ONE launch (k_dyn_one, the default where its grid is co-resident): the
-// roles of k_dyn_up ([deferred stopping test] [deepest subtrees] .. [tier 0] [top]), and
-// every subtree workgroup then sweeps its own subtree forward too: it keeps d_i in LDS (its
-// XD rows), stages its forward tables while it waits for its parent's flag, and releases
-// its children's. The top sweeps backward and forward (its F rows in LDS or, to keep two
-// workgroups per CU, read from L2). A subtree workgroup now waits after its own backward
-// sweep for workgroups that may not have started, so the host launches it only when the
-// whole grid is co-resident (hipOccupancyMaxActiveBlocksPerMultiprocessor), and every wait
-// stays bounded. The epoch is read by every workgroup at its start and advanced by the top
-// after the last arrival (so after every read).
-template <int NXc, int NUc, bool FL>
-// two workgroups per CU (<= 128 VGPRs, 4 waves per SIMD): the grid (272 + 2 workgroups at
-// config 2) must be co-resident on 256 CUs
-__global__ void __launch_bounds__(kFuseBlock) __attribute__((amdgpu_waves_per_eu(4, 4))) k_dyn_one(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
-                                                        double* qbuf_, const double* x0_, FuseArg fa) {
-    extern __shared__ __attribute__((aligned(16))) double smem_[];
-    __shared__ Prologue pl;
-    __shared__ int s_ok;
-    const int tid = threadIdx.x;
-    if (fa.ck.on && blockIdx.x == 0) {  // the previous CP iteration's stopping test
-        if (tid < 64) cp_check_wave(fa.ck);
-        return;
-    }
-    ldsd* smem = (ldsd*)smem_;
-    glbd* z = dyn_z(bf, zsel, ctl);
-    if (tid == 0) {
-        pl.nts = 0;
-        s_ok = 1;
-    }
-    fz_stamp(p, pl);
-    const int D = fa.K - 1;
-    int b = (int)blockIdx.x - (fa.ck.on ? 1 : 0), k = D;
-    for (; k >= 0 && b >= fa.t[k].ngroups * fa.t[k].r; --k) b -= fa.t[k].ngroups * fa.t[k].r;
-    if (k < 0) {  // the top: backward and forward
-        fz_top_stage<NXc, NUc, FL>(p, z, fa, smem, pl, false);
-        const unsigned tag = ld_u32_sc1(fa.epoch) + 1u;
-        const bool work = !ctl_done(ctl);
-        if (!fz_wait_eq(fa.t[0].cnt, (unsigned)fa.t[0].r, fa, s_ok)) return;
-        if (tid == 0) st_u32_sc1(fa.t[0].cnt, 0u);
-        fz_stamp(p, pl);
-        if (work) fz_top_run<NXc, NUc, FL>(p, z, qbuf_, x0_, fa, smem, pl, nullptr);
-        fz_stamp(p, pl);
-        fz_drain();
-        if (tid == 0) {
-            st_u32_sc1(fa.epoch, tag);
-            st_u32_sc1(fa.t[0].flag, tag);
-        }
-        if (p.stamps && tid == 0)
-            for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[q] = pl.ts[q];
-        return;
-    }
-    // subtree b of tier k: [XD (nnl, KF) | backward, then forward region]
-    const FuseTier& tt = fa.t[k];
-    ldsd* XD = smem;
-    ldsd* scr = smem + rup(tt.nnl * Geo<NXc, NUc>(p).KF, 2);
-    // (LDS stores before the LDS-DMA copies: a store after them would wait for them)
-    zero_fill(XD, tt.nnl * Geo<NXc, NUc>(p).KF, tid, blockDim.x);  // x (root: later) / d / zero tail
-    fz_back_stage<NXc, NUc>(p, z, tt, b, k == D, scr);
-    const unsigned tag = ld_u32_sc1(fa.epoch) + 1u;
-    const bool work = !ctl_done(ctl);
-    if (k < D && !fz_wait_eq(fa.t[k + 1].cnt + b, (unsigned)fa.t[k + 1].r, fa, s_ok)) return;
-    if (k < D && tid == 0) st_u32_sc1(fa.t[k + 1].cnt + b, 0u);
-    fz_stamp(p, pl);
-    if (work) {
-        fz_back_wait<NXc, NUc>(p, qbuf_, tt, b, k == D, scr, pl);
-        fz_back_levels<NXc, NUc>(p, qbuf_, tt, b, k == D, XD, scr, pl);
-    }
-    fz_stamp(p, pl);
-    fz_drain();
-    if (tid == 0) __hip_atomic_fetch_add(tt.cnt + b / tt.r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (work) fz_fwd_stage<NXc, NUc>(p, tt, b, scr);  // the backward region is free
     if (!fz_wait_eq(tt.flag + b / tt.r, tag, fa, s_ok)) return;
     fz_stamp(p, pl);
     if (work) fz_fwd_run<NXc, NUc>(p, z, tt, b, k < D, XD, scr, pl);

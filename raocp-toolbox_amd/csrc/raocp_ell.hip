@@ -59,56 +59,25 @@ struct Gather {
             }
         }
     }
-    // the same chunks by vector loads into registers (all of a lane's loads in flight, then
-    // LDS stores): a CU streams ~4x the bytes of its LDS-DMA path (staging)
-    __device__ __forceinline__ void issue_reg() const {
-        const int tid = threadIdx.x, nt = blockDim.x;
-        constexpr int K = 8;
-        for (int b0 = 0; b0 < total; b0 += K * nt) {
-            d2v v[K];
-            _Pragma("unroll") for (int k = 0; k < K; ++k) {
-                const int ch = b0 + k * nt + tid;
-                if (ch < total) {
-                    const char* s = src[0];
-                    int c = cum[0];
-                    _Pragma("unroll") for (int r = 1; r < MAXR; ++r)
-                        if (r < nr && ch >= cum[r]) { s = src[r]; c = cum[r]; }
-                    v[k] = *(const glb2*)(s + 16 * (ch - c));
-                }
-            }
-            _Pragma("unroll") for (int k = 0; k < K; ++k) {
-                const int ch = b0 + k * nt + tid;
-                if (ch < total) *(lds2*)(base + 2 * ch) = v[k];
-            }
-        }
-    }
-    __device__ __forceinline__ void issue(bool reg) const {
-        if (reg) issue_reg();
-        else issue();
-    }
 };
 
 // sequential LDS regions filled by LDS-DMA (CP kernels). Region r occupies F_r 16-B chunk
 // slots from chunk offset o / 2 (F_r = its bytes rounded up plus one pad chunk, the
 // footprint the host's LDS plan counts). The regions are only recorded (source, first
-// slot, slots: a table in LDS, a few instructions per region); issue() then sends them:
-//   packed (Dev::cp_pack): every slot of the block, 64 per wave instruction, through a
-//             slot -> region map, so several short regions share one instruction;
-//   unpacked: one DMA pass per region (at least one instruction per region, however small:
-//             a family block of k_cpp has ~50 regions).
+// slot, slots: a table in LDS, a few instructions per region); issue() then sends them, one
+// DMA pass per region (packing short regions into shared instructions through a slot ->
+// region map measured neutral to 6 % slower: two more barriers per block).
 // Only a region's data chunks are loaded (its first chunk may start up to 8 B before the
 // range, its last end up to 15 B after it: inside the allocation or its 64-B slack).
 // (Recording instead of issuing per call keeps the kernels small: the inlined per-region
 // DMA loops made k_cpp 89 KB of code, more than the instruction cache.)
-constexpr int kStgMaxR = 64, kStgMaxChunks = 4096;
+constexpr int kStgMaxR = 64;
 // the recorded regions of one block (LDS tables: each kernel declares them, StgLds)
 struct StgTable {
     __attribute__((address_space(3))) unsigned long long* tsrc = nullptr;  // per region: 16-B aligned source
     __attribute__((address_space(3))) int* tc0 = nullptr;                 // per region: first slot
     __attribute__((address_space(3))) int* tF = nullptr;                  // per region: chunks to load
-    __attribute__((address_space(3))) unsigned char* regof = nullptr;     // slot -> region (packed)
     int nr = 0;
-    bool pack = false;
     __device__ __forceinline__ void record(const char* s16, int bytes, int c0) {
         if (threadIdx.x == 0 && nr < kStgMaxR) {
             tsrc[nr] = (unsigned long long)(uintptr_t)s16;
@@ -121,45 +90,24 @@ struct StgTable {
     // by the whole block); total = slots of the footprint
     __device__ __forceinline__ void issue(ldsd* base, int total) const {
         __syncthreads();  // the region table is written
-        const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wave = tid >> 6, nw = nt >> 6;
         const int R = min(nr, kStgMaxR);
-        if (pack && total <= kStgMaxChunks) {
-            for (int c = tid; c < total; c += nt) regof[c] = (unsigned char)kStgMaxR;  // footprint slots not loaded
-            __syncthreads();
-            _Pragma("unroll 1") for (int r = 0; r < R; ++r) {
-                const int c0 = tc0[r], F = tF[r];
-                for (int c = tid; c < F; c += nt) regof[c0 + c] = (unsigned char)r;
-            }
-            __syncthreads();
-            for (int c0 = wave * 64; c0 < total; c0 += nw * 64) {
-                const int ch = c0 + lane;
-                const int r = ch < total ? regof[ch] : kStgMaxR;
-                if (r < kStgMaxR) {
-                    const char* src = (const char*)(uintptr_t)tsrc[r];
-                    __builtin_amdgcn_global_load_lds((const glbd*)(src + 16 * (ch - tc0[r])), base + 2 * c0, 16, 0, 0);
-                }
-            }
-        } else {
-            int rot = 0;
-            _Pragma("unroll 1") for (int r = 0; r < R; ++r) {
-                const char* src = (const char*)(uintptr_t)tsrc[r];
-                rot += dma_gen(base + 2 * tc0[r], tF[r], [=](int ch) { return (const double*)(src + 16 * ch); }, rot);
-            }
+        (void)total;
+        int rot = 0;
+        _Pragma("unroll 1") for (int r = 0; r < R; ++r) {
+            const char* src = (const char*)(uintptr_t)tsrc[r];
+            rot += dma_gen(base + 2 * tc0[r], tF[r], [=](int ch) { return (const double*)(src + 16 * ch); }, rot);
         }
     }
 };
 // the LDS tables of a StgTable, declared once per kernel (a __shared__ array in an inlined
 // device function is one allocation per kernel that uses it)
-__device__ __forceinline__ StgTable stg_table(bool pack) {
+__device__ __forceinline__ StgTable stg_table() {
     __shared__ unsigned long long s_tsrc[kStgMaxR];
     __shared__ int s_tc0[kStgMaxR], s_tF[kStgMaxR];
-    __shared__ unsigned char s_regof[kStgMaxChunks];
     StgTable t;
     t.tsrc = (__attribute__((address_space(3))) unsigned long long*)s_tsrc;
     t.tc0 = (__attribute__((address_space(3))) int*)s_tc0;
     t.tF = (__attribute__((address_space(3))) int*)s_tF;
-    t.regof = (__attribute__((address_space(3))) unsigned char*)s_regof;
-    t.pack = pack;
     return t;
 }
 struct Stg {
@@ -451,7 +399,7 @@ __global__ void __launch_bounds__(512) k_ell(Dev p, const double* __restrict__ z
     const ldsd* XL = g.dbl(zg + p.X0 + (size_t)l0 * nx, nl * nx);  // leaves' x, s
     const ldsd* SL = g.dbl(zg + p.S0 + l0, nl);
     const ldsrec* LR = g.rec(p.lrec + (l0 - p.m), nl);  // {iSP, iBl, e14off, 0}
-    g.issue(p.regstage);
+    g.issue();
     const Rec t3 = tb[3];
     FamRun<NXc, NUc> fr(Fam{p.SQ, t3.x, nx, c0, nc, X}, Fam{p.SR, t3.y, nu, c0, nc, U}, Fam{p.SP, t3.z, nx, l0, nl, XL});
     fr.prefetch();
@@ -530,7 +478,7 @@ __global__ void __launch_bounds__(512) k_ell_t(Dev p, const double* __restrict__
     const ldsd* D12 = g.dbl(eg + p.E12 + l0, nl);
     const ldsd* D13 = g.dbl(eg + p.E13 + l0, nl);
     const ldsrec* LR = g.rec(p.lrec + (l0 - p.m), nl);  // {iSP, iBl, e14off, 0}
-    g.issue(p.regstage);
+    g.issue();
     // products sqrtQ_j eta3_j, sqrtR_j eta4_j (children) in LDS, summed per parent below; the
     // leaves' sqrtPf_l eta11_l (+ eta14_l) go straight from the MFMA tile to x_l
     ldsd* PX = (ldsd*)ell_smem + 2 * g.total;

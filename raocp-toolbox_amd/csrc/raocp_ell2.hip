@@ -26,7 +26,7 @@ __global__ void __launch_bounds__(256) k_ell2(Dev p, const double* __restrict__ 
     const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int lo = lane & 15, h = lane >> 4;
     const crec4* tab = (const crec4*)p.cp2_tab;
-    StgB st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
+    StgB st{(ldsd*)smem_, 0, stg_table()};
     if (bid < nbF) {
         const Rec t0 = tab[kCpFamRecs * bid], t1 = tab[kCpFamRecs * bid + 1], t2 = tab[kCpFamRecs * bid + 2];
         const int i0 = t1.z, i1 = t1.w, P = i1 - i0;
@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) k_ellt2(Dev p, const double* __restrict__
     const int bid = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nw = blockDim.x >> 6;
     const int lo = lane & 15, h = lane >> 4;
     const crec4* tab = (const crec4*)p.cp2_tab;
-    StgB st{(ldsd*)smem_, 0, stg_table(p.cp_pack)};
+    StgB st{(ldsd*)smem_, 0, stg_table()};
     if (bid < nbF) {
         const Rec t0 = tab[kCpFamRecs * bid], t1 = tab[kCpFamRecs * bid + 1], t2 = tab[kCpFamRecs * bid + 2];
         const int i0 = t1.z, i1 = t1.w, P = i1 - i0;

@@ -12,56 +12,11 @@
 //
 // Reference formulas are cited as /root/reference file:line.
 
-#include <hip/hip_runtime.h>
-#include <stdint.h>
-#include <type_traits>
+#include "raocp_common.h"
 
 namespace raocp {
 
-typedef unsigned long long u64;
-
 constexpr int kBlock = 256;
-
-struct Ctl {
-    u64 red[6];          // |xi0| |xi1| |xi2| |delta0| |delta1| |delta2| maxima (bit patterns)
-    double alpha;        // CP step size (alpha_1 = alpha_2, solver.py:116-118)
-    int k;               // current CP iteration
-    int done;            // 1 once the stopping test fired
-    int final_k;
-    int flags;           // bit0: NaN reached a box projection
-    int max_iters;
-    int pad;
-    double tol;
-};
-
-// the stopping test of the previous CP iteration run by an extra workgroup (block 0) of the
-// next iteration's first dynamics launch (raocp_capi.hip, defer_check): on = 0 disables it
-struct ChkArg {
-    Ctl* ctl;
-    double* hist;
-    const double* part;
-    int rows;
-    int on;
-};
-
-// explicit address spaces: loads through these types are ds_read / global_load, never flat
-typedef __attribute__((address_space(3))) double ldsd;
-typedef __attribute__((address_space(1))) double glbd;
-// node records for the dynamics sweep: a builtin 4-int vector (usable in any address space)
-typedef int Rec __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const Rec glbrec;
-typedef __attribute__((address_space(3))) Rec ldsrec;
-
-// the rotating CP buffers: primal Z[k % 3], dual E[k % 2] (selected by the iteration counter)
-struct Bufs {
-    double* z0;
-    double* z1;
-    double* z2;
-    double* e0;
-    double* e1;
-};
-
-__device__ __forceinline__ glbd* pick2(const Bufs& bf, int k) { return (glbd*)((k & 1) ? bf.e1 : bf.e0); }
 
 // Device-side problem description (all pointers are HBM).
 struct Dev {
@@ -102,10 +57,7 @@ struct Dev {
     const int* stage_ptr;  // [N+2] first node id of each stage (BFS numbering)
     int N;                 // last stage
     unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)
-    int regstage;          // staging by vector loads + LDS stores instead of LDS-DMA (RAOCP_REGSTAGE)
-    int dyn_regtab;        // dynamics kernels stage their matrix tables by vector loads (RAOCP_DYN_REGTAB)
     int dyn_rot;           // tier kernels rotate the first wave of each staged range (RAOCP_DYN_ROT)
-    int cp_pack;           // k_cpd / k_cpp pack their staged regions into shared DMA instructions (RAOCP_CP_PACK)
     int cp_dbg;            // timing diagnostics only (RAOCP_CP2_DBG bits): skip phases of k_cpd2 / k_cpp2
 };
 
@@ -115,20 +67,6 @@ __device__ __forceinline__ void stamp(const Dev& p, int slot) {
 }
 
 
-// agent-scope relaxed accesses (global_store / global_load ... sc1): write-through stores and
-// L1-bypassing loads for values another workgroup of the same launch reads (MI355X: per-XCD
-// L2s are not coherent with each other)
-typedef __attribute__((address_space(1))) unsigned long long gu64;
-typedef __attribute__((address_space(1))) unsigned int gu32;
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-    __hip_atomic_store((gu64*)p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_sc1(const double* p) {
-    return __longlong_as_double(
-        (long long)__hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
 __device__ __forceinline__ int e3(const Dev& p, int j) { return p.E3 + 1 + (j - 1) * p.nx; }
 __device__ __forceinline__ int e4(const Dev& p, int j) { return p.E4 + 1 + (j - 1) * p.nu; }
 __device__ __forceinline__ int e11(const Dev& p, int l) { return p.E11 + p.m + (l - p.m) * p.nx; }
@@ -136,34 +74,6 @@ __device__ __forceinline__ int e11(const Dev& p, int l) { return p.E11 + p.m + (
 __device__ __forceinline__ int cdiv_dev(int a, int b) { return (a + b - 1) / b; }
 
 __device__ __forceinline__ u64 dbits(double v) { return (u64)__double_as_longlong(v); }
-
-// max for the residual reductions: a NaN operand wins (fmax would drop it). The reference
-// takes its inf-norms with numpy, which propagates NaN, so a NaN residual fails the
-// stopping test `max(error) <= tol` there (solver.py:137-161) and must fail it here too.
-__device__ __forceinline__ double nmax(double a, double b) { return (a > b || a != a) ? a : b; }
-
-// k_cp_check by one wave (the deferred test's extra workgroup): lanes take rows, then a
-// butterfly of NaN-propagating maxima; the same record, history row and decision
-__device__ __forceinline__ void cp_check_wave(const ChkArg& ck) {
-    Ctl* ctl = ck.ctl;
-    if (ctl->done) return;
-    const int lane = threadIdx.x & 63;
-    double m[6] = {0, 0, 0, 0, 0, 0};
-    for (int r = lane; r < ck.rows; r += 64)
-        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], ck.part[(size_t)r * 6 + q]);
-    _Pragma("unroll") for (int off = 32; off > 0; off >>= 1)
-        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], __shfl_xor(m[q], off));
-    if (lane != 0) return;
-    const int k = ctl->k;
-    for (int q = 0; q < 6; ++q) ck.hist[(size_t)k * 6 + q] = m[q];
-    const double err = nmax(nmax(m[0], m[1]), m[2]);
-    if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
-        ctl->done = 1;
-        ctl->final_k = k;
-    } else {
-        ctl->k = k + 1;
-    }
-}
 
 // ---- batched dot products ----------------------------------------------------------
 // All loads of a chunk are issued before its FMAs (a sched_barrier keeps hipcc from

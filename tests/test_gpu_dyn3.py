@@ -113,25 +113,25 @@ def test_dyn3_deferred_stopping_test_matches_eager(iters, stop):
 
 def test_kernel_info_lists_the_projection_launches():
     """raocp_kernel_info(9) names every launch of one projection as "name xcount" terms
-    (bench.py sums their PMC traffic): the split sweep (k_dyn_up + k_dyn_down) at config 2, in
-    one launch (k_dyn_one) with RAOCP_DYN_ONE=1, 2 tiers + the top with RAOCP_DYN_SPLIT=0, the fused sweep (one launch) with
-    RAOCP_DYN_FUSE=1, one k_dy3_back and one k_dy3_fwd per nonleaf stage with RAOCP_DYN3=1."""
+    (bench.py sums their PMC traffic): the regular-tree sweep (k_dr_up + k_dr_down) at config 2;
+    with RAOCP_DR=0 the split sweep (k_dyn_up + k_dyn_down), the tier launches (2 tiers + the
+    top) with RAOCP_DYN_SPLIT=0 too, one k_dy3_back and one k_dy3_fwd per nonleaf stage with
+    RAOCP_DYN3=1."""
     import re
     r = recipe_config(2)
     prob = build_problem(r)[1]
-    for env, want in (({}, "split"), ({"RAOCP_DYN_ONE": "1"}, "one"), ({"RAOCP_DYN_SPLIT": "0"}, None),
-                      ({"RAOCP_DYN_FUSE": "1"}, "fuse"), ({"RAOCP_DYN3": "1"}, "dy3")):
+    off = {"RAOCP_DR": "0"}
+    for env, want in (({}, "dr"), (off, "split"), ({**off, "RAOCP_DYN_SPLIT": "0"}, None),
+                      ({"RAOCP_DYN3": "1"}, "dy3")):
         cache = _with_env(env, lambda: core.Cache(prob))
         terms = [re.fullmatch(r"(k_\w+<[^>]*>) x(\d+)", t) for t in cache.native.kernel_info(9).split(" + ")]
         assert all(terms), cache.native.kernel_info(9)
         cnt = {m.group(1).split("<")[0]: int(m.group(2)) for m in terms}
         if want == "dy3":
             assert cnt == {"k_dy3_back": 12, "k_dy3_fwd": 12}
-        elif want == "fuse":
-            assert cnt == {"k_dyn_fuse": 1}
+        elif want == "dr":
+            assert cnt == {"k_dr_up": 1, "k_dr_down": 1}
         elif want == "split":
             assert cnt == {"k_dyn_up": 1, "k_dyn_down": 1}
-        elif want == "one":
-            assert cnt == {"k_dyn_one": 1}
         else:
             assert cnt["k_dyn_top"] == 1 and cnt["k_dyn_bottom_back"] == cnt["k_dyn_bottom_fwd"] >= 1

@@ -1,0 +1,171 @@
+"""GPU parity of the regular-tree dynamics sweep k_dr_up / k_dr_down (raocp_dynr.hip;
+cache.py:259-288): one workgroup per subtree of every tier, counters of arrivals up the
+tiers, epoch flags down, every node address computed from (stage, subtree). The default of
+fp64 regular trees at nx = 20, nu = 8 (config 2); RAOCP_DR=0 falls back to the tiered sweep
+(raocp_dynf.hip / raocp_dyn.hip).
+
+Tolerances: the projection against the oracle within 1e-12 of the largest entry and exact
+feasibility x_j = A_j x_i + B_j u_i to 1e-12; against the tiered sweep (the same algebra, a
+different summation order) 1e-13 of the largest entry; the CP loop against the tiered sweep
+1e-10 per trace entry and the oracle 1e-8 (BASELINE.json north_star); the projection after
+1,000 graph-replayed launches (counters reset and epoch advanced inside the kernels) bit for
+bit; a forced hand-off timeout reported as an error within a fraction of a second.
+"""
+import os
+import time
+
+import numpy as np
+import pytest
+
+import raocp.core as core
+from raocp.problems import build_problem, recipe_config, recipe_synthetic
+from helpers import rel_err, trace_rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _recipe(cfg):
+    if cfg == "quad":  # branching 4, 6 stages
+        return recipe_synthetic(np.full((4, 4), .25), np.full(4, .25), 6, 6, 20, 8, seed=6)
+    if cfg == "tri":  # branching 3 (split-k groups of 4 lanes, one idle slot)
+        return recipe_synthetic(np.full((3, 3), 1 / 3), np.full(3, 1 / 3), 7, 7, 20, 8, seed=8)
+    if cfg == "bin10":
+        return recipe_synthetic(np.full((2, 2), .5), np.full(2, .5), 10, 10, 20, 8, seed=4)
+    if cfg == "bin3":  # a shallow tree: one tier
+        return recipe_synthetic(np.full((2, 2), .5), np.full(2, .5), 3, 3, 20, 8, seed=5)
+    return recipe_config(int(cfg[1:]))
+
+
+TIERS = {"RAOCP_DR": "0", "RAOCP_DYN_SPLIT": "0"}
+
+
+def _project(cache, r, zz):
+    cache.cache_initial_state(r["x0"])
+    cache.native.set_primal(zz)
+    cache.native.project_on_dynamics()
+    return cache.native.get_primal()
+
+
+@pytest.mark.parametrize("cuts", [None, "4,7", "6", "3,6,9", "2"])
+@pytest.mark.parametrize("cfg", ["c2", "quad", "tri", "bin10", "bin3"])
+def test_dr_projection_matches_oracle_and_tiers(cfg, cuts):
+    from oracle.raocp_oracle import OracleProblem
+    r = _recipe(cfg)
+    tree, prob = build_problem(r)
+    env = {"RAOCP_DR_CUTS": cuts} if cuts else {}
+    try:
+        dr = _with_env(env, lambda: core.Cache(prob))
+    except Exception as e:  # a forced cut list this tree cannot take
+        assert cuts and "RAOCP_DR_CUTS" in str(e)
+        pytest.skip(f"cuts {cuts} invalid for {cfg}")
+    assert dr.native.kernel_info(9) == "k_dr_up<20, 8> x1 + k_dr_down<20, 8> x1"
+    tiers = _with_env(TIERS, lambda: core.Cache(prob))
+    assert "k_dr_" not in tiers.native.kernel_info(9)
+    zz = np.random.default_rng(5).standard_normal(dr.primal_size)
+    z1 = _project(dr, r, zz)
+    z2 = _project(tiers, r, zz)
+    assert rel_err(z1, z2) <= 1e-13
+    orc = OracleProblem(prob)
+    assert rel_err(z1, orc.project_on_dynamics(zz, r["x0"])) <= 1e-12
+    X = z1[orc.X0:orc.U0].reshape(orc.n, orc.nx)
+    U = z1[orc.U0:orc.Y0].reshape(orc.m, orc.nu)
+    j = np.arange(1, orc.n)
+    pred = np.einsum("jab,jb->ja", orc.A[orc.iA[j]], X[orc.anc[j]]) + \
+        np.einsum("jab,jb->ja", orc.B[orc.iB[j]], U[orc.anc[j]])
+    assert np.max(np.abs(X[j] - pred)) <= 1e-12 * max(1.0, np.max(np.abs(X)))
+    assert np.array_equal(X[0], np.asarray(r["x0"], float))
+    # everything outside (x, u) untouched
+    assert np.array_equal(z1[orc.Y0:], zz[orc.Y0:])
+
+
+def test_dr_cp_loop_matches_tiers_and_oracle():
+    """30 CP iterations (a full 24-iteration graph batch plus a remainder; the deferred
+    stopping test rides on k_dr_up), tol = 0."""
+    from oracle.raocp_oracle import OracleProblem
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    dr = core.Cache(prob)
+    tiers = _with_env(TIERS, lambda: core.Cache(prob))
+    assert dr.native.kernel_info(9).startswith("k_dr_up")
+    alpha = 0.999 / dr.native.step_size()
+    out = []
+    for cache in (dr, tiers):
+        st, err, derr = cache.native.cp_run(r["x0"], 30, 0.0, alpha)
+        out.append((st, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
+    (s1, e1, d1, z1, y1), (s2, e2, d2, z2, y2) = out
+    assert s1 == s2 == 1 and e1.shape == e2.shape == (31, 3)
+    assert trace_rel_err(e1, e2) <= 1e-10 and trace_rel_err(d1, d2) <= 1e-10
+    assert rel_err(z1, z2) <= 1e-11 and rel_err(y1, y2) <= 1e-11
+    st_o, err_o, _, z_o, _, _ = OracleProblem(prob).chock(r["x0"], 30, 0.0, alpha=alpha)
+    assert trace_rel_err(e1, err_o) <= 1e-8 and rel_err(z1, z_o) <= 1e-10
+
+
+@pytest.mark.parametrize("iters,stop", [(1, None), (24, None), (30, None), (60, True)])
+def test_dr_deferred_stopping_test_matches_eager(iters, stop):
+    """The deferred stopping test (an extra workgroup of k_dr_up) against k_cp_check after
+    every iteration (RAOCP_DEFER_CHECK=0): bit for bit, early stops included."""
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    dfr = core.Cache(prob)
+    eag = _with_env({"RAOCP_DEFER_CHECK": "0"}, lambda: core.Cache(prob))
+    assert dfr.native.kernel_info(9).startswith("k_dr_up")
+    alpha = 0.999 / dfr.native.step_size()
+    tol = 0.0
+    if stop:
+        _, err, _ = eag.native.cp_run(r["x0"], iters, 0.0, alpha)
+        tol = float(err[37].max())
+    out = []
+    for cache in (dfr, eag):
+        status, err, derr = cache.native.cp_run(r["x0"], iters, tol, alpha)
+        out.append((status, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
+    for u, v in zip(out[0], out[1]):
+        assert np.array_equal(u, v)
+    if stop:
+        assert out[0][0] == 0 and out[0][1].shape[0] <= 38
+
+
+def test_dr_many_launches_then_projection():
+    """1,000 back-to-back launches (graph-replayed, as in the CP loop): the counters are reset
+    by their consumers and the epoch advances inside the kernels; a projection afterwards is
+    the same bit for bit."""
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    dr = core.Cache(prob)
+    zz = np.random.default_rng(9).standard_normal(dr.primal_size)
+    out = []
+    for rep in range(2):
+        out.append(_project(dr, r, zz))
+        dr.native.op_bench(9, 1000)
+    assert np.array_equal(out[0], out[1])
+
+
+def test_dr_forced_timeout_is_reported_quickly():
+    """RAOCP_DR_FAULT=1: the deepest tier's first subtree never arrives, so its parent's wait
+    times out (RAOCP_FUSE_TIMEOUT_MS=5), sets the error word and leaves; every workgroup of a
+    later launch sees the word at its start and leaves at once. The projection raises, and
+    so does the next one, each within a fraction of a second (not a 1 s wait per tier)."""
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    bad = _with_env({"RAOCP_DR_FAULT": "1", "RAOCP_FUSE_TIMEOUT_MS": "5"}, lambda: core.Cache(prob))
+    zz = np.random.default_rng(3).standard_normal(bad.primal_size)
+    for _ in range(2):
+        t0 = time.perf_counter()
+        with pytest.raises(Exception, match="timed out"):
+            _project(bad, r, zz)
+        assert time.perf_counter() - t0 < 0.5
+    # a healthy context on the same device is unaffected
+    good = core.Cache(prob)
+    assert rel_err(_project(good, r, zz), _project(_with_env(TIERS, lambda: core.Cache(prob)), r, zz)) <= 1e-13

@@ -5,7 +5,7 @@ device of the test box and exchange through device copies (raocp_group_cp_run); 
 multi-GPU transport is RCCL with the same packing (bench.py --shard).
 
 Parity: the residual histories and the owned parts of the final iterate equal those of
-the unsharded solve on the same CP kernels -- the fused k_cp3 (a shard runs it as two
+the unsharded solve on the same dynamics and CP kernels -- the fused k_cp3 (a shard runs it as two
 launches around X1, the cut's parents reading their children's eta2 entries from the
 exchange) or the two-launch k_cpd* / k_cpp* (RAOCP_CP3=0) -- bit for bit: the per-node
 arithmetic is identical and only max reductions are regrouped, which is exact. The two
@@ -39,16 +39,19 @@ def c2():
 def _kern_cache(prob, kern, dtype=None):
     """A context on the fused CP kernel k_cp3 ("fused", the default) or the two-launch
     k_cpd* / k_cpp* ("two", RAOCP_CP3=0)."""
-    old = os.environ.get("RAOCP_CP3")
+    env = {"RAOCP_DR": "0"}  # the dynamics a shard runs (the tiered sweep; fp32 / config 4: dyn3)
     if kern == "two":
-        os.environ["RAOCP_CP3"] = "0"
+        env["RAOCP_CP3"] = "0"
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
     try:
         return core.Cache(prob, dtype=dtype) if dtype else core.Cache(prob)
     finally:
-        if old is None:
-            os.environ.pop("RAOCP_CP3", None)
-        else:
-            os.environ["RAOCP_CP3"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
 
 
 def _two_launch_cache(prob):
@@ -91,6 +94,10 @@ def test_sharded_solve_matches_unsharded(cfg, R, kern):
     other = _kern_cache(prob, "two" if kern == "fused" else "fused")
     stf, errf, _ = other.native.cp_run(r["x0"], iters, 0.0, alpha)
     assert stf == st0 and np.max(np.abs(errf - err0) / np.abs(err0)) <= 1e-10
+    # the unsharded default (config 2: the regular-tree sweep k_dr_up / k_dr_down)
+    dflt = core.Cache(prob)
+    std, errd, _ = dflt.native.cp_run(r["x0"], iters, 0.0, alpha)
+    assert std == st0 and np.max(np.abs(errd - err0) / np.abs(err0)) <= 1e-10
     st_o, err_o, _, z_o, _, _ = _oracle_run(cfg, prob, r["x0"], iters, alpha)
     assert np.max(np.abs(err0 - err_o) / np.abs(err_o)) <= 1e-8
     assert np.max(np.abs(z0 - z_o)) <= 1e-10 * np.max(np.abs(z_o))

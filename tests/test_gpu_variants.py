@@ -1,9 +1,7 @@
-"""GPU parity of the opt-in kernel variants (measured slower on MI355X than the defaults,
-kept correct): the CP stopping test fused into k_cpp's last block (RAOCP_FUSE_CHECK=1);
-the eager stopping test after every iteration (RAOCP_DEFER_CHECK=0) against the default
-deferred one; the staging switches (RAOCP_CP_PACK=1: the staged regions of k_cpd / k_cpp
-packed into shared LDS-DMA instructions; RAOCP_DYN_ROT=0: every staged range of the dynamics kernels starts at
-wave 0), which must not change a bit; and the default per-parent L^T tiles against the
+"""GPU parity of the kernel variants kept selectable: the eager stopping test after every
+iteration (RAOCP_DEFER_CHECK=0) against the default deferred one; the staging switch
+RAOCP_DYN_ROT=0 (every staged range of the tiered dynamics kernels starts at wave 0), which
+must not change a bit; and the default per-parent L^T tiles against the
 LDS-staged path (RAOCP_ELLT_PARENT_TILES=0); the streaming L^T (k_ellt3, default on
 uniform trees) against the block kernel (RAOCP_ELLT3=0) and the oracle.
 
@@ -34,33 +32,6 @@ def _with_env(env, fn):
                 os.environ[k] = v
 
 
-def test_fused_stopping_test_c2_vs_oracle():
-    from oracle.raocp_oracle import OracleProblem
-    r = recipe_config(2)
-    tree, prob = build_problem(r)
-    orc = OracleProblem(prob)
-    cache = _with_env({"RAOCP_FUSE_CHECK": "1"}, lambda: core.Cache(prob))
-    alpha = 0.999 / cache.native.step_size()
-    st_o, err_o, derr_o, z_o, e_o, _ = orc.chock(r["x0"], 29, 0.0, alpha=alpha)
-    for _ in range(2):  # the ticket is re-armed by the last block of every launch
-        status, err, derr = cache.native.cp_run(r["x0"], 29, 0.0, alpha)
-        assert status == st_o == 1 and err.shape == (30, 3)
-        assert trace_rel_err(err, err_o) <= 1e-8
-        assert trace_rel_err(derr, derr_o) <= 1e-8
-        assert rel_err(cache.get_primal_flat(), z_o) <= 1e-10
-
-
-def test_fused_stopping_test_main_py(golden):
-    z = golden("main_trace")
-    r, tree, prob = problem_from_golden(z, "main")
-    solver = _with_env({"RAOCP_FUSE_CHECK": "1"}, lambda: core.Solver(problem_spec=prob))
-    status = solver.chock(initial_state=r["x0"].reshape(-1, 1), max_iters=int(z["main/cp_max_iters"]),
-                          tol=float(z["main/cp_tol"]), step_size=float(z["main/cp_alpha"]))
-    assert status == 0 and solver.error_cache.shape == (937, 3)
-    assert trace_rel_err(solver.error_cache, z["main/cp_error"]) <= 1e-8
-    assert rel_err(solver.cache.get_primal_flat(), z["main/cp_z"]) <= 1e-9
-
-
 @pytest.mark.parametrize("iters,stop", [(0, None), (1, None), (23, None), (24, None), (30, None), (60, 37), (60, 24)])
 def test_deferred_stopping_test_matches_eager(iters, stop):
     """The default deferred stopping test (iteration k's test in an extra workgroup of
@@ -88,16 +59,17 @@ def test_deferred_stopping_test_matches_eager(iters, stop):
         assert s1 == 0 and e1.shape[0] <= stop + 1  # stopped early
 
 
-@pytest.mark.parametrize("env", [{"RAOCP_CP_PACK": "1"}, {"RAOCP_DYN_ROT": "0"}], ids=["cp_pack1", "dyn_rot0"])
 @pytest.mark.parametrize("cfg", [1, 2])
-def test_staging_switches_bit_identical(env, cfg):
-    """Staging only moves bytes: the CP loop with a staging switch flipped reproduces the
-    default run bit for bit (config 1: the generic-size kernels; config 2: the benchmark)."""
+def test_staging_switches_bit_identical(cfg):
+    """Staging only moves bytes: the CP loop with RAOCP_DYN_ROT=0 reproduces the default run
+    bit for bit (config 1: the generic-size kernels; config 2 on the tiered sweep, RAOCP_DR=0,
+    the regular-tree sweep has no rotation)."""
     from raocp.problems import recipe_main
     r = recipe_main() if cfg == 1 else recipe_config(2)
     tree, prob = build_problem(r)
-    a = core.Cache(prob)
-    b = _with_env(env, lambda: core.Cache(prob))
+    base = {"RAOCP_DR": "0"}
+    a = _with_env(base, lambda: core.Cache(prob))
+    b = _with_env({**base, "RAOCP_DYN_ROT": "0"}, lambda: core.Cache(prob))
     alpha = 0.999 / a.native.step_size()
     out = []
     for cache in (a, b):

@@ -1,0 +1,57 @@
+# Round-4 GPU runner (one script for every GPU call of the round):
+#   gpurun -- 'bash tools/gpu_r04.sh <tag> <step> [<step> ...]'
+# Steps run in order, each under its own time limit, output under gpurun_out/<tag>/; the
+# first failing step ends the call (no GPU step runs after a failure).
+#   dynr        tests/test_gpu_dynr.py (the regular-tree sweep)
+#   dyntests    the dynamics test files (dynr, dyn_fuse, dyn3, variants)
+#   tests       the whole -m gpu suite
+#   smoke       __graft_entry__.smoke()
+#   dyn         dynamics projection timings at config 2 (tools/dyn_time.py, variants in $DYN_VARIANTS)
+#   stamps      in-kernel stamps of the regular-tree sweep at config 2 (tools/dr_stamps.py)
+#   cp          CP kernel / dynamics / loop timings (tools/cp3_time.py)
+#   bench20     bench.py --steps 20 --warmup 5 (the driver's K)
+#   bench       bench.py default run
+#   prof        rocprofv3 --kernel-trace --stats of bench.py (eager launches)
+#   pmc         FETCH_SIZE / WRITE_SIZE passes of the same bench command
+#   asan        the host-ASan ABI driver on the GPU
+export TMPDIR=/tmp
+set -o pipefail
+tag=$1
+shift
+out=gpurun_out/$tag
+mkdir -p "$out"
+PYT="python -u -m pytest -m gpu -x -v --timeout 120 --timeout-method thread"
+BARGS="--steps 96 --warmup 24 --no-cpu --no-shard --op-reps 200 --fp32-steps 12"
+fail() { echo "step $1 failed"; tail -40 "$2"; exit 1; }
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    dynr) timeout -k 10 500 $PYT tests/test_gpu_dynr.py > $out/pytest_dynr.log 2>&1 || fail $step $out/pytest_dynr.log
+          tail -3 $out/pytest_dynr.log ;;
+    dyntests) timeout -k 10 900 $PYT tests/test_gpu_dynr.py tests/test_gpu_dyn_split.py tests/test_gpu_dyn3.py tests/test_gpu_variants.py > $out/pytest_dyn.log 2>&1 || fail $step $out/pytest_dyn.log
+          tail -3 $out/pytest_dyn.log ;;
+    tests) timeout -k 10 1100 $PYT tests > $out/pytest_gpu.log 2>&1 || fail $step $out/pytest_gpu.log
+          tail -3 $out/pytest_gpu.log ;;
+    smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || fail $step $out/smoke.log
+          tail -2 $out/smoke.log ;;
+    dyn) timeout -k 10 400 python -u tools/dyn_time.py 2 default ${DYN_VARIANTS:-} > $out/dyn_time.log 2>&1 || fail $step $out/dyn_time.log
+          cat $out/dyn_time.log ;;
+    stamps) timeout -k 10 200 python -u tools/dr_stamps.py 2 6 > $out/stamps_c2.log 2>&1 || fail $step $out/stamps_c2.log
+          cat $out/stamps_c2.log ;;
+    cp) timeout -k 10 500 python -u tools/cp3_time.py ${CP_ARGS:-} > $out/cp3_time.log 2>&1 || fail $step $out/cp3_time.log
+          cat $out/cp3_time.log ;;
+    bench20) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $out/bench_k20.log 2>&1 || fail $step $out/bench_k20.log
+          tail -1 $out/bench_k20.log > $out/bench_k20.json; cut -c1-400 $out/bench_k20.json ;;
+    bench) timeout -k 10 500 python -u bench.py > $out/bench.log 2>&1 || fail $step $out/bench.log
+          tail -1 $out/bench.log > $out/bench.json; cut -c1-400 $out/bench.json ;;
+    prof) RAOCP_EAGER=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o prof --output-format csv -- python3 bench.py $BARGS > $out/prof.log 2>&1 || fail $step $out/prof.log
+          find $out/prof -name "*kernel_stats.csv" -exec cp {} $out/prof_kernel_stats.csv \; ; head -30 $out/prof_kernel_stats.csv ;;
+    pmc) for ctr in FETCH_SIZE WRITE_SIZE; do
+           timeout -s KILL 300 rocprofv3 --pmc $ctr --kernel-trace -d $out/pmc_$ctr -o pmc --output-format csv -- python3 bench.py $BARGS > $out/pmc_$ctr.log 2>&1 || fail $step $out/pmc_$ctr.log
+         done ;;
+    asan) LSAN_OPTIONS=suppressions=tests/asan/lsan.supp timeout -k 10 120 ./build/asan_abi gpu > $out/asan_gpu.log 2>&1 || fail $step $out/asan_gpu.log
+          tail -2 $out/asan_gpu.log ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"
