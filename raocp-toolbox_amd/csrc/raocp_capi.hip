@@ -5,6 +5,7 @@
 
 #include "raocp_kernels.hip"
 #include "raocp_dynr.h"
+#include "raocp_cp4.h"
 #include "../../include/raocp_hip.h"
 
 #include <dlfcn.h>
@@ -58,6 +59,7 @@ struct raocp_ctx {
     int ellt3_C = 0;             // L^T by streaming wave tasks: uniform branching factor (0 = off)
     int ellt3_grid = 0;
     bool cp3 = false;            // the CP iteration after the dynamics as one streaming kernel (raocp_cp3.hip)
+    bool cp4 = false;            // ... with every operand of a tile loaded at its start (raocp_cp4.hip; RAOCP_CP4=0: off)
     int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
     int cp3_split = 0;           // leaves as tasks of their own (small trees: more waves, shorter chains)
@@ -1026,6 +1028,11 @@ int cp3_image(raocp_ctx* c) {
     return cp3_imaget<double, 32, 12>(c);
 }
 void launch_cp3(raocp_ctx* c, int part = 0) {
+    if (c->cp4 && c->sh_S == 0) {
+        raocp::cp4_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->cp3_ta, c->cp3img, c->cp3_grid,
+                          c->stream);
+        return;
+    }
     if (c->sh_S > 0)
         launch_cp3t<true>(c, part ? c->cp3_gridb : c->cp3_grid, c->redpart + (part ? (size_t)c->cp3_grid * 6 : 0),
                           part ? c->cp3_tb : c->cp3_ta);
@@ -1263,6 +1270,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             return s;
         }
         case 10:
+            if (c->cp4 && c->sh_S == 0) return raocp::cp4_name(c->f32, c->nx, c->nu);
             if (c->cp3) return "k_cp3<" + T + ", " + nn + (c->sh_S > 0 ? ", true> x2" : ", false>");
             return kernel_name(c, 2) + " + " + kernel_name(c, 6);
         default: return "";
@@ -2645,6 +2653,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             }
             c->cp_rows = c->cp3_grid;
             if ((rc = cp3_image(c))) return bail(rc);
+            c->cp4 = raocp::cp4_supported(c->f32, nx, nu, c->unif_C, c->box_mode);
+            if (const char* e = getenv("RAOCP_CP4")) c->cp4 = c->cp4 && atoi(e) != 0;
         }
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels

@@ -195,16 +195,7 @@ struct LeafIn {
 // children's eta2 entries (eta+, xi2) come from the buffers the exchange filled (ext2)
 // instead of being recomputed from rows another shard owns; the first launch stores xi2 of
 // its roots' eta2 (parents [xlo, xhi)) for X1.
-constexpr int kCp3MaxR = 36;
-struct Cp3Tasks {
-    int l0, l1;    // split leaf tiles (l0 == l1: none)
-    int split;     // the leaf rows belong to the leaf tasks (1) or to their parents' tiles (0)
-    int mL;        // first parent whose children are leaves
-    int ext2;      // children's eta2 (eta+, xi2) from the buffers
-    int xlo, xhi;  // parents whose xi2 of eta2 is stored
-    int nr;        // parent ranges
-    int lo[kCp3MaxR], hi[kCp3MaxR], t0[kCp3MaxR + 1];  // t0: first task of each range
-};
+// (kCp3MaxR and Cp3Tasks: raocp_common.h, shared with raocp_cp4.hip)
 
 // The weight fragments of the launch ([sqrtQ | sqrtR | sqrtPf] in LDS order), laid out once
 // per context: every workgroup copies them by LDS-DMA (one memory round trip in front of its

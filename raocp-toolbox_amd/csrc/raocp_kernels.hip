@@ -18,48 +18,6 @@ namespace raocp {
 
 constexpr int kBlock = 256;
 
-// Device-side problem description (all pointers are HBM).
-struct Dev {
-    int n, m, nx, nu, cmax;
-    int X0, U0, Y0, T0, S0, P;
-    int E1, E2, E3, E4, E5, E6, E7, E11, E12, E13, E14, D;
-    const int* anc;
-    const int* ch_start;
-    const int* nch;
-    const int* rank;
-    const int* yrel;     // [m] offset of y_i (and eta1_i) inside its segment
-    const int* e7off;    // [m] absolute offset of eta7_i or -1
-    const int* e14off;   // [n-m] absolute offset of eta14_l or -1
-    // L / L^T weights, column-major: M[k*rows + r] = M_rk
-    const double* SQ; const double* SR; const double* SP;
-    const double* SQr; const double* SRr; const double* SPr;  // the same tables row-major
-    const int* iSQ; const int* iSR; const int* iSP;
-    int nSQ, nSR, nSP;   // table counts
-    const double* alpha_r; const double* cond;
-    const double* blo_nl; const double* bhi_nl; const double* blo_l; const double* bhi_l;
-    const int* iBnl; const int* iBl;
-    // dynamics projection (raocp_dyn.hip header): per child kind W = [B'; A'], per class
-    // RG = [R~^-1; G] and K, per (kind, parent class) pair F = [Abar | B]; padded rows
-    const double* dW; const double* dRG; const double* dKM; const double* dF;
-    const double* dWT;     // per (kind, class) pair: [-Rinv B' ; A' - G B'] (one-phase backward level)
-    int nkind;             // number of child kinds (rows of W)
-    const double* zpage;   // 16 doubles of zeros (LDS-DMA source of padding)
-    const Rec* crec;       // [n] {anc, iSQ, iSR, 0} (node 0: unused) — CP child blocks
-    const Rec* frec;       // [m] {yrel, nch, ch_start, e7off} — CP family blocks (raocp_cp.hip)
-    const Rec* lrec;       // [n-m] {iSP, iBl, e14off, 0} — CP leaf blocks
-    const Rec* cpd_tab;    // per CP block: family {cb, ce, y0, y1}, {e7a, e7b}; leaf {e14a, e14b}
-    const Rec* cp2_tab;    // per MFMA CP block (raocp_cp2.hip): family 3 records, leaf 2
-    int nBnl, nBl;         // box table counts
-    const Rec* ell_tab;    // [L / L^T blocks][kEllRecs] node ranges (raocp_ell.hip)
-    const Rec* dblk;       // [child blocks of the CP kernels] {first parent, last parent, 0, 0}
-    const Rec* ninfo;      // [m] {ch_start, nch, class, stage}
-    const Rec* cinfo;      // [n] {kind, pair, anc, 0} (node 0: unused)
-    const int* stage_ptr;  // [N+2] first node id of each stage (BFS numbering)
-    int N;                 // last stage
-    unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)
-    int dyn_rot;           // tier kernels rotate the first wave of each staged range (RAOCP_DYN_ROT)
-    int cp_dbg;            // timing diagnostics only (RAOCP_CP2_DBG bits): skip phases of k_cpd2 / k_cpp2
-};
 
 // diagnostic timestamp (100 MHz constant clock), thread 0 only, when enabled
 __device__ __forceinline__ void stamp(const Dev& p, int slot) {

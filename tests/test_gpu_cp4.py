@@ -1,0 +1,83 @@
+"""GPU parity of k_cp4 (raocp_cp4.hip): the fused CP iteration of k_cp3 (raocp_cp3.hip;
+solver.py:27-95, cache.py:248-393) with every operand of a tile loaded at the tile's start.
+The default of fp64 trees with one branching factor C = 2 at nx = 20, nu = 8 (config 2) whose
+nonleaf and leaf nodes are all boxed or all unboxed; RAOCP_CP4=0 keeps k_cp3.
+
+The arithmetic is k_cp3's operation for operation, so the CP loop on the two kernels must
+agree bit for bit (residual histories, final primal and dual); against the oracle 1e-8 per
+residual entry (BASELINE.json north_star) and 1e-10 on the iterate. Cases: config 2 with its
+boxes, without boxes, with leaf boxes only; the leaves inside their families' tiles
+(RAOCP_CP3_SPLIT=0); a graph batch boundary (30 iterations) and an early stop.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import raocp.core as core
+from raocp.problems import build_problem, recipe_config
+from helpers import rel_err, trace_rel_err
+
+pytestmark = pytest.mark.gpu
+
+
+def _with_env(env, fn):
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update({k: str(v) for k, v in env.items()})
+    try:
+        return fn()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def _recipe(case):
+    r = recipe_config(2)
+    if case in ("nobox", "leafbox"):
+        r["nl_min"] = r["nl_max"] = None
+        if case == "nobox":
+            r["l_min"] = r["l_max"] = None
+    return r
+
+
+@pytest.mark.parametrize("case,env", [("boxed", {}), ("nobox", {}), ("leafbox", {}),
+                                      ("boxed", {"RAOCP_CP3_SPLIT": "0"})],
+                         ids=["boxed", "nobox", "leafbox", "nosplit"])
+def test_cp4_matches_cp3_bit_for_bit_and_oracle(case, env):
+    from oracle.raocp_oracle import OracleProblem
+    r = _recipe(case)
+    tree, prob = build_problem(r)
+    c4 = _with_env(env, lambda: core.Cache(prob))
+    c3 = _with_env({**env, "RAOCP_CP4": "0"}, lambda: core.Cache(prob))
+    assert c4.native.kernel_info(10) == "k_cp4<double, 20, 8>"
+    assert c3.native.kernel_info(10).startswith("k_cp3<double, 20, 8")
+    alpha = 0.999 / c4.native.step_size()
+    out = []
+    for cache in (c4, c3):
+        st, err, derr = cache.native.cp_run(r["x0"], 30, 0.0, alpha)
+        out.append((st, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
+    for u, v in zip(out[0], out[1]):
+        assert np.array_equal(u, v)
+    st_o, err_o, _, z_o, _, _ = OracleProblem(prob).chock(r["x0"], 30, 0.0, alpha=alpha)
+    assert out[0][0] == st_o == 1
+    assert trace_rel_err(out[0][1], err_o) <= 1e-8 and rel_err(out[0][3], z_o) <= 1e-10
+
+
+def test_cp4_early_stop_matches_cp3():
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    c4 = core.Cache(prob)
+    c3 = _with_env({"RAOCP_CP4": "0"}, lambda: core.Cache(prob))
+    alpha = 0.999 / c4.native.step_size()
+    _, err, _ = c3.native.cp_run(r["x0"], 60, 0.0, alpha)
+    tol = float(err[41].max())
+    out = []
+    for cache in (c4, c3):
+        st, err, derr = cache.native.cp_run(r["x0"], 60, tol, alpha)
+        out.append((st, err, derr, cache.get_primal_flat()))
+    for u, v in zip(out[0], out[1]):
+        assert np.array_equal(u, v)
+    assert out[0][0] == 0 and out[0][1].shape[0] <= 42

@@ -3,6 +3,7 @@
 # Steps run in order, each under its own time limit, output under gpurun_out/<tag>/; the
 # first failing step ends the call (no GPU step runs after a failure).
 #   dynr        tests/test_gpu_dynr.py (the regular-tree sweep)
+#   cp4         tests/test_gpu_cp4.py (k_cp4 against k_cp3 and the oracle)
 #   dyntests    the dynamics test files (dynr, dyn_fuse, dyn3, variants)
 #   tests       the whole -m gpu suite
 #   smoke       __graft_entry__.smoke()
@@ -28,6 +29,8 @@ for step in "$@"; do
   case $step in
     dynr) timeout -k 10 500 $PYT tests/test_gpu_dynr.py > $out/pytest_dynr.log 2>&1 || fail $step $out/pytest_dynr.log
           tail -3 $out/pytest_dynr.log ;;
+    cp4) timeout -k 10 500 $PYT tests/test_gpu_cp4.py > $out/pytest_cp4.log 2>&1 || fail $step $out/pytest_cp4.log
+          tail -3 $out/pytest_cp4.log ;;
     dyntests) timeout -k 10 900 $PYT tests/test_gpu_dynr.py tests/test_gpu_dyn_split.py tests/test_gpu_dyn3.py tests/test_gpu_variants.py > $out/pytest_dyn.log 2>&1 || fail $step $out/pytest_dyn.log
           tail -3 $out/pytest_dyn.log ;;
     tests) timeout -k 10 1100 $PYT tests > $out/pytest_gpu.log 2>&1 || fail $step $out/pytest_gpu.log
