@@ -18,11 +18,14 @@ script starts the N rank processes itself before anything touches a GPU.
   value: every rank solves its own config-2 tree instance (an MPC-style batch of
       independent problems: same tree, its own x0), no collective on the data path;
       value = total CP iterations/s of the job (weak scaling).
-  sharded: ONE config-4 tree (BASELINE configs[3]: branching 3, N = 10, 88,573 nodes,
-      nx = 32, nu = 12) whose subtrees below the replicated top are sharded across the N
-      GPUs, with RCCL exchanges each iteration; CP iterations/s of that
-      one tree (strong scaling; N = 1 is the unsharded solve). Run by N fresh child
-      processes under a time limit so that a failure there cannot take the line down.
+  sharded: two strong-scaling legs, {"config4", "config5_fp32"}: ONE config-4 tree
+      (BASELINE configs[3]: branching 3, N = 10, 88,573 nodes, nx = 32, nu = 12, fp64) and
+      ONE config-5 tree (configs[4]: branching 4, N = 9, 349,525 nodes, nx = 64, nu = 16,
+      fp32) whose subtrees below the replicated top are sharded across the N GPUs
+      (SURVEY.md 8(e)), with RCCL exchanges each iteration; CP iterations/s of that one tree
+      (N = 1 is the unsharded solve, reported from the one-GPU legs below). At N > 1 each
+      leg runs as N fresh child processes under a time limit, so that a failure there
+      cannot take the line down.
 
 torch is never imported: its wheel bundles a second ROCm runtime with the same soname
 as the /opt/rocm one libraocp_hip.so links, and RCCL (dlopen'ed by the library) cannot
@@ -294,7 +297,8 @@ def timed_cp(nat, x0, alpha, steps, warmup, group):
 
 
 def shard_leg(args):
-    """One process of the sharded config-4 solve (a child of rank 0, see spawn)."""
+    """One process of a sharded solve (config 4 fp64 or config 5 fp32; a child of rank 0, see
+    spawn)."""
     import raocp.core as core
     from raocp.core._native import comm_unique_id, load_library
     from raocp.problems import build_problem, recipe_config
@@ -303,9 +307,9 @@ def shard_leg(args):
     rank = int(os.environ.get("RANK", "0"))
     group = SocketGroup(rank, world) if world > 1 else None
     recipe = recipe_config(args.shard_config, seed=0)
-    cache = core.Cache(build_problem(recipe)[1])
+    cache = core.Cache(build_problem(recipe)[1], dtype=args.shard_dtype)
     nat = cache.native
-    alpha = 0.999 / nat.step_size()
+    alpha = 0.999 / nat.step_size(rtol=1e-7 if args.shard_dtype == "float32" else 1e-14)
     if world > 1:
         nat.shard(rank, world)
         uid = group.bcast(comm_unique_id() if rank == 0 else b"")
@@ -320,14 +324,24 @@ def shard_leg(args):
         group.barrier()
 
 
-def sharded_entry(args, world):
-    """The config-4 strong-scaling leg: N = 1 in this process (no shards, no RCCL); N > 1 by
-    N fresh child processes (one per GPU) under a time limit."""
-    desc = {"config": f"SURVEY.md 8(d) config {args.shard_config} (BASELINE configs[{args.shard_config - 1}]): "
+# the strong-scaling legs: (config, dtype) — BASELINE configs[3] (config 4, fp64) and
+# configs[4] (config 5 in fp32, "report 1/2/4/8-GPU scaling")
+SHARD_LEGS = ((4, "float64"), (5, "float32"))
+
+
+def leg_key(cfg, dtype):
+    return f"config{cfg}" + ("_fp32" if dtype == "float32" else "")
+
+
+def sharded_entry(args, world, cfg, dtype, steps, warmup):
+    """One strong-scaling leg at N > 1: N fresh child processes (one per GPU) under a time
+    limit, ONE tree whose subtrees below the replicated top are sharded across them."""
+    desc = {"config": f"SURVEY.md 8(d) config {cfg} (BASELINE configs[{cfg - 1}]): "
                       "ONE tree, subtrees below the replicated top sharded across the GPUs",
-            "n_gpus": world, "steps": args.shard_steps, "unit": "it/s", "scaling": "strong"}
-    argv = ["--shard-leg", "--shard-config", str(args.shard_config), "--shard-steps", str(args.shard_steps),
-            "--shard-warmup", str(args.shard_warmup)]
+            "dtype": "f32" if dtype == "float32" else "f64",
+            "n_gpus": world, "steps": steps, "unit": "it/s", "scaling": "strong"}
+    argv = ["--shard-leg", "--shard-config", str(cfg), "--shard-dtype", dtype, "--shard-steps", str(steps),
+            "--shard-warmup", str(warmup)]
     out, rcs = spawn(world, argv, timeout=args.shard_timeout)
     line = [ln for ln in out.splitlines() if ln.startswith("{")]
     if any(rc != 0 for rc in rcs) or not line:
@@ -425,10 +439,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-hbm", action="store_true", help="skip the config-4 L / L^T measurement")
-    ap.add_argument("--no-shard", action="store_true", help="skip the sharded config-4 leg")
+    ap.add_argument("--no-shard", action="store_true", help="skip the sharded strong-scaling legs (configs 4, 5)")
     ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 config-5 leg")
     ap.add_argument("--fp32-steps", type=int, default=48)
-    ap.add_argument("--shard-config", type=int, default=4)
+    ap.add_argument("--shard-config", type=int, default=4, help=argparse.SUPPRESS)
+    ap.add_argument("--shard-dtype", default="float64", help=argparse.SUPPRESS)
     ap.add_argument("--shard-steps", type=int, default=200)
     ap.add_argument("--shard-warmup", type=int, default=20)
     ap.add_argument("--shard-timeout", type=float, default=240.0)
@@ -500,17 +515,23 @@ def main():
         "fp32_config5": fp32,
     }
     if not args.no_shard:
-        out["sharded"] = sharded_entry(args, world) if world > 1 else None
+        sharded = {}
+        for cfg, dtype in SHARD_LEGS:
+            steps, warmup = (args.shard_steps, args.shard_warmup) if dtype == "float64" else (args.fp32_steps, 2)
+            key = leg_key(cfg, dtype)
+            if world > 1:
+                sharded[key] = sharded_entry(args, world, cfg, dtype, steps, warmup)
+                continue
+            # the N = 1 point: the same tree unsharded in this process (the leg measured above)
+            leg = legs.get(key) or config_leg(cfg, dtype, steps, warmup, 40, 0)
+            sharded[key] = {"config": f"SURVEY.md 8(d) config {cfg} (BASELINE configs[{cfg - 1}]): ONE tree, "
+                                      "unsharded on 1 GPU (the N = 1 point of the strong-scaling leg)",
+                            "dtype": leg["dtype"], "n_gpus": 1, "steps": steps, "unit": "it/s", "scaling": "strong",
+                            "value": leg["cp"]["value"], "ms_per_step": leg["cp"]["ms_per_step"],
+                            "device_ms_per_step": leg["cp"]["device_ms_per_step"], "nodes": leg["nodes"]}
+        out["sharded"] = sharded
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(recipe, args.cpu_seconds)
-    if world == 1 and not args.no_shard:
-        # N = 1 point of the strong-scaling leg: the same config-4 tree unsharded in this process
-        c4 = (legs.get("config4") if args.shard_config == 4 else None) or config_leg(args.shard_config, "float64", args.shard_steps, args.shard_warmup, 200, 0)
-        out["sharded"] = {"config": f"SURVEY.md 8(d) config {args.shard_config} (BASELINE configs[{args.shard_config - 1}]): "
-                                    "ONE tree, unsharded on 1 GPU (the N = 1 point of the strong-scaling leg)",
-                          "n_gpus": 1, "steps": args.shard_steps, "unit": "it/s", "scaling": "strong",
-                          "value": c4["cp"]["value"], "ms_per_step": c4["cp"]["ms_per_step"],
-                          "device_ms_per_step": c4["cp"]["device_ms_per_step"], "nodes": c4["nodes"]}
     print(json.dumps(out), flush=True)
     if group:
         group.barrier()

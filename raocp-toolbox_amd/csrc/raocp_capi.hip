@@ -126,7 +126,8 @@ struct raocp_ctx {
     bool dr = false;
     raocp::DrPlan drp{};
     int dr_block = 512;
-    size_t dr_lds_up = 0, dr_lds_dn = 0;
+    size_t dr_lds = 0;
+    size_t dr_gran = 0;  // granules of each hand-off buffer
     double* x0 = nullptr;
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
     Ctl* ctl = nullptr;
@@ -652,10 +653,8 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
     if (c->dr && c->sh_S == 0 && part == 0) {  // the regular-tree sweep (raocp_dynr.hip)
         raocp::DrPlan p = c->drp;
         if (c->dev.stamps) p.stamps = c->dev.stamps;
-        raocp::dr_launch_up(p, c->nx, c->nu, c->dr_block, c->dr_lds_up, bf, zsel, ctl,
-                            ck ? *ck : raocp::ChkArg{nullptr, nullptr, nullptr, 0, 0}, c->stream);
-        if (c->dev.stamps) p.stamps = c->dev.stamps + 64;
-        raocp::dr_launch_down(p, c->nx, c->nu, c->dr_block, c->dr_lds_dn, bf, zsel, ctl, c->stream);
+        raocp::dr_launch(p, c->nx, c->nu, c->dr_lds, bf, zsel, ctl,
+                         ck ? *ck : raocp::ChkArg{nullptr, nullptr, nullptr, 0, 0}, c->stream);
         return;
     }
     if (c->dyn3) {
@@ -679,10 +678,12 @@ int fuse_err(raocp_ctx* c) {
         unsigned e = 0;
         HIPCHK(hipMemcpy(&e, c->drp.sync + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
         if (e) {
-            // clear every counter, flag, the epoch and the error word: the next projection
-            // starts from a clean protocol state
-            HIPCHK(hipMemset(c->drp.sync, 0, (2 + 2 * (size_t)c->drp.S) * sizeof(unsigned)));
-            return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dr_up / k_dr_down); "
+            // clear the epoch, the error word and every granule: the next projection starts
+            // from a clean protocol state
+            HIPCHK(hipMemset(c->drp.sync, 0, 2 * sizeof(unsigned)));
+            HIPCHK(hipMemset(c->drp.gq, 0, c->dr_gran * sizeof(unsigned long long)));
+            HIPCHK(hipMemset(c->drp.gx, 0, c->dr_gran * sizeof(unsigned long long)));
+            return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dr); "
                                          "RAOCP_DR=0 selects the tiered sweep");
         }
         return RAOCP_OK;
@@ -697,49 +698,56 @@ int fuse_err(raocp_ctx* c) {
 }
 
 // ---- the regular-tree sweep (raocp_dynr.hip) -----------------------------------------------
-// Tables in the kernels' LDS order, per nonleaf stage t (its class and the pairs of its child
-// slots, c->reg_st[t]):
-//   backward [R rows][KS slots][SX]: WT = [-Rinv B' ; A' - G B'] of slot k's pair (zero rows for
-//            k >= C), then [R rows][NUP]: RG = [Rinv ; G] of the class (zero tail);
-//   forward  [C slots][nx rows][SF]: [Abar_k | B_k], then [nu rows][SX]: K of the class.
-// The tier plan minimises a cost model of the critical path (us: per level a barrier and the
-// lane work of the backward and forward passes, per tier boundary one hand-off each way) over
-// cut lists of at most kDrMaxTiers tiers, with the whole grid (one workgroup per subtree of
-// every tier) within the CU count: every workgroup of a launch is then resident at once, so no
-// wait depends on the dispatch order. RAOCP_DR_CUTS="s1,s2,.." forces the cuts.
+// Tables in the kernel's LDS order, per nonleaf stage t (its class and the pairs of its child
+// slots, c->reg_st[t]), element-pair-major [p][lane][2] so lane s reads its row pair p as one
+// 16-B word:
+//   backward lane s = r KS + k (row r < nx + nu, slot k; LB = (nx + nu) KS lanes): WT = [-Rinv B' ; A' - G B'] row r of
+//            slot k's pair (zero for k >= C), then entries [k UP, (k + 1) UP) of RG = [Rinv ; G]
+//            row r of the class;
+//   forward  lane s = k nx + r (slot k, row r < nx; LF = C nx + nu lanes): [Abar_k | B_k] row r; lane C nx + r
+//            (r < nu): [K row r | unit vector e_r] (u_r = K x + d_r as one dot product).
+// The tier plan minimises a cost model of the critical path (us, fitted to measured cut lists:
+// per level of each sweep a fixed part and a part per node, per tier boundary its two
+// hand-offs) over cut lists of at most kDrMaxTiers tiers whose grid (one workgroup per subtree
+// of every tier, plus the stopping test) is resident at once (occupancy x CU count): no wait
+// then depends on the dispatch order. RAOCP_DR_CUTS="s1:s2:.." forces the cuts.
 int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::vector<double>& RG, int SNU,
              const std::vector<double>& KM, const std::vector<double>& F, int SKF, int n_cus) {
     const int nx = c->nx, nu = c->nu, C = c->reg_C, N = c->N, R = nx + nu;
-    const int KS = raocp::dr_ks(C), SX = raocp::dr_stride(nx), SF = raocp::dr_stride(nx + nu), NUP = raocp::dr_nup(nu, C);
-    const int nb = raocp::dr_back_n(nx, nu, C), nf = raocp::dr_fwd_n(nx, nu, C);
+    const int KS = raocp::dr_ks(C), UP = raocp::dr_up(nu, C), LB = raocp::dr_lb(nx, nu, C),
+              LF = raocp::dr_lf(nx, nu, C);
+    const int nb = raocp::dr_tb_n(nx, nu, C), nf = raocp::dr_tf_n(nx, nu, C);
     auto npow = [&](int e) {
         long v = 1;
         for (int i = 0; i < e; ++i) v *= C;
         return v;
     };
-    const size_t kLds = 160 * 1024 - 1024;  // minus the kernels' static LDS
+    if (N >= raocp::kDrMaxStages) return RAOCP_OK;  // the sweep stays off
+    int block = 512;
     // cost (us) of a cut list s = {0, s1, .., N}; 1e300 where it does not fit
-    int best_block = 512;
-    auto eval = [&](const std::vector<int>& s, int* block) -> double {
+    auto eval = [&](const std::vector<int>& s) -> double {
         const int T = (int)s.size() - 1;
         if (T < 1 || T > raocp::kDrMaxTiers) return 1e300;
-        long wgs = 0, maxitems = 0;
+        long wgs = 1;  // the stopping test
+        size_t lds = 0;
+        int lmax = 0;
         for (int k = 0; k < T; ++k) {
             const int L = s[k + 1] - s[k];
-            if (L < 1 || L > raocp::kDrMaxLevels) return 1e300;
+            if (L < 1 || L > raocp::kDrMaxL) return 1e300;
+            lmax = std::max(lmax, L);
             wgs += npow(s[k]);
-            if (raocp::dr_lds_up(nx, nu, C, L, k == T - 1) > kLds || raocp::dr_lds_down(nx, nu, C, L) > kLds) return 1e300;
-            maxitems = std::max(maxitems, npow(L - 1) * std::max<long>(R * KS, C * nx + nu));
+            lds = std::max(lds, raocp::dr_lds(nx, nu, C, L));
+            if (k + 1 < T && npow(L) * 2 * nx > (long)raocp::kDrMaxGran * block) return 1e300;
         }
-        if (wgs > n_cus) return 1e300;
-        const int B = maxitems > 512 ? 1024 : 512;
-        if (block) *block = B;
-        double cost = 4.0 * (T - 1);
+        if (lds > 160 * 1024 - 512) return 1e300;
+        const int occ = raocp::dr_occupancy(nx, nu, C, lmax, lds);
+        if (occ < 1 || wgs > (long)occ * n_cus) return 1e300;
+        // fitted to the config-2 cut lists measured on MI355X (profiles/r04_*/dr_cuts.log): a
+        // level 0.6 us plus 0.045 us per node beyond the first, each way; a tier boundary
+        // 2.5 us (its two hand-offs)
+        double cost = 2.5 * (T - 1);
         for (int k = 0; k < T; ++k)
-            for (int l = 0; l < s[k + 1] - s[k]; ++l) {
-                const long ib = npow(l) * R * KS, inf = npow(l) * (C * nx + nu);
-                cost += 0.24 + 0.05 * (double)((ib + B - 1) / B + (inf + B - 1) / B) + 4e-4 * ib + 6e-4 * inf;
-            }
+            for (int l = 0; l < s[k + 1] - s[k]; ++l) cost += 2 * (0.6 + 0.045 * (double)(npow(l) - 1));
         return cost;
     };
     std::vector<int> cuts;
@@ -753,7 +761,7 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
             p = *q ? q + 1 : q;
         }
         cuts.push_back(N);
-        if (!std::is_sorted(cuts.begin(), cuts.end()) || eval(cuts, &best_block) >= 1e299)
+        if (!std::is_sorted(cuts.begin(), cuts.end()) || eval(cuts) >= 1e299)
             return fail(RAOCP_ERR_ARG, std::string("RAOCP_DR_CUTS=") + e + ": not a valid tier plan for this tree");
     } else {
         double best = 1e300;
@@ -761,12 +769,10 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
         // every increasing cut list of at most kDrMaxTiers tiers
         auto rec = [&](auto&& self, int from) -> void {
             s.push_back(N);
-            int B = 512;
-            const double v = eval(s, &B);
+            const double v = eval(s);
             if (v < best) {
                 best = v;
                 cuts = s;
-                best_block = B;
             }
             s.pop_back();
             if ((int)s.size() >= raocp::kDrMaxTiers) return;
@@ -783,19 +789,24 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
     for (int t = 0; t < N; ++t) {
         const raocp::Dy3Stage& st = c->reg_st[t];
         double* b = &bimg[(size_t)t * nb];
-        for (int r = 0; r < R; ++r) {
-            for (int k = 0; k < C; ++k)
-                for (int e = 0; e < nx; ++e) b[((size_t)r * KS + k) * SX + e] = WT[((size_t)st.pair[k] * R + r) * SKP + e];
-            for (int e = 0; e < nu; ++e)
-                b[(size_t)R * KS * SX + (size_t)r * NUP + e] = RG[((size_t)st.cls * R + r) * SNU + e];
-        }
+        auto bset = [&](int e, int lane, double v) { b[((size_t)(e / 2) * LB + lane) * 2 + (e & 1)] = v; };
+        for (int r = 0; r < R; ++r)
+            for (int k = 0; k < KS; ++k) {
+                const int lane = r * KS + k;
+                if (k < C)
+                    for (int e = 0; e < nx; ++e) bset(e, lane, WT[((size_t)st.pair[k] * R + r) * SKP + e]);
+                for (int e = 0; e < UP && k * UP + e < nu; ++e)
+                    bset(nx + e, lane, RG[((size_t)st.cls * R + r) * SNU + k * UP + e]);
+            }
         double* f = &fimg[(size_t)t * nf];
+        auto fset = [&](int e, int lane, double v) { f[((size_t)(e / 2) * LF + lane) * 2 + (e & 1)] = v; };
         for (int k = 0; k < C; ++k)
             for (int r = 0; r < nx; ++r)
-                for (int e = 0; e < nx + nu; ++e)
-                    f[((size_t)k * nx + r) * SF + e] = F[((size_t)st.pair[k] * nx + r) * SKF + e];
-        for (int r = 0; r < nu; ++r)
-            for (int e = 0; e < nx; ++e) f[(size_t)C * nx * SF + (size_t)r * SX + e] = KM[((size_t)st.cls * nu + r) * SKP + e];
+                for (int e = 0; e < nx + nu; ++e) fset(e, k * nx + r, F[((size_t)st.pair[k] * nx + r) * SKF + e]);
+        for (int r = 0; r < nu; ++r) {
+            for (int e = 0; e < nx; ++e) fset(e, C * nx + r, KM[((size_t)st.cls * nu + r) * SKP + e]);
+            fset(nx + r, C * nx + r, 1.0);
+        }
     }
     raocp::DrPlan& p = c->drp;
     memset(&p, 0, sizeof(p));
@@ -803,44 +814,44 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
     p.T = T;
     p.C = C;
     p.N = N;
-    int w = 0, bup = 0;
-    for (int k = T - 1; k >= 0; --k) {  // k_dr_up: the deepest tier first
-        p.t[k].bup = bup;
-        bup += (int)npow(cuts[k]);
+    int w = 0, b0 = 0;
+    for (int k = T - 1; k >= 0; --k) {  // the deepest tier first, the top last
+        p.t[k].b0 = b0;
+        b0 += (int)npow(cuts[k]);
     }
+    c->dr_lds = 0;
     for (int k = 0; k < T; ++k) {
         raocp::DrTier& tt = p.t[k];
         tt.s0 = cuts[k];
         tt.L = cuts[k + 1] - cuts[k];
         tt.nsub = (int)npow(cuts[k]);
-        tt.bdn = w;  // k_dr_down: the top first
         tt.w0 = w;
         w += tt.nsub;
-        c->dr_lds_up = std::max(c->dr_lds_up, raocp::dr_lds_up(nx, nu, C, tt.L, k == T - 1));
-        c->dr_lds_dn = std::max(c->dr_lds_dn, raocp::dr_lds_down(nx, nu, C, tt.L));
+        c->dr_lds = std::max(c->dr_lds, raocp::dr_lds(nx, nu, C, tt.L));
     }
-    p.nblk = w;
-    p.S = w;
+    p.nblk = b0;
+    for (int t = 0; t <= N; ++t) p.sbase[t] = (int)((npow(t) - 1) / (C - 1));
     p.X0 = c->dev.X0;
     p.U0 = c->dev.U0;
-    c->dr_block = best_block;
-    if (const char* e = getenv("RAOCP_DR_BLOCK")) c->dr_block = atoi(e) > 512 ? 1024 : 512;
+    c->dr_block = block;
     // diagnostics (tests/test_gpu_dynr.py): RAOCP_DR_FAULT=1 makes the deepest tier's first
-    // subtree skip its arrival, so its parent's wait times out
+    // subtree skip its publish, so its parent's wait times out
     if (const char* e = getenv("RAOCP_DR_FAULT")) p.fault = atoi(e);
     int rc;
     const double *bi = nullptr, *fi = nullptr;
-    double *qb = nullptr, *db = nullptr;
+    unsigned long long *gq = nullptr, *gx = nullptr;
     unsigned* sy = nullptr;
-    if ((rc = c->upload_vec(&bi, bimg)) || (rc = c->upload_vec(&fi, fimg)) || (rc = c->alloc(&qb, (size_t)c->n * nx)) ||
-        (rc = c->alloc(&db, (size_t)c->m * nu)) || (rc = c->alloc(&sy, 2 + 2 * (size_t)w)))
+    c->dr_gran = (size_t)w * 2 * nx;
+    if ((rc = c->upload_vec(&bi, bimg)) || (rc = c->upload_vec(&fi, fimg)) || (rc = c->alloc(&gq, c->dr_gran)) ||
+        (rc = c->alloc(&gx, c->dr_gran)) || (rc = c->alloc(&sy, 2)))
         return rc;
-    HIPCHK(hipMemset(sy, 0, (2 + 2 * (size_t)w) * sizeof(unsigned)));
-    HIPCHK(hipMemset(qb, 0, (size_t)c->n * nx * sizeof(double)));
+    HIPCHK(hipMemset(sy, 0, 2 * sizeof(unsigned)));
+    HIPCHK(hipMemset(gq, 0, c->dr_gran * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(gx, 0, c->dr_gran * sizeof(unsigned long long)));
     p.bimg = bi;
     p.fimg = fi;
-    p.qbuf = qb;
-    p.dbuf = db;
+    p.gq = gq;
+    p.gx = gx;
     p.sync = sy;
     long long ms = 1000;  // a wait normally lasts microseconds
     if (const char* e = getenv("RAOCP_FUSE_TIMEOUT_MS")) ms = std::max(1, atoi(e));
@@ -849,7 +860,10 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
     if (getenv("RAOCP_DYN_VERBOSE")) {
         fprintf(stderr, "[raocp] regular sweep: %d tiers,", T);
         for (int k = 0; k < T; ++k) fprintf(stderr, " [%d,%d) x%d", p.t[k].s0, p.t[k].s0 + p.t[k].L, p.t[k].nsub);
-        fprintf(stderr, "; %d lanes, LDS %zu / %zu B\n", c->dr_block, c->dr_lds_up, c->dr_lds_dn);
+        int lmax = 0;
+        for (int k = 0; k < T; ++k) lmax = std::max(lmax, p.t[k].L);
+        fprintf(stderr, "; %d lanes, LDS %zu B, occupancy %d\n", c->dr_block, c->dr_lds,
+                raocp::dr_occupancy(nx, nu, C, lmax, c->dr_lds));
     }
     return RAOCP_OK;
 }
@@ -1249,7 +1263,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             };
             auto b = [](bool v) { return std::string(v ? "true" : "false"); };
             if (c->dr && c->sh_S == 0) {
-                return std::string(raocp::dr_name_up(c->nx, c->nu)) + " x1 + " + raocp::dr_name_down(c->nx, c->nu) + " x1";
+                return std::string(raocp::dr_name(c->nx, c->nu)) + " x1";
             } else if (c->dyn3) {  // one backward and one forward launch per nonleaf stage
                 for (int t = 0; t < c->N; ++t) add("k_dy3_back<" + T + ", " + nn + ">");
                 for (int t = 0; t < c->N; ++t) add("k_dy3_fwd<" + T + ", " + nn + ">");

@@ -113,7 +113,7 @@ def test_dyn3_deferred_stopping_test_matches_eager(iters, stop):
 
 def test_kernel_info_lists_the_projection_launches():
     """raocp_kernel_info(9) names every launch of one projection as "name xcount" terms
-    (bench.py sums their PMC traffic): the regular-tree sweep (k_dr_up + k_dr_down) at config 2;
+    (bench.py sums their PMC traffic): the regular-tree sweep (one k_dr) at config 2;
     with RAOCP_DR=0 the split sweep (k_dyn_up + k_dyn_down), the tier launches (2 tiers + the
     top) with RAOCP_DYN_SPLIT=0 too, one k_dy3_back and one k_dy3_fwd per nonleaf stage with
     RAOCP_DYN3=1."""
@@ -130,7 +130,7 @@ def test_kernel_info_lists_the_projection_launches():
         if want == "dy3":
             assert cnt == {"k_dy3_back": 12, "k_dy3_fwd": 12}
         elif want == "dr":
-            assert cnt == {"k_dr_up": 1, "k_dr_down": 1}
+            assert cnt == {"k_dr": 1}
         elif want == "split":
             assert cnt == {"k_dyn_up": 1, "k_dyn_down": 1}
         else:

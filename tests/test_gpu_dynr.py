@@ -1,15 +1,14 @@
-"""GPU parity of the regular-tree dynamics sweep k_dr_up / k_dr_down (raocp_dynr.hip;
-cache.py:259-288): one workgroup per subtree of every tier, counters of arrivals up the
-tiers, epoch flags down, every node address computed from (stage, subtree). The default of
-fp64 regular trees at nx = 20, nu = 8 (config 2); RAOCP_DR=0 falls back to the tiered sweep
-(raocp_dynf.hip / raocp_dyn.hip).
+"""GPU parity of the regular-tree dynamics sweep k_dr (raocp_dynr.hip; cache.py:259-288): one
+launch, one workgroup per subtree of every tier running its backward and forward sweeps, the
+q rows up and the x rows down as tagged 8-byte granules, every node address computed from
+(stage, subtree). The default of fp64 regular trees at nx = 20, nu = 8 (config 2);
+RAOCP_DR=0 falls back to the tiered sweep (raocp_dynf.hip / raocp_dyn.hip).
 
 Tolerances: the projection against the oracle within 1e-12 of the largest entry and exact
 feasibility x_j = A_j x_i + B_j u_i to 1e-12; against the tiered sweep (the same algebra, a
 different summation order) 1e-13 of the largest entry; the CP loop against the tiered sweep
 1e-10 per trace entry and the oracle 1e-8 (BASELINE.json north_star); the projection after
-1,000 graph-replayed launches (counters reset and epoch advanced inside the kernels) bit for
-bit; a forced hand-off timeout reported as an error within a fraction of a second.
+1,000 back-to-back launches (the tag advanced inside the kernel) bit for bit; a forced hand-off timeout reported as an error within a fraction of a second.
 """
 import os
 import time
@@ -59,7 +58,7 @@ def _project(cache, r, zz):
     return cache.native.get_primal()
 
 
-@pytest.mark.parametrize("cuts", [None, "4,7", "6", "3,6,9", "2"])
+@pytest.mark.parametrize("cuts", [None, "4,8", "6", "3,6,9", "2", "3,7"])
 @pytest.mark.parametrize("cfg", ["c2", "quad", "tri", "bin10", "bin3"])
 def test_dr_projection_matches_oracle_and_tiers(cfg, cuts):
     from oracle.raocp_oracle import OracleProblem
@@ -71,7 +70,7 @@ def test_dr_projection_matches_oracle_and_tiers(cfg, cuts):
     except Exception as e:  # a forced cut list this tree cannot take
         assert cuts and "RAOCP_DR_CUTS" in str(e)
         pytest.skip(f"cuts {cuts} invalid for {cfg}")
-    assert dr.native.kernel_info(9) == "k_dr_up<20, 8> x1 + k_dr_down<20, 8> x1"
+    assert dr.native.kernel_info(9) == "k_dr<20, 8> x1"
     tiers = _with_env(TIERS, lambda: core.Cache(prob))
     assert "k_dr_" not in tiers.native.kernel_info(9)
     zz = np.random.default_rng(5).standard_normal(dr.primal_size)
@@ -83,8 +82,8 @@ def test_dr_projection_matches_oracle_and_tiers(cfg, cuts):
     X = z1[orc.X0:orc.U0].reshape(orc.n, orc.nx)
     U = z1[orc.U0:orc.Y0].reshape(orc.m, orc.nu)
     j = np.arange(1, orc.n)
-    pred = np.einsum("jab,jb->ja", orc.A[orc.iA[j]], X[orc.anc[j]]) + \
-        np.einsum("jab,jb->ja", orc.B[orc.iB[j]], U[orc.anc[j]])
+    pred = np.einsum("jab,jb->ja", np.stack(orc.A)[orc.iA[j]], X[orc.anc[j]]) + \
+        np.einsum("jab,jb->ja", np.stack(orc.B)[orc.iB[j]], U[orc.anc[j]])
     assert np.max(np.abs(X[j] - pred)) <= 1e-12 * max(1.0, np.max(np.abs(X)))
     assert np.array_equal(X[0], np.asarray(r["x0"], float))
     # everything outside (x, u) untouched
@@ -93,13 +92,13 @@ def test_dr_projection_matches_oracle_and_tiers(cfg, cuts):
 
 def test_dr_cp_loop_matches_tiers_and_oracle():
     """30 CP iterations (a full 24-iteration graph batch plus a remainder; the deferred
-    stopping test rides on k_dr_up), tol = 0."""
+    stopping test rides on k_dr), tol = 0."""
     from oracle.raocp_oracle import OracleProblem
     r = recipe_config(2)
     tree, prob = build_problem(r)
     dr = core.Cache(prob)
     tiers = _with_env(TIERS, lambda: core.Cache(prob))
-    assert dr.native.kernel_info(9).startswith("k_dr_up")
+    assert dr.native.kernel_info(9).startswith("k_dr<")
     alpha = 0.999 / dr.native.step_size()
     out = []
     for cache in (dr, tiers):
@@ -115,13 +114,13 @@ def test_dr_cp_loop_matches_tiers_and_oracle():
 
 @pytest.mark.parametrize("iters,stop", [(1, None), (24, None), (30, None), (60, True)])
 def test_dr_deferred_stopping_test_matches_eager(iters, stop):
-    """The deferred stopping test (an extra workgroup of k_dr_up) against k_cp_check after
+    """The deferred stopping test (an extra workgroup of k_dr) against k_cp_check after
     every iteration (RAOCP_DEFER_CHECK=0): bit for bit, early stops included."""
     r = recipe_config(2)
     tree, prob = build_problem(r)
     dfr = core.Cache(prob)
     eag = _with_env({"RAOCP_DEFER_CHECK": "0"}, lambda: core.Cache(prob))
-    assert dfr.native.kernel_info(9).startswith("k_dr_up")
+    assert dfr.native.kernel_info(9).startswith("k_dr<")
     alpha = 0.999 / dfr.native.step_size()
     tol = 0.0
     if stop:
@@ -138,9 +137,8 @@ def test_dr_deferred_stopping_test_matches_eager(iters, stop):
 
 
 def test_dr_many_launches_then_projection():
-    """1,000 back-to-back launches (graph-replayed, as in the CP loop): the counters are reset
-    by their consumers and the epoch advances inside the kernels; a projection afterwards is
-    the same bit for bit."""
+    """1,000 back-to-back launches: the tag advances inside the kernel (the top stores it when
+    every workgroup has read it); a projection afterwards is the same bit for bit."""
     r = recipe_config(2)
     tree, prob = build_problem(r)
     dr = core.Cache(prob)
@@ -153,10 +151,11 @@ def test_dr_many_launches_then_projection():
 
 
 def test_dr_forced_timeout_is_reported_quickly():
-    """RAOCP_DR_FAULT=1: the deepest tier's first subtree never arrives, so its parent's wait
-    times out (RAOCP_FUSE_TIMEOUT_MS=5), sets the error word and leaves; every workgroup of a
-    later launch sees the word at its start and leaves at once. The projection raises, and
-    so does the next one, each within a fraction of a second (not a 1 s wait per tier)."""
+    """RAOCP_DR_FAULT=1: the deepest tier's first subtree never publishes its q row, so its
+    parent's wait times out (RAOCP_FUSE_TIMEOUT_MS=5), sets the error word and leaves, and the
+    waits on that parent time out in turn; the projection raises within a fraction of a
+    second, the host clears the words and the granules, and the next projection raises the
+    same way (not a 1 s wait per tier)."""
     r = recipe_config(2)
     tree, prob = build_problem(r)
     bad = _with_env({"RAOCP_DR_FAULT": "1", "RAOCP_FUSE_TIMEOUT_MS": "5"}, lambda: core.Cache(prob))

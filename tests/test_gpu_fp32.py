@@ -128,10 +128,10 @@ def test_fp32_node_block_kernels_match_mfma_kernels():
 
 
 def test_fp32_dynamics_projection_config5(c5):
-    """The per-stage MFMA dynamics sweep (raocp_dyn2.hip) in fp32 at config 5 against the
-    fp64 oracle (cache.py:259-288): 2e-5 relative to the largest entry (a backward and a
-    forward recursion of 9 stages of 64 x 80 products), and feasibility x_j = A_j x_i + B_j u_i
-    of its output to fp32 accuracy."""
+    """The per-stage dynamics sweep k_dy3<float> (raocp_dyn3.hip: per-stage table images,
+    MFMA node blocks) at config 5 against the fp64 oracle (cache.py:259-288): 2e-5 relative to
+    the largest entry (a backward and a forward recursion of 9 stages of 64 x 80 products),
+    and feasibility x_j = A_j x_i + B_j u_i of its output to fp32 accuracy."""
     r, prob, cache, orc = c5
     rng = np.random.default_rng(17)
     zz = rng.standard_normal(cache.primal_size)
@@ -163,3 +163,54 @@ def test_fp32_cp_loop_config5_vs_oracle(c5):
     assert np.max(np.abs(derr - derr_o) / np.abs(derr_o)) <= 1e-3
     assert rel_err(cache.get_primal_flat(), z_o) <= 1e-4
     assert rel_err(cache.get_dual_flat(), e_o) <= 1e-4
+
+
+def _c5_fixture(golden):
+    try:
+        return golden("c5_cp")
+    except FileNotFoundError:
+        pytest.skip("tests/golden/c5_cp.npz missing (tests/golden/gen_c5_cp.py)")
+
+
+def _c5_against_fixture(cache, fx, K, x0):
+    """cp_run of K iterations (tol = 0) at the fixture's step size; the oracle's K-iteration
+    traces and iterate samples / norms (tests/golden/gen_c5_cp.py)."""
+    alpha = float(fx["alpha"])
+    status, err, derr = cache.native.cp_run(x0, K - 1, 0.0, alpha)
+    z, eta = cache.get_primal_flat(), cache.get_dual_flat()
+    pre = f"k{K}/"
+    assert status == 1 and err.shape == fx[pre + "err"].shape == (K, 3)
+    te = float(np.max(np.abs(err - fx[pre + "err"]) / np.abs(fx[pre + "err"])))
+    td = float(np.max(np.abs(derr - fx[pre + "derr"]) / np.abs(fx[pre + "derr"])))
+    zs = float(np.max(np.abs(z[fx["ip"]] - fx[pre + "z_sample"])) / fx[pre + "z_norms"][1])
+    es = float(np.max(np.abs(eta[fx["id"]] - fx[pre + "eta_sample"])) / fx[pre + "eta_norms"][1])
+    zn = abs(np.linalg.norm(z) / fx[pre + "z_norms"][0] - 1)
+    en = abs(np.linalg.norm(eta) / fx[pre + "eta_norms"][0] - 1)
+    print(f"config 5, {K} iterations: traces {te:.2e} / {td:.2e}, iterate samples {zs:.2e} / {es:.2e}, "
+          f"norms {zn:.2e} / {en:.2e}")
+    return te, td, zs, es, zn, en
+
+
+def test_fp32_cp_loop_config5_20_iterations_vs_oracle(c5, golden):
+    """20 iterations of the fp32 CP loop at config 5 (k_cp3<float, 64, 16> + k_dy3<float>)
+    against the fp64 oracle at the oracle's own step size (c5_cp.npz: the oracle's traces and
+    iterate samples, 6 min of CPU per run, hence stored). Tolerances from fp32 rounding
+    through 20 nonexpansive CP steps: the residual traces 2e-3 relative per entry, the iterate
+    samples 2e-4 of the largest entry, the iterate norms 1e-4 relative."""
+    r, prob, cache, orc = c5
+    fx = _c5_fixture(golden)
+    assert np.array_equal(fx["x0"], np.asarray(r["x0"], float))
+    te, td, zs, es, zn, en = _c5_against_fixture(cache, fx, 20, r["x0"])
+    assert te <= 2e-3 and td <= 2e-3 and zs <= 2e-4 and es <= 2e-4 and zn <= 1e-4 and en <= 1e-4
+
+
+def test_fp64_config5_path_10_iterations_vs_oracle(golden):
+    """The fp64 context at nx = 64, nu = 16 (the reference the fp32 drift test of
+    test_gpu_cp3.py compares with: k_cpd2 / k_cpp2<double> + k_dy3<double, 64, 16>) for 10
+    iterations against the oracle (c5_cp.npz): traces 1e-8 relative per entry (BASELINE.json
+    north_star), iterate samples 1e-10 of the largest entry."""
+    r = recipe_config(5)
+    fx = _c5_fixture(golden)
+    cache = core.Cache(build_problem(r)[1])
+    te, td, zs, es, zn, en = _c5_against_fixture(cache, fx, 10, r["x0"])
+    assert te <= 1e-8 and td <= 1e-8 and zs <= 1e-10 and es <= 1e-10 and zn <= 1e-12 and en <= 1e-12

@@ -94,7 +94,7 @@ def test_sharded_solve_matches_unsharded(cfg, R, kern):
     other = _kern_cache(prob, "two" if kern == "fused" else "fused")
     stf, errf, _ = other.native.cp_run(r["x0"], iters, 0.0, alpha)
     assert stf == st0 and np.max(np.abs(errf - err0) / np.abs(err0)) <= 1e-10
-    # the unsharded default (config 2: the regular-tree sweep k_dr_up / k_dr_down)
+    # the unsharded default (config 2: the regular-tree sweep k_dr)
     dflt = core.Cache(prob)
     std, errd, _ = dflt.native.cp_run(r["x0"], iters, 0.0, alpha)
     assert std == st0 and np.max(np.abs(errd - err0) / np.abs(err0)) <= 1e-10

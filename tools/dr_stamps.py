@@ -1,7 +1,9 @@
-"""Diagnostics: in-kernel stamps of the regular-tree sweep (raocp_dynr.hip). For the first
-subtree of every tier, k_dr_up stamps [start, (children arrived), prologue landed, levels
-done, published] and k_dr_down [start, (parent's flag seen), root x in LDS, levels done,
-flag set]; printed in ns from the launch's earliest stamp (100 MHz clock).
+"""Diagnostics: in-kernel stamps of the regular-tree sweep k_dr (raocp_dynr.hip). For the first
+subtree of every tier the kernel stamps [start, (prologue landed: RAOCP_DR_FAULT bit 1),
+(children's q rows landed), the start of every backward level, backward sweep done, (root's
+x row landed), the start of every forward level, forward sweep done, written out] and the end,
+printed in ns from the launch's earliest stamp (100 MHz clock), and the shader clock over the
+workgroup's span (s_memtime cycles / ns).
 usage: python tools/dr_stamps.py [config] [reps]"""
 import os
 import sys
@@ -23,15 +25,15 @@ for rep in range(reps):
     st = cache.native.debug_dyn_stamps(4096).astype(np.int64)
     if rep < reps - 3:
         continue
-    for name, base in (("up", 0), ("down", 64)):
-        blk = st[base:base + 64].reshape(4, 16)
-        live = blk[blk != 0]
-        if live.size == 0:
-            continue
-        t0 = live.min()
-        rows = []
-        for k in range(4):
-            v = blk[k][blk[k] != 0]
-            if v.size:
-                rows.append(f"tier {k}: " + " ".join(f"{(x - t0) * 10:6d}" for x in v))
-        print(f"rep {rep} {name:4s} " + " | ".join(rows), flush=True)
+    blk = st[0:128].reshape(4, 32)
+    live = blk[:, :31][blk[:, :31] != 0]
+    if live.size == 0:
+        continue
+    t0 = live.min()
+    for k in range(4):
+        v = blk[k][:30][blk[k][:30] != 0]
+        if v.size:
+            span = (blk[k][30] - v[0]) * 10
+            ghz = blk[k][31] / span if span > 0 else 0.0
+            print(f"rep {rep} tier {k}: " + " ".join(f"{(x - t0) * 10:6d}" for x in v) +
+                  f" | end {(blk[k][30] - t0) * 10:6d}  clock {ghz:.2f} GHz", flush=True)
