@@ -110,12 +110,31 @@ struct Dma {
 
 // every lane polls granules g = tid + i * blockDim (g < n) of src until each carries tag, and
 // puts their halves at dst[g]; false (error word set) on a timeout
-__device__ __forceinline__ bool poll_gran(const unsigned long long* src, int n, unsigned tag, ldsu* dst,
+//
+// The wait itself is one wave's: its lanes poll the last granule of each of the rows rows
+// (sleeping between rounds) while the other waves sit at the barrier; then every lane reads
+// its granules (normally all there) and re-polls only the missing ones.
+__device__ __forceinline__ bool poll_gran(const unsigned long long* src, int n, int rows, unsigned tag, ldsu* dst,
                                           long long timeout, unsigned* sync, int& s_ok) {
-    const int tid = threadIdx.x, bs = blockDim.x;
-    unsigned got = 0;
+    const int tid = threadIdx.x, bs = blockDim.x, G = n / rows;
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     bool bad = false;
+    if (tid < 64) {
+        for (int r0 = 0; r0 < rows && !bad; r0 += 64) {
+            const int r = r0 + tid;
+            for (;;) {
+                const bool ok = r >= rows || (unsigned)(ld_gran(src + (size_t)r * G + G - 1) >> 32) == tag;
+                if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+                    bad = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
+            }
+        }
+    }
+    __syncthreads();
+    unsigned got = 0;
     for (;;) {
         unsigned long long v[kDrMaxGran];
         _Pragma("unroll") for (int i = 0; i < kDrMaxGran; ++i) {
@@ -134,7 +153,7 @@ __device__ __forceinline__ bool poll_gran(const unsigned long long* src, int n, 
                 }
             }
         }
-        if (all) break;
+        if (all || bad) break;
         if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
             bad = true;
             break;
@@ -223,10 +242,12 @@ __device__ __forceinline__ void back_level(const ldsd* tb, ldsd* xd, const ldsd*
     int nn[UN];
     _Pragma("unroll") for (int h = 0; h < UN; ++h) nn[h] = n0 + h < cnt ? n0 + h : n0;
     d2v q[UN][NX / 2], u[UN][UP / 2];
+    double xo[UN];  // x_i entry r - NU (read with the rows: q_i = acc - x_i)
     _Pragma("unroll") for (int p = 0; p < NX / 2; ++p)
         _Pragma("unroll") for (int h = 0; h < UN; ++h) q[h][p] = ld2(qk + nn[h] * C * qs + 2 * p);
     _Pragma("unroll") for (int p = 0; p < UP / 2; ++p)
         _Pragma("unroll") for (int h = 0; h < UN; ++h) u[h][p] = ld2(uk + nn[h] * NU + 2 * p);
+    _Pragma("unroll") for (int h = 0; h < UN; ++h) xo[h] = xd[nn[h] * SXD + (r >= NU && live ? r - NU : 0)];
     _Pragma("unroll") for (int h = 0; h < UN; ++h) {
         d2v a = {0.0, 0.0}, b = {0.0, 0.0}, c = {0.0, 0.0};
         _Pragma("unroll") for (int p = 0; p < NX / 2; p += 2) {
@@ -237,12 +258,8 @@ __device__ __forceinline__ void back_level(const ldsd* tb, ldsd* xd, const ldsd*
         const double acc = ks_sum<KS>(sign * ((a.x + a.y) + (b.x + b.y)) + (c.x + c.y));
         if (live && k == 0 && (h == 0 || n0 + h < cnt)) {
             ldsd* row = xd + nn[h] * SXD;
-            if (r < NU) {
-                row[NX + r] = acc;
-            } else {
-                const double xr = row[r - NU];
-                row[r - NU] = acc - xr;
-            }
+            if (r < NU) row[NX + r] = acc;
+            else row[r - NU] = acc - xo[h];
         }
     }
     }
@@ -368,7 +385,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     // ---- 2. the child subtrees' q rows
     if (!deepest) {
         const DrTier& ct = pl.t[k + 1];
-        if (!poll_gran(pl.gq + (size_t)(ct.w0 + o * NB) * G, NB * G, tag, (ldsu*)XL, pl.timeout, pl.sync, s_ok)) {
+        if (!poll_gran(pl.gq + (size_t)(ct.w0 + o * NB) * G, NB * G, NB, tag, (ldsu*)XL, pl.timeout, pl.sync, s_ok)) {
             dma_wait();
             return;
         }
@@ -403,7 +420,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
                 constexpr int f = fc.value;
                 TF::issue(SL + (L - 1 - f) * SLOT, pl.fimg + (size_t)(s0 + f) * TFN);
             });
-        if (!poll_gran(pl.gx + (size_t)(tt.w0 + o) * G, G, tag, (ldsu*)XD, pl.timeout, pl.sync, s_ok)) {
+        if (!poll_gran(pl.gx + (size_t)(tt.w0 + o) * G, G, 1, tag, (ldsu*)XD, pl.timeout, pl.sync, s_ok)) {
             dma_wait();
             return;
         }
@@ -452,8 +469,11 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
 
 // LMAX: the deepest tier body compiled in (a plan whose subtrees have at most LMAX levels runs
 // the instantiation of its largest L: small plans keep the registers of small levels)
+// (waves per SIMD: two workgroups per CU at LMAX <= 4, else one; the register budget is then
+// 128 / 256 VGPRs and the scheduler keeps a level's LDS reads in flight together)
 template <int NX, int NU, int C, int BS, int LMAX>
-__global__ void __launch_bounds__(BS) k_dr(DrPlan pl, Bufs bf, int zsel, const Ctl* __restrict__ ctl, ChkArg ck) {
+__global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LMAX <= 4 ? 4 : 2, LMAX <= 4 ? 4 : 2)))
+k_dr(DrPlan pl, Bufs bf, int zsel, const Ctl* __restrict__ ctl, ChkArg ck) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Stamps stp;
     __shared__ int s_ok;

@@ -113,17 +113,19 @@ def test_dyn3_deferred_stopping_test_matches_eager(iters, stop):
 
 def test_kernel_info_lists_the_projection_launches():
     """raocp_kernel_info(9) names every launch of one projection as "name xcount" terms
-    (bench.py sums their PMC traffic): the regular-tree sweep (one k_dr) at config 2;
-    with RAOCP_DR=0 the split sweep (k_dyn_up + k_dyn_down), the tier launches (2 tiers + the
-    top) with RAOCP_DYN_SPLIT=0 too, one k_dy3_back and one k_dy3_fwd per nonleaf stage with
-    RAOCP_DYN3=1."""
+    (bench.py sums their PMC traffic): the regular-tree sweep (one k_dr) at config 2; with
+    RAOCP_DR=0 the tier launches (2 tiers + the top: the split sweep's grid of 274
+    workgroups is not co-resident there), the same with RAOCP_DYN_SPLIT=0, one k_dy3_back and
+    one k_dy3_fwd per nonleaf stage with RAOCP_DYN3=1; the split sweep (k_dyn_up + k_dyn_down)
+    on a co-resident tree of a size k_dr does not take (nx = 32, nu = 12, 3,280 nodes)."""
     import re
     r = recipe_config(2)
     prob = build_problem(r)[1]
     off = {"RAOCP_DR": "0"}
-    for env, want in (({}, "dr"), (off, "split"), ({**off, "RAOCP_DYN_SPLIT": "0"}, None),
-                      ({"RAOCP_DYN3": "1"}, "dy3")):
-        cache = _with_env(env, lambda: core.Cache(prob))
+    t32 = build_problem(recipe_synthetic(np.full((3, 3), 1 / 3), np.full(3, 1 / 3), 7, 7, 32, 12, seed=7))[1]
+    for env, want, pb in (({}, "dr", prob), (off, None, prob), ({**off, "RAOCP_DYN_SPLIT": "0"}, None, prob),
+                          ({"RAOCP_DYN3": "1"}, "dy3", prob), ({}, "split", t32)):
+        cache = _with_env(env, lambda: core.Cache(pb))
         terms = [re.fullmatch(r"(k_\w+<[^>]*>) x(\d+)", t) for t in cache.native.kernel_info(9).split(" + ")]
         assert all(terms), cache.native.kernel_info(9)
         cnt = {m.group(1).split("<")[0]: int(m.group(2)) for m in terms}

@@ -58,18 +58,20 @@ def _project(cache, r, zz):
     return cache.native.get_primal()
 
 
-@pytest.mark.parametrize("cuts", [None, "4,8", "6", "3,6,9", "2", "3,7"])
-@pytest.mark.parametrize("cfg", ["c2", "quad", "tri", "bin10", "bin3"])
+# (tree, forced cut list): the planner's own plan and the resident plans of other depths
+# (config 2: [0,6)+[6,12) runs the LMAX = 6 build, the rest the LMAX = 4 one)
+CASES = [("c2", None), ("c2", "4,8"), ("c2", "6"), ("c2", "3,7"), ("quad", None), ("quad", "2"), ("quad", "3"),
+         ("tri", None), ("tri", "3"), ("tri", "4"), ("bin10", None), ("bin10", "4,8"), ("bin10", "6"),
+         ("bin10", "3,7"), ("bin3", None)]
+
+
+@pytest.mark.parametrize("cfg,cuts", CASES)
 def test_dr_projection_matches_oracle_and_tiers(cfg, cuts):
     from oracle.raocp_oracle import OracleProblem
     r = _recipe(cfg)
     tree, prob = build_problem(r)
     env = {"RAOCP_DR_CUTS": cuts} if cuts else {}
-    try:
-        dr = _with_env(env, lambda: core.Cache(prob))
-    except Exception as e:  # a forced cut list this tree cannot take
-        assert cuts and "RAOCP_DR_CUTS" in str(e)
-        pytest.skip(f"cuts {cuts} invalid for {cfg}")
+    dr = _with_env(env, lambda: core.Cache(prob))
     assert dr.native.kernel_info(9) == "k_dr<20, 8> x1"
     tiers = _with_env(TIERS, lambda: core.Cache(prob))
     assert "k_dr_" not in tiers.native.kernel_info(9)
@@ -88,6 +90,14 @@ def test_dr_projection_matches_oracle_and_tiers(cfg, cuts):
     assert np.array_equal(X[0], np.asarray(r["x0"], float))
     # everything outside (x, u) untouched
     assert np.array_equal(z1[orc.Y0:], zz[orc.Y0:])
+
+
+def test_dr_invalid_cut_list_is_rejected():
+    """A forced plan whose grid cannot be resident (config 2 cut at stage 2: a 10-level
+    deepest tier) is refused at context creation, naming the switch."""
+    tree, prob = build_problem(recipe_config(2))
+    with pytest.raises(Exception, match="RAOCP_DR_CUTS"):
+        _with_env({"RAOCP_DR_CUTS": "2"}, lambda: core.Cache(prob))
 
 
 def test_dr_cp_loop_matches_tiers_and_oracle():

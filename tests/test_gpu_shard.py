@@ -39,7 +39,10 @@ def c2():
 def _kern_cache(prob, kern, dtype=None):
     """A context on the fused CP kernel k_cp3 ("fused", the default) or the two-launch
     k_cpd* / k_cpp* ("two", RAOCP_CP3=0)."""
-    env = {"RAOCP_DR": "0"}  # the dynamics a shard runs (the tiered sweep; fp32 / config 4: dyn3)
+    # the dynamics a shard runs (the tiered sweep; fp32 / config 4: dyn3) and the CP kernel it
+    # runs (k_cp3: a shard's task list; the unsharded default at config 2 is k_cp4, the same
+    # arithmetic with a different FMA contraction, test_gpu_cp4.py)
+    env = {"RAOCP_DR": "0", "RAOCP_CP4": "0"}
     if kern == "two":
         env["RAOCP_CP3"] = "0"
     old = {k: os.environ.get(k) for k in env}
@@ -85,7 +88,7 @@ def test_sharded_solve_matches_unsharded(cfg, R, kern):
         _CFG[cfg] = _cache(cfg)
     r, tree, prob = _CFG[cfg]
     base = _kern_cache(prob, kern)
-    assert base.native.kernel_info(10).startswith("k_cp3") == (kern == "fused")
+    assert base.native.kernel_info(10).startswith(("k_cp3", "k_cp4")) == (kern == "fused")
     lam = base.native.step_size()
     alpha = 0.999 / lam
     iters = 40 if cfg == 2 else 12
