@@ -80,6 +80,7 @@ struct raocp_ctx {
     std::vector<raocp::Dy3Stage> d3st;
     double *d3img_b = nullptr, *d3img_f = nullptr;  // per-stage table images (k_dy3_image)
     std::vector<raocp::Dy3Stage> d3own;  // a shard's stages (owned parent ranges below its cut)
+    int d3ts = 0;  // the top stages k_dy3_top_back / k_dy3_top_fwd run in one workgroup (0: none)
     int wsz = 8;                 // bytes per scalar of the iterate
     hipStream_t stream = nullptr;
     Dev dev{};
@@ -456,7 +457,19 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
     auto threads = [&](int t) { return coop(t) ? thr : thr_w; };
     const int N = c->N, S = c->sh_S;  // S > 0: a shard owns the stages >= S partly
     auto stage = [&](int t) -> const raocp::Dy3Stage& { return S > 0 && t >= S ? c->d3own[t] : c->d3st[t]; };
-    for (int t = N - 1; t >= 0; --t) {
+    // the top stages t < ts in one workgroup per direction (unsharded contexts, dyn3_top_stages)
+    const int ts = S == 0 ? c->d3ts : 0;
+    raocp::Dy3Top tp{};
+    tp.ts = ts;
+    for (int t = 0; t < ts; ++t) tp.st[t] = c->d3st[t];
+    const size_t ltop = (size_t)(L::back_n(C) + (8 / C) * C * (RU + RX) * 4 * 64) * sizeof(T);
+    auto ktb = raocp::k_dy3_top_back<T, NX, NU>;
+    auto ktf = raocp::k_dy3_top_fwd<T, NX, NU>;
+    if (ts) {
+        allow_lds(ktb, ltop);
+        allow_lds(ktf, lf);
+    }
+    for (int t = N - 1; t >= ts; --t) {
         if (part == 1 && t < S) break;
         if (part == 2 && t >= S) continue;
         const raocp::Dy3Stage& st = stage(t);
@@ -468,7 +481,11 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
                                                                     coop(t) ? 1 : 0);
     }
     if (part == 1) return;
-    for (int t = 0; t < N; ++t) {
+    if (ts) {
+        ktb<<<1, 512, ltop, c->stream>>>(c->dev, ctl, z, c->Q2, c->Dd2, tp, C, (const double*)c->d3img_b);
+        ktf<<<1, 512, lf, c->stream>>>(c->dev, ctl, z, c->Dd2, c->x0, tp, C, (const double*)c->d3img_f);
+    }
+    for (int t = ts; t < N; ++t) {
         const raocp::Dy3Stage& st = stage(t);
         if (st.i1 <= st.i0) continue;
         const double* img = (const double*)((const char*)c->d3img_f + (size_t)t * L::fwd_n(C) * sizeof(T));
@@ -499,6 +516,18 @@ int dyn3_imagest(raocp_ctx* c) {
     int rc;
     if ((rc = c->alloc(&c->d3img_b, std::max<size_t>(1, N * nb))) || (rc = c->alloc(&c->d3img_f, std::max<size_t>(1, N * nf))))
         return rc;
+    // the top stages of at most two rounds of 512 / (64 C) tiles run in one workgroup per
+    // direction (k_dy3_top_back / k_dy3_top_fwd); RAOCP_DY3_TOP=0 keeps a launch per stage
+    {
+        constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
+        const int tpr = 8 / C;
+        const size_t ltop = (size_t)(L::back_n(C) + tpr * C * (RU + RX) * 4 * 64) * sizeof(T);
+        int ts = 0;
+        while (ts < N - 1 && ts < raocp::kDy3TopMax && (c->d3st[ts].i1 - c->d3st[ts].i0 + 15) / 16 <= 2 * tpr) ++ts;
+        if (ts < 2 || ltop > 159 * 1024 || (size_t)L::fwd_n(C) * sizeof(T) > 159 * 1024) ts = 0;
+        if (const char* e = getenv("RAOCP_DY3_TOP")) ts = atoi(e) ? ts : 0;
+        c->d3ts = ts;
+    }
     for (int t = 0; t < N; ++t)
         raocp::k_dy3_image<T, NX, NU><<<1, 512, 0, c->stream>>>(c->d3st[t], C, c->W2, c->RG2, c->KM2, c->F2,
                                                                 c->d3img_b + t * nb, c->d3img_f + t * nf);
@@ -1264,9 +1293,12 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             auto b = [](bool v) { return std::string(v ? "true" : "false"); };
             if (c->dr && c->sh_S == 0) {
                 return std::string(raocp::dr_name(c->nx, c->nu)) + " x1";
-            } else if (c->dyn3) {  // one backward and one forward launch per nonleaf stage
-                for (int t = 0; t < c->N; ++t) add("k_dy3_back<" + T + ", " + nn + ">");
-                for (int t = 0; t < c->N; ++t) add("k_dy3_fwd<" + T + ", " + nn + ">");
+            } else if (c->dyn3) {  // a backward and a forward launch per nonleaf stage below the top
+                const int ts = c->sh_S == 0 ? c->d3ts : 0;
+                for (int t = ts; t < c->N; ++t) add("k_dy3_back<" + T + ", " + nn + ">");
+                if (ts) add("k_dy3_top_back<" + T + ", " + nn + ">");
+                if (ts) add("k_dy3_top_fwd<" + T + ", " + nn + ">");
+                for (int t = ts; t < c->N; ++t) add("k_dy3_fwd<" + T + ", " + nn + ">");
             } else if (c->dyn2) {
                 return "k_d2_prod + k_d2_node + k_d2_x0 + k_d2_fwd (per stage, " + T + ")";
             } else if (c->cut > 0 && c->dyn_split && c->sh_S == 0) {

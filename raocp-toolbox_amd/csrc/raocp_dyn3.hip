@@ -125,9 +125,6 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
     lT* wl = (lT*)dsm_;
     dma((ldsd*)dsm_, img, L::back_n(C) * (int)sizeof(T) / 8);  // whole 16-B chunks (N: multiples of 64)
     const int done = ctl_done(ctl);  // read while the image is in flight (raocp_dyn.hip)
-    dma_wait();
-    __syncthreads();
-    if (done) return;
     lT* wr = wl + C * (L::WB::N + L::WA::N);
     const typename L::WRI wri{wr};
     const typename L::WG wg{wr + L::WRI::N};
@@ -140,27 +137,41 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
     // gathered in LDS (slot order) by wave 0; else a wave per tile, slots in sequence
     const int gw = sp ? blockIdx.x : blockIdx.x * (blockDim.x >> 6) + wv;
     const int nw = (gridDim.x - ck.on) * (sp ? 1 : (blockDim.x >> 6));
+    const int k0 = sp ? wv : 0, k1 = sp ? (wv < C ? wv + 1 : 0) : C;
     lT* red = wl + L::back_n(C);  // sp: [C][RU + RX][4][64 lanes]
+    // a task's rows (children's q, or -x at the leaves; the parents' u and x) are read into
+    // registers before its products: the first task's while the stage image is in flight
+    T qj[4][RX][4], u[RU][4], x[RX][4];
+    auto load = [&](int task) {
+        const int i = st.i0 + 16 * task + lo;
+        const bool live = i < st.i1;
+        _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+            if (k < k0 || k >= k1) continue;
+            const int j = 1 + C * (live ? i : st.i0) + k;
+            if (st.leaf) ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)j * NX, live, qj[k]);
+            else ld_rows<T, NX>((cglbp<T>)qb + (size_t)j * NX, live, qj[k]);
+        }
+        ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)i * NU, live, u);
+        ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+    };
+    if (gw < ntile) load(gw);
+    dma_wait();
+    __syncthreads();
+    if (done) return;
     for (int task = gw; task < ntile; task += nw) {
         const int i = st.i0 + 16 * task + lo;
         const bool live = i < st.i1;
         v4 ha[RU], aa[RX];
         _Pragma("unroll") for (int r = 0; r < RU; ++r) ha[r] = v4{0, 0, 0, 0};
         _Pragma("unroll") for (int r = 0; r < RX; ++r) aa[r] = v4{0, 0, 0, 0};
-        const int k0 = sp ? wv : 0, k1 = sp ? (wv < C ? wv + 1 : 0) : C;
-        for (int k = k0; k < k1; ++k) {
-            const int j = 1 + C * (live ? i : st.i0) + k;
-            T qj[RX][4];
-            if (st.leaf) {
-                ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)j * NX, live, qj);
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) qj[rt][e] = -qj[rt][e];
-            } else {
-                ld_rows<T, NX>((cglbp<T>)qb + (size_t)j * NX, live, qj);
-            }
+        _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+            if (k < k0 || k >= k1) continue;
+            if (st.leaf)
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) qj[k][rt][e] = -qj[k][rt][e];
             const typename L::WB wb{wl + k * (L::WB::N + L::WA::N)};
             const typename L::WA wa{wl + k * (L::WB::N + L::WA::N) + L::WB::N};
-            mmts(wb, qj, ha);
-            mmts(wa, qj, aa);
+            mmts(wb, qj[k], ha);
+            mmts(wa, qj[k], aa);
         }
         if (sp) {
             const int l = threadIdx.x & 63;
@@ -180,12 +191,16 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
                 }
             }
             __syncthreads();  // red is rewritten by the next tile
-            if (wv != 0) continue;
+            if (wv != 0) {
+                if (task + nw < ntile) load(task + nw);
+                continue;
+            }
         }
-        T u[RU][4], x[RX][4], v[RU][4];
-        ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)i * NU, live, u);
-        ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+        T v[RU][4];
         _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) v[rt][e] = u[rt][e] - ha[rt][e];
+        T xs[RX][4];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) xs[rt][e] = x[rt][e];
+        if (task + nw < ntile) load(task + nw);  // the next task's rows behind this one's products
         v4 dv[RU], gv[RX];
         _Pragma("unroll") for (int r = 0; r < RU; ++r) dv[r] = v4{0, 0, 0, 0};
         _Pragma("unroll") for (int r = 0; r < RX; ++r) gv[r] = v4{0, 0, 0, 0};
@@ -194,7 +209,7 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
         T dd[RU][4], qq[RX][4];
         _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) dd[rt][e] = dv[rt][e];
         _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
-            qq[rt][e] = (-x[rt][e] + aa[rt][e]) + gv[rt][e];
+            qq[rt][e] = (-xs[rt][e] + aa[rt][e]) + gv[rt][e];
         st_rows<T, NU>(db + (size_t)i * NU, live, dd);
         st_rows<T, NX>(qb + (size_t)i * NX, live, qq);
     }
@@ -212,9 +227,6 @@ __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ 
     lT* wl = (lT*)dsm_;
     dma((ldsd*)dsm_, img, L::fwd_n(C) * (int)sizeof(T) / 8);
     const int done = ctl_done(ctl);
-    dma_wait();
-    __syncthreads();
-    if (done) return;
     lT* wf = wl + L::WK::N;
     const typename L::WK wk{wl};
     glbp<T> z = (glbp<T>)z_;
@@ -224,29 +236,196 @@ __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ 
     const int ntile = (st.i1 - st.i0 + 15) >> 4;
     // sp (stages of few tiles): a task per (tile, child slot), slot 0 also writing u
     const int ntask = sp ? ntile * C : ntile;
+    // a task's x and d rows are read before its products: the first task's while the stage
+    // image is in flight, the next task's behind the current one's
+    T x[RX][4], d[RU][4];
+    auto load = [&](int tk) {
+        const int task = sp ? tk / C : tk;
+        const int i = st.i0 + 16 * task + lo;
+        const bool live = i < st.i1;
+        if (i == 0) ld_rows<T, NX>((cglbp<T>)x0_, true, x);  // x_0 = x0bar (cache.py:283)
+        else ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+        ld_rows<T, NU>(db + (size_t)i * NU, live, d);
+    };
+    if (gw < ntask) load(gw);
+    dma_wait();
+    __syncthreads();
+    if (done) return;
     for (int tk = gw; tk < ntask; tk += nw) {
         const int task = sp ? tk / C : tk, ks = sp ? tk % C : 0, ke = sp ? ks + 1 : C;
         const int i = st.i0 + 16 * task + lo;
         const bool live = i < st.i1;
-        T x[RX][4], d[RU][4];
-        if (i == 0) {
-            // x_0 = x0bar (cache.py:283), written into the iterate too (by the slot-0 task)
-            ld_rows<T, NX>((cglbp<T>)x0_, true, x);
-            if (ks == 0) st_rows<T, NX>(z + p.X0, true, x);
-        } else {
-            ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
-        }
-        ld_rows<T, NU>(db + (size_t)i * NU, live, d);
+        T xc[RX][4], dc[RU][4];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) xc[rt][e] = x[rt][e];
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) dc[rt][e] = d[rt][e];
+        if (tk + nw < ntask) load(tk + nw);
+        if (i == 0 && ks == 0) st_rows<T, NX>(z + p.X0, true, xc);  // x_0 into the iterate (slot-0 task)
         v4 ku[RU];
         _Pragma("unroll") for (int r = 0; r < RU; ++r) ku[r] = v4{0, 0, 0, 0};
-        mmts(wk, x, ku);
+        mmts(wk, xc, ku);
         T u[RU][4];
-        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) u[rt][e] = ku[rt][e] + d[rt][e];
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) u[rt][e] = ku[rt][e] + dc[rt][e];
         if (ks == 0) st_rows<T, NU>(z + p.U0 + (size_t)i * NU, live, u);
         for (int k = ks; k < ke; ++k) {
             const int j = 1 + C * (live ? i : st.i0) + k;
             const typename L::WA wa{wf + k * (L::WA::N + L::WG::N)};
             const typename L::WG wb{wf + k * (L::WA::N + L::WG::N) + L::WA::N};
+            v4 xa[RX];
+            _Pragma("unroll") for (int r = 0; r < RX; ++r) xa[r] = v4{0, 0, 0, 0};
+            mmts(wa, xc, xa);
+            mmts(wb, dc, xa);
+            T xj[RX][4];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) xj[rt][e] = xa[rt][e];
+            st_rows<T, NX>(z + p.X0 + (size_t)j * NX, live, xj);
+        }
+    }
+}
+
+// ---- the small top stages of both sweeps in ONE workgroup each (k_dy3_top_back /
+// k_dy3_top_fwd): a stage of a few tiles costs a launch (dispatch, image fill, one tile's
+// MFMA chain, drain: 3.5-7 us at configs 4 / 5) for a few microseconds of work, so the
+// stages t < ts run back to back in one 512-lane workgroup, the image of each filled into
+// the same LDS by LDS-DMA, a barrier between stages (the rows a stage writes are the next
+// one's inputs: the same CU, so workgroup-scope visibility suffices).
+constexpr int kDy3TopMax = 8;
+struct Dy3Top {
+    Dy3Stage st[kDy3TopMax];
+    int ts;  // stages 0 .. ts - 1
+};
+
+// backward, t = ts - 1 .. 0: rounds of TPR = waves / C tiles, wave w on tile w / C and child
+// slot w % C (the slot order of the sp launches: bit-identical sums), the slot sums of
+// slots >= 1 through LDS to the tile's slot-0 wave, which finishes the tile (v, d, q)
+template <class T, int NX, int NU>
+__global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* __restrict__ ctl, double* __restrict__ z_,
+                                                      double* __restrict__ q_, double* __restrict__ d_, Dy3Top tp, int C,
+                                                      const double* __restrict__ img0) {
+    typedef typename MF<T>::v4 v4;
+    typedef Dy3Lds<T, NX, NU> L;
+    constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
+    extern __shared__ __attribute__((aligned(16))) double dsm_[];
+    typedef __attribute__((address_space(3))) T lT;
+    lT* wl = (lT*)dsm_;
+    if (ctl_done(ctl)) return;
+    glbp<T> z = (glbp<T>)z_;
+    glbp<T> qb = (glbp<T>)q_;
+    glbp<T> db = (glbp<T>)d_;
+    const int lo = threadIdx.x & 15, l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int tpr = (blockDim.x >> 6) / C, tl = wv / C, k = wv - tl * C;
+    lT* wr = wl + C * (L::WB::N + L::WA::N);
+    lT* red = wl + L::back_n(C);  // [tpr][C][RU + RX][4][64 lanes]
+    for (int si = tp.ts - 1; si >= 0; --si) {
+        const Dy3Stage st = tp.st[si];
+        dma((ldsd*)dsm_, img0 + (size_t)si * L::back_n(C) * sizeof(T) / 8, L::back_n(C) * (int)sizeof(T) / 8);
+        dma_wait();
+        __syncthreads();
+        const typename L::WRI wri{wr};
+        const typename L::WG wg{wr + L::WRI::N};
+        const int ntile = (st.i1 - st.i0 + 15) >> 4;
+        for (int t0 = 0; t0 < ntile; t0 += tpr) {
+            const int task = t0 + tl;
+            const bool act = tl < tpr && task < ntile;
+            const int i = st.i0 + 16 * task + lo;
+            const bool live = act && i < st.i1;
+            v4 ha[RU], aa[RX];
+            _Pragma("unroll") for (int r = 0; r < RU; ++r) ha[r] = v4{0, 0, 0, 0};
+            _Pragma("unroll") for (int r = 0; r < RX; ++r) aa[r] = v4{0, 0, 0, 0};
+            if (act) {
+                const int j = 1 + C * (live ? i : st.i0) + k;
+                T qj[RX][4];
+                if (st.leaf) {
+                    ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)j * NX, live, qj);
+                    _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) qj[rt][e] = -qj[rt][e];
+                } else {
+                    ld_rows<T, NX>((cglbp<T>)qb + (size_t)j * NX, live, qj);
+                }
+                const typename L::WB wb{wl + k * (L::WB::N + L::WA::N)};
+                const typename L::WA wa{wl + k * (L::WB::N + L::WA::N) + L::WB::N};
+                mmts(wb, qj, ha);
+                mmts(wa, qj, aa);
+                if (k > 0) {
+                    lT* rd = red + (size_t)(tl * C + k) * (RU + RX) * 4 * 64;
+                    _Pragma("unroll") for (int r = 0; r < RU; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                        rd[(r * 4 + e) * 64 + l] = ha[r][e];
+                    _Pragma("unroll") for (int r = 0; r < RX; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                        rd[((RU + r) * 4 + e) * 64 + l] = aa[r][e];
+                }
+            }
+            __syncthreads();
+            if (act && k == 0) {
+                for (int kk = 1; kk < C; ++kk) {
+                    const lT* rd = red + (size_t)(tl * C + kk) * (RU + RX) * 4 * 64;
+                    _Pragma("unroll") for (int r = 0; r < RU; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                        ha[r][e] += rd[(r * 4 + e) * 64 + l];
+                    _Pragma("unroll") for (int r = 0; r < RX; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                        aa[r][e] += rd[((RU + r) * 4 + e) * 64 + l];
+                }
+                T u[RU][4], x[RX][4], v[RU][4];
+                ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)i * NU, live, u);
+                ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+                _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) v[rt][e] = u[rt][e] - ha[rt][e];
+                v4 dv[RU], gv[RX];
+                _Pragma("unroll") for (int r = 0; r < RU; ++r) dv[r] = v4{0, 0, 0, 0};
+                _Pragma("unroll") for (int r = 0; r < RX; ++r) gv[r] = v4{0, 0, 0, 0};
+                mmts(wri, v, dv);
+                mmts(wg, v, gv);
+                T dd[RU][4], qq[RX][4];
+                _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) dd[rt][e] = dv[rt][e];
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                    qq[rt][e] = (-x[rt][e] + aa[rt][e]) + gv[rt][e];
+                st_rows<T, NU>(db + (size_t)i * NU, live, dd);
+                st_rows<T, NX>(qb + (size_t)i * NX, live, qq);
+            }
+            __syncthreads();  // red is rewritten by the next round; the rows by the next stage
+        }
+    }
+}
+
+// forward, t = 0 .. ts - 1: the (tile, child slot) tasks of a stage over the waves (the sp
+// launches' task order), slot 0 also writing u
+template <class T, int NX, int NU>
+__global__ void __launch_bounds__(512) k_dy3_top_fwd(Dev p, const Ctl* __restrict__ ctl, double* __restrict__ z_,
+                                                     const double* __restrict__ d_, const double* __restrict__ x0_,
+                                                     Dy3Top tp, int C, const double* __restrict__ img0) {
+    typedef typename MF<T>::v4 v4;
+    typedef Dy3Lds<T, NX, NU> L;
+    constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
+    extern __shared__ __attribute__((aligned(16))) double dsm_[];
+    typedef __attribute__((address_space(3))) T lT;
+    lT* wl = (lT*)dsm_;
+    if (ctl_done(ctl)) return;
+    glbp<T> z = (glbp<T>)z_;
+    cglbp<T> db = (cglbp<T>)d_;
+    const int lo = threadIdx.x & 15, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    lT* wf = wl + L::WK::N;
+    for (int si = 0; si < tp.ts; ++si) {
+        const Dy3Stage st = tp.st[si];
+        dma((ldsd*)dsm_, img0 + (size_t)si * L::fwd_n(C) * sizeof(T) / 8, L::fwd_n(C) * (int)sizeof(T) / 8);
+        dma_wait();
+        __syncthreads();
+        const typename L::WK wk{wl};
+        const int ntile = (st.i1 - st.i0 + 15) >> 4, ntask = ntile * C;
+        for (int tk = wv; tk < ntask; tk += nwv) {
+            const int task = tk / C, ks = tk - task * C;
+            const int i = st.i0 + 16 * task + lo;
+            const bool live = i < st.i1;
+            T x[RX][4], d[RU][4];
+            if (i == 0) {
+                ld_rows<T, NX>((cglbp<T>)x0_, true, x);  // x_0 = x0bar (cache.py:283)
+                if (ks == 0) st_rows<T, NX>(z + p.X0, true, x);
+            } else {
+                ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+            }
+            ld_rows<T, NU>(db + (size_t)i * NU, live, d);
+            v4 ku[RU];
+            _Pragma("unroll") for (int r = 0; r < RU; ++r) ku[r] = v4{0, 0, 0, 0};
+            mmts(wk, x, ku);
+            T u[RU][4];
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) u[rt][e] = ku[rt][e] + d[rt][e];
+            if (ks == 0) st_rows<T, NU>(z + p.U0 + (size_t)i * NU, live, u);
+            const int j = 1 + C * (live ? i : st.i0) + ks;
+            const typename L::WA wa{wf + ks * (L::WA::N + L::WG::N)};
+            const typename L::WG wb{wf + ks * (L::WA::N + L::WG::N) + L::WA::N};
             v4 xa[RX];
             _Pragma("unroll") for (int r = 0; r < RX; ++r) xa[r] = v4{0, 0, 0, 0};
             mmts(wa, x, xa);
@@ -255,5 +434,6 @@ __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ 
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) xj[rt][e] = xa[rt][e];
             st_rows<T, NX>(z + p.X0 + (size_t)j * NX, live, xj);
         }
+        __syncthreads();  // the children's x rows are the next stage's inputs
     }
 }

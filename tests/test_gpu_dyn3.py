@@ -129,11 +129,39 @@ def test_kernel_info_lists_the_projection_launches():
         terms = [re.fullmatch(r"(k_\w+<[^>]*>) x(\d+)", t) for t in cache.native.kernel_info(9).split(" + ")]
         assert all(terms), cache.native.kernel_info(9)
         cnt = {m.group(1).split("<")[0]: int(m.group(2)) for m in terms}
-        if want == "dy3":
-            assert cnt == {"k_dy3_back": 12, "k_dy3_fwd": 12}
+        if want == "dy3":  # the 8 top stages (<= 8 tiles each) in one workgroup per direction
+            assert cnt == {"k_dy3_back": 4, "k_dy3_top_back": 1, "k_dy3_top_fwd": 1, "k_dy3_fwd": 4}
         elif want == "dr":
             assert cnt == {"k_dr": 1}
         elif want == "split":
             assert cnt == {"k_dyn_up": 1, "k_dyn_down": 1}
         else:
             assert cnt["k_dyn_top"] == 1 and cnt["k_dyn_bottom_back"] == cnt["k_dyn_bottom_fwd"] >= 1
+
+
+@pytest.mark.parametrize("cfg,dtype", [(4, "float64"), (2, "float64"), (5, "float32")])
+def test_top_stages_in_one_workgroup_bit_identical(cfg, dtype):
+    """k_dy3_top_back / k_dy3_top_fwd (the top stages back to back in one workgroup) sum the
+    child slots in the order of the slot-parallel per-stage launches they replace
+    (RAOCP_DY3_TOP=0): the projection and a 12-iteration CP loop are bit-identical."""
+    r = recipe_config(cfg)
+    prob = build_problem(r)[1]
+    env = {"RAOCP_DYN3": "1"} if cfg == 2 else {}
+    top = _with_env(env, lambda: core.Cache(prob, dtype=dtype))
+    per = _with_env({**env, "RAOCP_DY3_TOP": "0"}, lambda: core.Cache(prob, dtype=dtype))
+    assert "k_dy3_top_back" in top.native.kernel_info(9) and "k_dy3_top" not in per.native.kernel_info(9)
+    zz = np.random.default_rng(21).standard_normal(top.primal_size)
+    out = []
+    for cache in (top, per):
+        cache.cache_initial_state(r["x0"])
+        cache.native.set_primal(zz)
+        cache.native.project_on_dynamics()
+        out.append(cache.native.get_primal())
+    assert np.array_equal(out[0], out[1])
+    alpha = 0.999 / top.native.step_size(rtol=1e-7 if dtype == "float32" else 1e-14)
+    runs = []
+    for cache in (top, per):
+        st, err, derr = cache.native.cp_run(r["x0"], 12, 0.0, alpha)
+        runs.append((st, err, derr, cache.get_primal_flat()))
+    for u, v in zip(runs[0], runs[1]):
+        assert np.array_equal(u, v)
