@@ -60,6 +60,8 @@ struct raocp_ctx {
     int ellt3_grid = 0;
     bool cp3 = false;            // the CP iteration after the dynamics as one streaming kernel (raocp_cp3.hip)
     bool cp4 = false;            // ... with every operand of a tile loaded at its start (raocp_cp4.hip; RAOCP_CP4=0: off)
+    int cp4_wpb = 1;             // k_cp4's waves per workgroup (one task per wave; RAOCP_CP4_WAVES): one
+                                 // spreads the tasks' load bursts over all CUs (config 2: 16.7 vs 18.5 us at four)
     int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
     int cp3_split = 0;           // leaves as tasks of their own (small trees: more waves, shorter chains)
@@ -1073,7 +1075,7 @@ int cp3_image(raocp_ctx* c) {
 void launch_cp3(raocp_ctx* c, int part = 0) {
     if (c->cp4 && c->sh_S == 0) {
         raocp::cp4_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->cp3_ta, c->cp3img, c->cp3_grid,
-                          c->stream);
+                          c->cp4_wpb, c->stream);
         return;
     }
     if (c->sh_S > 0)
@@ -2701,6 +2703,17 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             if ((rc = cp3_image(c))) return bail(rc);
             c->cp4 = raocp::cp4_supported(c->f32, nx, nu, c->unif_C, c->box_mode);
             if (const char* e = getenv("RAOCP_CP4")) c->cp4 = c->cp4 && atoi(e) != 0;
+            if (c->cp4) {  // k_cp4: cp4_wpb waves per workgroup, the same waves over more CUs
+                if (const char* e = getenv("RAOCP_CP4_WAVES")) c->cp4_wpb = std::max(1, std::min(4, atoi(e)));
+                c->cp3_grid = c->cp3_grid * 4 / c->cp4_wpb;
+                if (c->cp3_grid > c->red_rows) {
+                    c->red_rows = c->cp3_grid;
+                    if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
+                    if (hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)) != hipSuccess)
+                        return bail(fail(RAOCP_ERR_HIP, "memset"));
+                }
+                c->cp_rows = c->cp3_grid;
+            }
         }
     }
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels
@@ -3163,6 +3176,12 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
         int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
         if (rc2) return rc2;
         launch_cpp(c);
+    } else if (which && which[0] == 'c') {  // the fused CP kernel (k_cp4 / k_cp3) on a valid control block
+        if (!c->cp3) return fail(RAOCP_ERR_ARG, "no fused CP kernel on this context");
+        std::vector<double> x0(c->nx, 0.0);
+        int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
+        if (rc2) return rc2;
+        launch_cp3(c);
     } else if (which && which[0] == 'l') {  // k_ell on the staging buffers
         launch_ell(c, c->tmpP, c->tmpD);
     } else if (which && which[0] == 't') {  // k_ell_t

@@ -12,6 +12,6 @@ const char* cp4_name(bool f32, int nx, int nu);
 // one launch on stream s (hipGetLastError() after it is the caller's); the task list, weight
 // image and grid are k_cp3's (raocp_capi.hip)
 void cp4_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, const Cp3Tasks& tk, const double* img,
-                int grid, hipStream_t s);
+                int grid, int wpb, hipStream_t s);
 
 }  // namespace raocp

@@ -75,18 +75,31 @@ __device__ __forceinline__ constexpr bool tok(int rt, int e) {
 }
 // row-layout load / store of an R-row node vector (raocp_cp3.hip): a[rt][e] = v[R/4 h + 4 rt + e]
 template <class T, int R>
+// (v must be a valid row address even when !live: every load is issued unconditionally and
+// the value selected after it — a load under a runtime condition makes the compiler branch
+// around it and wait for it on its own, one memory round trip per load)
 __device__ __forceinline__ void ld_rows(cglbp<T> v, bool live, T (&a)[(R + 15) / 16][4]) {
     typedef typename V4a<T>::type vt;
     constexpr int KC = R / 4;
     cglbp<T> b = v + KC * ((threadIdx.x & 63) >> 4);
     _Pragma("unroll") for (int rt = 0; rt < (R + 15) / 16; ++rt) {
-        if (live && 4 * rt + 3 < KC) {
+        if (4 * rt + 3 < KC) {
             const vt w = *(const __attribute__((address_space(1))) vt*)(b + 4 * rt);
-            _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = w[e];
+            _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = live ? w[e] : T(0);
         } else {
-            _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = (live && tok<R>(rt, e)) ? b[4 * rt + e] : T(0);
+            _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                T w = T(0);
+                if (tok<R>(rt, e)) w = b[4 * rt + e];
+                a[rt][e] = live ? w : T(0);
+            }
         }
     }
+}
+// one scalar at a valid address, zero when !live (unconditional load, see ld_rows)
+template <class T>
+__device__ __forceinline__ T ldz(cglbp<T> v, bool live) {
+    const T w = *v;
+    return live ? w : T(0);
 }
 template <class T, int R>
 __device__ __forceinline__ void st_rows(glbp<T> v, bool live, const T (&a)[(R + 15) / 16][4]) {
@@ -161,12 +174,20 @@ struct LeafIn {
         ld_rows<T, NX>(zp + p.X0 + (size_t)lq * NX, live, lz);
         ld_rows<T, NX>(pz + p.X0 + (size_t)lq * NX, live, lp);
         ld_rows<T, NX>(d + p.E11 + p.m + (size_t)(lq - p.m) * NX, live, d11);
-        ld_rows<T, NX>(d + p.E14 + p.m + (size_t)(lq - p.m) * NX, BXL == 1 && full && live, d14);
-        d12 = live ? d[p.E12 + l] : T(0);
-        d13 = live ? d[p.E13 + l] : T(0);
-        sz = live ? zp[p.S0 + l] : T(0);
-        sp = live ? pz[p.S0 + l] : T(0);
-        bl = (BXL == 1 && full && p.nBl > 1 && live) ? p.iBl[l] : 0;
+        if constexpr (BXL == 1) {  // (eta14 exists only where the leaves are boxed)
+            ld_rows<T, NX>(d + p.E14 + p.m + (size_t)(lq - p.m) * NX, full && live, d14);
+        } else {
+            _Pragma("unroll") for (int rt = 0; rt < (NX + 15) / 16; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) d14[rt][e] = T(0);
+        }
+        d12 = ldz(d + p.E12 + lq, live);
+        d13 = ldz(d + p.E13 + lq, live);
+        sz = ldz(zp + p.S0 + lq, live);
+        sp = ldz(pz + p.S0 + lq, live);
+        bl = 0;
+        if (BXL == 1 && full && p.nBl > 1) {
+            const int b = p.iBl[lq];
+            bl = live ? b : 0;
+        }
     }
 };
 
@@ -192,21 +213,22 @@ struct FamIn {
         const int iq = live ? i : 0;
         const int yo = G * iq;
         _Pragma("unroll") for (int k = 0; k < C; ++k) {
-            cp[k] = live ? cond[1 + C * i + k] : T(0);
-            zyk[k] = live ? zp[p.Y0 + yo + k] : T(0);
-            pyk[k] = live ? pz[p.Y0 + yo + k] : T(0);
+            cp[k] = ldz(cond + 1 + C * iq + k, live);
+            zyk[k] = ldz(zp + p.Y0 + yo + k, live);
+            pyk[k] = ldz(pz + p.Y0 + yo + k, live);
         }
-        zyc = live ? zp[p.Y0 + yo + 2 * C] : T(0);
-        pyc = live ? pz[p.Y0 + yo + 2 * C] : T(0);
-        zs = live ? zp[p.S0 + i] : T(0);
-        ps = live ? pz[p.S0 + i] : T(0);
-        d2 = live ? d[p.E2 + i] : T(0);
+        zyc = ldz(zp + p.Y0 + yo + 2 * C, live);
+        pyc = ldz(pz + p.Y0 + yo + 2 * C, live);
+        zs = ldz(zp + p.S0 + iq, live);
+        ps = ldz(pz + p.S0 + iq, live);
+        d2 = ldz(d + p.E2 + iq, live);
         _Pragma("unroll") for (int t = 0; t < NQ; ++t) {
             const int q = h + 4 * t;
             const bool ok = live && q < G;
-            qz[t] = ok ? zp[p.Y0 + yo + q] : T(0);
-            qp[t] = ok ? pz[p.Y0 + yo + q] : T(0);
-            qd[t] = ok ? d[p.E1 + yo + q] : T(0);
+            const int qq = q < G ? q : 0;
+            qz[t] = ldz(zp + p.Y0 + yo + qq, ok);
+            qp[t] = ldz(pz + p.Y0 + yo + qq, ok);
+            qd[t] = ldz(d + p.E1 + yo + qq, ok);
         }
         ld_rows<T, NX>(zp + p.X0 + (size_t)iq * NX, live, xz);
         ld_rows<T, NX>(pz + p.X0 + (size_t)iq * NX, live, xp);
@@ -216,33 +238,37 @@ struct FamIn {
             const int j = 1 + C * iq + k;
             ld_rows<T, NX>(d + p.E3 + 1 + (size_t)(j - 1) * NX, live, d3[k]);
             ld_rows<T, NU>(d + p.E4 + 1 + (size_t)(j - 1) * NU, live, d4[k]);
-            d5[k] = live ? d[p.E5 + j] : T(0);
-            d6[k] = live ? d[p.E6 + j] : T(0);
-            tz[k] = live ? zp[p.T0 + j] : T(0);
-            tp[k] = live ? pz[p.T0 + j] : T(0);
+            d5[k] = ldz(d + p.E5 + j, live);
+            d6[k] = ldz(d + p.E6 + j, live);
+            tz[k] = ldz(zp + p.T0 + j, live);
+            tp[k] = ldz(pz + p.T0 + j, live);
         }
         if (!LEAFP) {
             const bool g0 = live && h == 0;
             _Pragma("unroll") for (int k = 0; k < C; ++k) {
                 const int j = 1 + C * iq + k, yj = G * j;
-                csz[k] = g0 ? zp[p.S0 + j] : T(0);
-                csp[k] = g0 ? pz[p.S0 + j] : T(0);
-                cdj[k] = g0 ? d[p.E2 + j] : T(0);
+                csz[k] = ldz(zp + p.S0 + j, g0);
+                csp[k] = ldz(pz + p.S0 + j, g0);
+                cdj[k] = ldz(d + p.E2 + j, g0);
                 _Pragma("unroll") for (int q = 0; q < C; ++q) {
-                    ccp[k][q] = g0 ? cond[1 + C * j + q] : T(0);
-                    czy[k][q] = g0 ? zp[p.Y0 + yj + q] : T(0);
-                    cpy[k][q] = g0 ? pz[p.Y0 + yj + q] : T(0);
+                    ccp[k][q] = ldz(cond + 1 + C * j + q, g0);
+                    czy[k][q] = ldz(zp + p.Y0 + yj + q, g0);
+                    cpy[k][q] = ldz(pz + p.Y0 + yj + q, g0);
                 }
-                czy[k][C] = g0 ? zp[p.Y0 + yj + 2 * C] : T(0);
-                cpy[k][C] = g0 ? pz[p.Y0 + yj + 2 * C] : T(0);
+                czy[k][C] = ldz(zp + p.Y0 + yj + 2 * C, g0);
+                cpy[k][C] = ldz(pz + p.Y0 + yj + 2 * C, g0);
             }
         }
         if (BXN == 1) {
             ld_rows<T, NX>(d + p.E7 + (size_t)iq * (NX + NU), live, d7x);
             ld_rows<T, NU>(d + p.E7 + (size_t)iq * (NX + NU) + NX, live, d7u);
         }
-        al = live ? ((cglbp<T>)p.alpha_r)[i] : T(0);
-        bi = (BXN == 1 && p.nBnl > 1 && live) ? p.iBnl[i] : 0;
+        al = ldz((cglbp<T>)p.alpha_r + iq, live);
+        bi = 0;
+        if (BXN == 1 && p.nBnl > 1) {
+            const int b = p.iBnl[iq];
+            bi = live ? b : 0;
+        }
     }
 };
 
@@ -406,8 +432,16 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
         st_rows<T, NX>(out + p.X0 + (size_t)(live ? l : 0) * NX, live, ox);
     };
     // one family tile: parents i0 + lo (< iend); LEAFP: the children are leaves
+    // diagnostics (p.stamps, RAOCP_STAMP_KERNEL=c): s_memrealtime at the phase boundaries of
+    // one family task (lane 0 of the wave that takes task nTL + 200)
+    bool stp_on = false;
+    int stp_n = 0;
+    auto stamp = [&]() {
+        if (stp_on && (threadIdx.x & 63) == 0 && stp_n < 16) p.stamps[stp_n++] = __builtin_amdgcn_s_memrealtime();
+    };
     auto family = [&](auto leafp_tag, int i0, int iend, int split) {
         constexpr bool LEAFP = decltype(leafp_tag)::value;
+        stamp();
         const int i = i0 + lo;
         const bool live = i < iend;
         const int yo = G * i;
@@ -417,9 +451,11 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
         if (LEAFP)
             _Pragma("unroll") for (int k = 0; k < C; ++k) lf[k].load(p, zp, pz, d, 1 + C * i + k, live, !split);
         in.load(p, zp, pz, d, cond, i, live);
+        stamp();  // loads issued
         // ---------------- phase 4 (parents of leaves): leaf children; their s_l to the scratch
         if (LEAFP)
             _Pragma("unroll") for (int k = 0; k < C; ++k) leaf_work(lf[k], 1 + C * i + k, k, live, !split, true);
+        stamp();
         // ---------------- phase 1: the parent's rows
         T bya = T(0), byb = T(0);
         if (live) {
@@ -489,6 +525,7 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
             sxA[rt][e] = sxW[rt][e] = sxC[rt][e] = T(0);
         _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
             suA[rt][e] = suW[rt][e] = suC[rt][e] = T(0);
+        stamp();
         // ---------------- phase 2: child slots (child block SOC, L^T accumulation)
         _Pragma("unroll") for (int k = 0; k < C; ++k) {
             const int j = 1 + C * i + k;
@@ -572,6 +609,7 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
                 account(sp, sz, dj - ep, x2);
             }
         }
+        stamp();
         // ---------------- phase 3: eta7 (box on [x_i; u_i]) and x_i, u_i of the half step:
         // L^T = Gamma' eta7 + sqrtQ (sum of the children's eta3) (operators.py:73-85)
         {
@@ -645,6 +683,7 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
             }
             st_rows<T, NU>(out + p.U0 + (size_t)(live ? i : 0) * NU, live, ou);
         }
+        stamp();
         // ---------------- phase 5: AVaR kernel projection of the family (cache.py:290-317)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -678,9 +717,12 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
             if (h == 0) out[p.Y0 + yo + 2 * C] = y2c - sw;
         }
         __builtin_amdgcn_wave_barrier();
+        stamp();
     };
     const int split = tk.split;
     const int nTL = (tk.l1 - tk.l0 + 15) >> 4;  // leaf tiles (split), then the parent ranges' tiles
+    // diagnostics: every wave's [first task start, last task end] at stamps[32 + 2 gw]
+    const unsigned long long w_t0 = p.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
     for (int tt = gw; tt < nTL + tk.t0[tk.nr]; tt += nwv) {
         if (tt < nTL) {
             // a tile of 16 consecutive leaves (split): everything of the leaf but s_l
@@ -692,11 +734,16 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
             continue;
         }
         const int task = tt - nTL;
+        stp_on = p.stamps != nullptr && task == p.cp_dbg;  // (diagnostics: the stamped task)
         int r = 0;
         while (r + 1 < tk.nr && task >= tk.t0[r + 1]) ++r;
         const int i0 = tk.lo[r] + 16 * (task - tk.t0[r]), iend = tk.hi[r];
         if (tk.lo[r] >= tk.mL) family(std::true_type{}, i0, iend, split);
         else family(std::false_type{}, i0, iend, split);
+    }
+    if (p.stamps && (threadIdx.x & 63) == 0 && gw < 2000) {
+        p.stamps[32 + 2 * gw] = w_t0;
+        p.stamps[33 + 2 * gw] = __builtin_amdgcn_s_memrealtime();
     }
     // per-block residual maxima -> one row of `part` (plain stores, k_cp_check reduces)
     double mm[6] = {m0, m1, m2, m3, m4, m5};
@@ -713,12 +760,13 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
 
 template <class T, int NX, int NU, int C>
 void launch_c(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, const Cp3Tasks& tk, const double* img, int grid,
-              hipStream_t s) {
+              int wpb, hipStream_t s) {
     const int bn = bx & 3, bl = (bx >> 2) & 3;
-    if (bn == 1 && bl == 1) k_cp4<T, NX, NU, C, 1, 1><<<grid, 256, 0, s>>>(p, ctl, bf, part, tk, img);
-    else if (bn == 2 && bl == 2) k_cp4<T, NX, NU, C, 2, 2><<<grid, 256, 0, s>>>(p, ctl, bf, part, tk, img);
-    else if (bn == 2 && bl == 1) k_cp4<T, NX, NU, C, 2, 1><<<grid, 256, 0, s>>>(p, ctl, bf, part, tk, img);
-    else k_cp4<T, NX, NU, C, 1, 2><<<grid, 256, 0, s>>>(p, ctl, bf, part, tk, img);
+    const int g = grid, th = 64 * wpb;
+    if (bn == 1 && bl == 1) k_cp4<T, NX, NU, C, 1, 1><<<g, th, 0, s>>>(p, ctl, bf, part, tk, img);
+    else if (bn == 2 && bl == 2) k_cp4<T, NX, NU, C, 2, 2><<<g, th, 0, s>>>(p, ctl, bf, part, tk, img);
+    else if (bn == 2 && bl == 1) k_cp4<T, NX, NU, C, 2, 1><<<g, th, 0, s>>>(p, ctl, bf, part, tk, img);
+    else k_cp4<T, NX, NU, C, 1, 2><<<g, th, 0, s>>>(p, ctl, bf, part, tk, img);
 }
 
 }  // namespace
@@ -736,9 +784,9 @@ const char* cp4_name(bool f32, int nx, int nu) {
     return "k_cp4<double, 20, 8>";
 }
 void cp4_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, const Cp3Tasks& tk, const double* img,
-                int grid, hipStream_t s) {
+                int grid, int wpb, hipStream_t s) {
     (void)C;
-    launch_c<double, 20, 8, 2>(p, ctl, bf, part, bx, tk, img, grid, s);
+    launch_c<double, 20, 8, 2>(p, ctl, bf, part, bx, tk, img, grid, wpb, s);
 }
 
 }  // namespace raocp

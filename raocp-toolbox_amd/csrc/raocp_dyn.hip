@@ -323,7 +323,7 @@ __device__ __forceinline__ void back_fold(const Dev& p, const TB& tb, const INF&
 // ---- forward: u_i = K x_i + d_i (nodes [b, e)), x_j = F [x_i; d_i] (their children) ---
 // xd(i): padded row [x_i | d_i | 0] (KF); child rows also go to xdo(j) when XOUT.
 // SCX: the children's x rows are stored write-through (st_sc1): another workgroup of the
-// same launch reads them (the fused sweep, raocp_dynf.hip)
+// same launch reads them (the split sweep, raocp_dynf.hip)
 template <int KS, int NXc, int NUc, bool XOUT, bool SCX, class TB, class INF, class XDI, class XDO>
 __device__ __forceinline__ void fwd_phase_ks(const Dev& p, const TB& tb, const INF& inf, int b, int e, int cb, int ce,
                                              XDI xd, glbd* z, XDO xdo, int tid, int nthr) {

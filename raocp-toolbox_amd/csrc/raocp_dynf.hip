@@ -11,8 +11,9 @@
 // the dependent rows (the children's q, the parent's x) wait for a hand-off (below).
 //
 // Hand-offs across workgroups (MI355X: per-XCD L2s are not coherent): the roots' q rows
-// and the boundary x rows are stored write-through (st_sc1) and read with ld_sc1; the
-// storing waves drain (vmcnt 0), a barrier, then one lane arrives / stores the flag. The
+// and the boundary x rows are stored write-through (st_sc1) and read with ld_sc1; after a
+// barrier one lane arrives / stores the flag with agent-scope release, the waiter polls
+// relaxed and takes an agent-scope acquire before the barrier that frees its readers. The
 // host launches the sweep only where the whole grid is co-resident
 // (hipOccupancyMaxActiveBlocksPerMultiprocessor), so no wait depends on the dispatch order;
 // every wait is bounded (FuseArg::timeout) and a timed-out workgroup sets the error word,
@@ -385,10 +386,17 @@ __device__ void fz_top_run(const Dev& p, glbd* z, const double* qbuf_, const dou
     }
 }
 
-// stores of this workgroup drained, then one lane publishes
-__device__ __forceinline__ void fz_drain() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+// hand-off publish: the workgroup's payload stores (write-through) happen before the barrier,
+// then one lane releases at agent scope (HIP memory model: the barrier orders every lane's
+// stores before lane 0's release; the waiter's acquire after its poll orders the payload
+// reads after it)
+__device__ __forceinline__ void fz_release_add(unsigned* c) {
     __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void fz_release_store(unsigned* f, unsigned v) {
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store((gu32*)f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ==============================================================================
@@ -404,7 +412,8 @@ __device__ __forceinline__ void fz_drain() {
 // Counters are reset by their one consumer after its wait; flags carry the epoch, which
 // k_dyn_up's top advances once per projection.
 
-// spin (one lane) until *f == v, bounded; false on a timeout (error word set)
+// spin (one lane, relaxed polls) until *f == v, bounded, then an agent-scope acquire; false
+// on a timeout (error word set)
 __device__ __forceinline__ bool fz_wait_eq(const unsigned* f, unsigned v, const FuseArg& fa, int& ok) {
     if (threadIdx.x == 0) {
         const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -416,6 +425,7 @@ __device__ __forceinline__ bool fz_wait_eq(const unsigned* f, unsigned v, const 
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
     __syncthreads();
     return ok != 0;
@@ -455,8 +465,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_up(Dev p, Bufs bf, const Ctl
             fz_back_levels<NXc, NUc>(p, qbuf_, tt, b, k == D, nullptr, smem, pl, (glbd*)dbuf_);
         }
         fz_stamp(p, pl);
-        fz_drain();
-        if (tid == 0) __hip_atomic_fetch_add(tt.cnt + b / tt.r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fz_release_add(tt.cnt + b / tt.r);
         fz_stamp(p, pl);
         if (p.stamps && tid == 0 && b == 0 && (k == 0 || k == D))  // diagnostics: tier 0 / deepest, subtree 0
             for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
@@ -469,8 +478,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_up(Dev p, Bufs bf, const Ctl
         fz_stamp(p, pl);
         if (work) fz_top_run<NXc, NUc, false>(p, z, qbuf_, nullptr, fa, smem, pl, (glbd*)dbuf_);
         fz_stamp(p, pl);
-        fz_drain();
-        if (tid == 0) st_u32_sc1(fa.epoch, e + 1u);
+        fz_release_store(fa.epoch, e + 1u);
         if (p.stamps && tid == 0)
             for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[q] = pl.ts[q];
     }
@@ -562,8 +570,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const C
         const unsigned tag = ld_u32_sc1(fa.epoch);
         if (!ctl_done(ctl)) fz_top_fwd<NXc, NUc, FL>(p, z, dbuf_, x0_, fa, smem, pl);
         fz_stamp(p, pl);
-        fz_drain();
-        if (tid == 0) st_u32_sc1(fa.t[0].flag, tag);
+        fz_release_store(fa.t[0].flag, tag);
         if (p.stamps && tid == 0)
             for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[q] = pl.ts[q];
         return;
@@ -585,8 +592,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const C
     if (work) fz_fwd_run<NXc, NUc>(p, z, tt, b, k < D, XD, scr, pl);
     fz_stamp(p, pl);
     if (k < D) {
-        fz_drain();
-        if (tid == 0) st_u32_sc1(fa.t[k + 1].flag + b, tag);
+        fz_release_store(fa.t[k + 1].flag + b, tag);
     }
     if (p.stamps && tid == 0 && b == 0)  // diagnostics: tier 0 / deepest, subtree 0
         for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
