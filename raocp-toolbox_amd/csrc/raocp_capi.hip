@@ -2512,7 +2512,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     // over B blocks; B from the node count (env RAOCP_ELL_NODES overrides the nodes per
     // block), raised until every block's LDS stage fits 64 KB
     {
-        // measured (tools/ell_try.sh): 512-thread blocks while the grid is one block per CU,
+        // measured (round-2 A/B of the block size): 512-thread blocks while the grid is one block per CU,
         // 256-thread blocks of 64 nodes once there are several per CU
         int per = 64;
         if (const char* e = getenv("RAOCP_ELL_NODES")) per = std::max(1, atoi(e));
