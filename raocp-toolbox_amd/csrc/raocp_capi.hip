@@ -450,10 +450,12 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
     // stages of few tiles run slot-parallel (a wave per child slot): the dependent MFMA chain
     // of a tile is what a small stage costs. Decided on the whole stage, so a shard sums a
     // parent's child slots in the same order as the unsharded sweep (bit-identical results).
+    // (every stage slot-parallel, a workgroup looping over its tiles, measured slower: config 4
+    // 112.3 vs 110.4 us, config 5 227.5 vs 197.3 us per projection, profiles/r04/cp3_time_dy3.log)
     auto coop = [&](int t) { return (c->d3st[t].i1 - c->d3st[t].i0 + 15) / 16 * C <= 256 * wpb; };
     auto grid = [&](const raocp::Dy3Stage& st, int t, bool back) {
         const int tiles = (st.i1 - st.i0 + 15) / 16;
-        if (coop(t)) return std::max(1, back ? tiles : (tiles * C + wpb - 1) / wpb);
+        if (coop(t)) return std::max(1, std::min(cap, back ? tiles : (tiles * C + wpb - 1) / wpb));
         return std::max(1, std::min(cap, (tiles + wpb_w - 1) / wpb_w));
     };
     auto threads = [&](int t) { return coop(t) ? thr : thr_w; };
@@ -464,6 +466,9 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
     raocp::Dy3Top tp{};
     tp.ts = ts;
     for (int t = 0; t < ts; ++t) tp.st[t] = c->d3st[t];
+    tp.same_kinds = 1;
+    for (int t = 1; t < ts; ++t)
+        for (int k = 0; k < C; ++k) tp.same_kinds &= c->d3st[t].kind[k] == c->d3st[0].kind[k];
     const size_t ltop = (size_t)(L::back_n(C) + (8 / C) * C * (RU + RX) * 4 * 64) * sizeof(T);
     auto ktb = raocp::k_dy3_top_back<T, NX, NU>;
     auto ktf = raocp::k_dy3_top_fwd<T, NX, NU>;
@@ -524,8 +529,11 @@ int dyn3_imagest(raocp_ctx* c) {
         constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16;
         const int tpr = 8 / C;
         const size_t ltop = (size_t)(L::back_n(C) + tpr * C * (RU + RX) * 4 * 64) * sizeof(T);
+        // (stages of up to 4 / 16 rounds measured slower: config 4 117.8 / 145.4 vs 111.6 us,
+        // profiles/r04/cp3_time_dy3_rounds.log)
+        const int rounds = 2;
         int ts = 0;
-        while (ts < N - 1 && ts < raocp::kDy3TopMax && (c->d3st[ts].i1 - c->d3st[ts].i0 + 15) / 16 <= 2 * tpr) ++ts;
+        while (ts < N - 1 && ts < raocp::kDy3TopMax && (c->d3st[ts].i1 - c->d3st[ts].i0 + 15) / 16 <= rounds * tpr) ++ts;
         if (ts < 2 || ltop > 159 * 1024 || (size_t)L::fwd_n(C) * sizeof(T) > 159 * 1024) ts = 0;
         if (const char* e = getenv("RAOCP_DY3_TOP")) ts = atoi(e) ? ts : 0;
         c->d3ts = ts;

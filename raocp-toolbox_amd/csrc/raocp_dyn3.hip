@@ -40,6 +40,15 @@ struct WLs {
             dst[q] = r >= 0 ? ((cglbp<T>)M)[(size_t)(c0 + k) * ld + r0 + r] : T(0);
         }
     }
+    // the same from a row-major source: M[r][k] = src[(r0 + r) ld + c0 + k]
+    template <class DP>
+    static __device__ __forceinline__ void fill_t(DP dst, const T* M, int ld, int r0, int c0) {
+        for (int q = threadIdx.x; q < N; q += blockDim.x) {
+            const int l = q & 63, lo = l & 15, h = l >> 4, s = (q >> 6) % KS, ro = (q >> 6) / KS;
+            const int r = wrow<T, R>(ro, lo), k = KS * h + s;
+            dst[q] = r >= 0 ? ((cglbp<T>)M)[(size_t)(r0 + r) * ld + c0 + k] : T(0);
+        }
+    }
 };
 template <class T, int R, int K>
 __device__ __forceinline__ void mmts(const WLs<T, R, K>& W, const T (&b)[(K + 15) / 16][4],
@@ -87,15 +96,20 @@ __device__ __forceinline__ void dy3_back_tables(DP wl, const Dy3Stage& st, int C
     L::WRI::fill(wr, (const T*)RG2 + (size_t)st.cls * R * NU, R, 0, 0);
     L::WG::fill(wr + L::WRI::N, (const T*)RG2 + (size_t)st.cls * R * NU, R, NU, 0);
 }
-// forward image: K of the class, then per slot k [Abar_k | B_k]
+// forward image: K of the class, then per slot k [A_k | B_k] (x_j = A_k x + B_k u with
+// u = K x + d, the reference's Abar_k x + B_k d (cache.py:286-288) re-associated so that the
+// slot tables do not depend on the class: the top workgroup keeps them across stages)
 template <class T, int NX, int NU, class DP>
-__device__ __forceinline__ void dy3_fwd_tables(DP wl, const Dy3Stage& st, int C, const double* KM2, const double* F2) {
+__device__ __forceinline__ void dy3_fwd_tables(DP wl, const Dy3Stage& st, int C, const double* W2,
+                                               const double* KM2, const double* F2) {
     typedef Dy3Lds<T, NX, NU> L;
+    constexpr int R = NX + NU;
     L::WK::fill(wl, (const T*)KM2 + (size_t)st.cls * NU * NX, NU, 0, 0);
     DP wf = wl + L::WK::N;
     for (int k = 0; k < C; ++k) {
         const T* F = (const T*)F2 + (size_t)st.pair[k] * NX * (NX + NU);
-        L::WA::fill(wf + k * (L::WA::N + L::WG::N), F, NX, 0, 0);                 // Abar_k
+        // A_k[r][c] = (A_k')[c][r]: row NU + c, column r of W2[kind] (column-major, R rows)
+        L::WA::fill_t(wf + k * (L::WA::N + L::WG::N), (const T*)W2 + (size_t)st.kind[k] * R * NX, R, 0, NU);
         L::WG::fill(wf + k * (L::WA::N + L::WG::N) + L::WA::N, F, NX, 0, NX);    // B_k
     }
 }
@@ -105,7 +119,7 @@ __global__ void __launch_bounds__(512) k_dy3_image(Dy3Stage st, int C, const dou
                                                    const double* __restrict__ RG2, const double* __restrict__ KM2,
                                                    const double* __restrict__ F2, double* bimg, double* fimg) {
     dy3_back_tables<T, NX, NU>((glbp<T>)bimg, st, C, W2, RG2);
-    dy3_fwd_tables<T, NX, NU>((glbp<T>)fimg, st, C, KM2, F2);
+    dy3_fwd_tables<T, NX, NU>((glbp<T>)fimg, st, C, W2, KM2, F2);
 }
 
 template <class T, int NX, int NU>
@@ -154,6 +168,66 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
         ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)i * NU, live, u);
         ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
     };
+    // fp32 (config 5: two tiles per wave in the widest stage): a wave per tile, its next tile's
+    // rows double-buffered, issued before the current tile's slot products, so that a wide
+    // stage's load burst overlaps the MFMA chains instead of following them. Branch-free loads:
+    // a dead lane reads its tile's last live row, a slot k >= C re-reads slot C - 1 (valid
+    // addresses, results unused). (fp64: the second buffer spills at 32 / 12 and config 4's
+    // wide stages have one tile per wave: the single-buffer loop below.)
+    if constexpr (sizeof(T) == 4) if (!sp) {
+        T qn[4][RX][4], un[RU][4], xn[RX][4];
+        auto ld_all = [&](int task, T(&q)[4][RX][4], T(&uu)[RU][4], T(&xx)[RX][4]) {
+            const int ic = min(st.i0 + 16 * task + lo, st.i1 - 1);
+            cglbp<T> src = st.leaf ? (cglbp<T>)z + p.X0 : (cglbp<T>)qb;
+            _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+                const int kk = k < C ? k : C - 1;
+                ld_rows<T, NX>(src + (size_t)(1 + C * ic + kk) * NX, true, q[k]);
+            }
+            ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)ic * NU, true, uu);
+            ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)ic * NX, true, xx);
+        };
+        ld_all(min(gw, ntile - 1), qj, u, x);
+        dma_wait();
+        __syncthreads();
+        if (done) return;
+        for (int task = gw; task < ntile; task += nw) {
+            const int i = st.i0 + 16 * task + lo;
+            const bool live = i < st.i1;
+            ld_all(min(task + nw, ntile - 1), qn, un, xn);
+            v4 ha[RU], aa[RX];
+            _Pragma("unroll") for (int r = 0; r < RU; ++r) ha[r] = v4{0, 0, 0, 0};
+            _Pragma("unroll") for (int r = 0; r < RX; ++r) aa[r] = v4{0, 0, 0, 0};
+            _Pragma("unroll") for (int k = 0; k < 4; ++k) {
+                if (k >= C) continue;
+                if (st.leaf)
+                    _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) qj[k][rt][e] = -qj[k][rt][e];
+                const typename L::WB wb{wl + k * (L::WB::N + L::WA::N)};
+                const typename L::WA wa{wl + k * (L::WB::N + L::WA::N) + L::WB::N};
+                mmts(wb, qj[k], ha);
+                mmts(wa, qj[k], aa);
+            }
+            T v[RU][4];
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) v[rt][e] = u[rt][e] - ha[rt][e];
+            v4 dv[RU], gv[RX];
+            _Pragma("unroll") for (int r = 0; r < RU; ++r) dv[r] = v4{0, 0, 0, 0};
+            _Pragma("unroll") for (int r = 0; r < RX; ++r) gv[r] = v4{0, 0, 0, 0};
+            mmts(wri, v, dv);
+            mmts(wg, v, gv);
+            T dd[RU][4], qq[RX][4];
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) dd[rt][e] = dv[rt][e];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                qq[rt][e] = (-x[rt][e] + aa[rt][e]) + gv[rt][e];
+            st_rows<T, NU>(db + (size_t)i * NU, live, dd);
+            st_rows<T, NX>(qb + (size_t)i * NX, live, qq);
+            _Pragma("unroll") for (int k = 0; k < 4; ++k) _Pragma("unroll") for (int rt = 0; rt < RX; ++rt)
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) qj[k][rt][e] = qn[k][rt][e];
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) u[rt][e] = un[rt][e];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) x[rt][e] = xn[rt][e];
+        }
+        return;
+    }
+    // sp: a workgroup per tile (looping over tiles), wave k on child slot k; fp64: also a wave
+    // per tile
     if (gw < ntile) load(gw);
     dma_wait();
     __syncthreads();
@@ -273,7 +347,7 @@ __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ 
             v4 xa[RX];
             _Pragma("unroll") for (int r = 0; r < RX; ++r) xa[r] = v4{0, 0, 0, 0};
             mmts(wa, xc, xa);
-            mmts(wb, dc, xa);
+            mmts(wb, u, xa);
             T xj[RX][4];
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) xj[rt][e] = xa[rt][e];
             st_rows<T, NX>(z + p.X0 + (size_t)j * NX, live, xj);
@@ -290,7 +364,8 @@ __global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ 
 constexpr int kDy3TopMax = 8;
 struct Dy3Top {
     Dy3Stage st[kDy3TopMax];
-    int ts;  // stages 0 .. ts - 1
+    int ts;          // stages 0 .. ts - 1
+    int same_kinds;  // every top stage has the same child-slot kinds (the slot tables stay in LDS)
 };
 
 // backward, t = ts - 1 .. 0: rounds of TPR = waves / C tiles, wave w on tile w / C and child
@@ -314,9 +389,37 @@ __global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* __restri
     const int tpr = (blockDim.x >> 6) / C, tl = wv / C, k = wv - tl * C;
     lT* wr = wl + C * (L::WB::N + L::WA::N);
     lT* red = wl + L::back_n(C);  // [tpr][C][RU + RX][4][64 lanes]
+    // a round's rows (the children's q, the parents' u and x) are read into registers before
+    // the wait for the stage image, the first round's while the image is in flight: the image's
+    // and the rows' memory latencies overlap instead of following each other
+    T qj[RX][4], u[RU][4], x[RX][4];
+    auto load = [&](const Dy3Stage& st, int t0) {
+        const int task = t0 + tl;
+        const bool act = tl < tpr && task < ((st.i1 - st.i0 + 15) >> 4);
+        const int i = st.i0 + 16 * task + lo;
+        const bool live = act && i < st.i1;
+        if (!act) return;
+        const int j = 1 + C * (live ? i : st.i0) + k;
+        if (st.leaf) ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)j * NX, live, qj);
+        else ld_rows<T, NX>((cglbp<T>)qb + (size_t)j * NX, live, qj);
+        if (k == 0) {
+            ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)i * NU, live, u);
+            ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+        }
+    };
+    // the child slots' tables [B_k' | A_k'] depend on the slot's (A, B) kind only: when every
+    // top stage has the same kinds (tp.same_kinds) they stay in LDS after the first stage and a
+    // stage loads only its class's [Rinv | G] (a CU ingests ~12 B/cycle: the whole fp32 64/16
+    // image is ~3 us, the class part ~0.2 us)
+    const int off = C * (L::WB::N + L::WA::N);  // elements; a multiple of 64
     for (int si = tp.ts - 1; si >= 0; --si) {
         const Dy3Stage st = tp.st[si];
-        dma((ldsd*)dsm_, img0 + (size_t)si * L::back_n(C) * sizeof(T) / 8, L::back_n(C) * (int)sizeof(T) / 8);
+        const double* src = img0 + (size_t)si * L::back_n(C) * sizeof(T) / 8;
+        if (tp.same_kinds && si < tp.ts - 1)
+            dma((ldsd*)(wl + off), src + (size_t)off * sizeof(T) / 8, (L::back_n(C) - off) * (int)sizeof(T) / 8);
+        else
+            dma((ldsd*)dsm_, src, L::back_n(C) * (int)sizeof(T) / 8);
+        load(st, 0);
         dma_wait();
         __syncthreads();
         const typename L::WRI wri{wr};
@@ -331,14 +434,8 @@ __global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* __restri
             _Pragma("unroll") for (int r = 0; r < RU; ++r) ha[r] = v4{0, 0, 0, 0};
             _Pragma("unroll") for (int r = 0; r < RX; ++r) aa[r] = v4{0, 0, 0, 0};
             if (act) {
-                const int j = 1 + C * (live ? i : st.i0) + k;
-                T qj[RX][4];
-                if (st.leaf) {
-                    ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)j * NX, live, qj);
+                if (st.leaf)
                     _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) qj[rt][e] = -qj[rt][e];
-                } else {
-                    ld_rows<T, NX>((cglbp<T>)qb + (size_t)j * NX, live, qj);
-                }
                 const typename L::WB wb{wl + k * (L::WB::N + L::WA::N)};
                 const typename L::WA wa{wl + k * (L::WB::N + L::WA::N) + L::WB::N};
                 mmts(wb, qj, ha);
@@ -349,6 +446,7 @@ __global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* __restri
                         rd[(r * 4 + e) * 64 + l] = ha[r][e];
                     _Pragma("unroll") for (int r = 0; r < RX; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                         rd[((RU + r) * 4 + e) * 64 + l] = aa[r][e];
+                    load(st, t0 + tpr);  // the next round's rows behind this one's products
                 }
             }
             __syncthreads();
@@ -360,9 +458,7 @@ __global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* __restri
                     _Pragma("unroll") for (int r = 0; r < RX; ++r) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                         aa[r][e] += rd[((RU + r) * 4 + e) * 64 + l];
                 }
-                T u[RU][4], x[RX][4], v[RU][4];
-                ld_rows<T, NU>((cglbp<T>)z + p.U0 + (size_t)i * NU, live, u);
-                ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+                T v[RU][4];
                 _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) v[rt][e] = u[rt][e] - ha[rt][e];
                 v4 dv[RU], gv[RX];
                 _Pragma("unroll") for (int r = 0; r < RU; ++r) dv[r] = v4{0, 0, 0, 0};
@@ -375,6 +471,7 @@ __global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* __restri
                     qq[rt][e] = (-x[rt][e] + aa[rt][e]) + gv[rt][e];
                 st_rows<T, NU>(db + (size_t)i * NU, live, dd);
                 st_rows<T, NX>(qb + (size_t)i * NX, live, qq);
+                load(st, t0 + tpr);
             }
             __syncthreads();  // red is rewritten by the next round; the rows by the next stage
         }
@@ -398,42 +495,53 @@ __global__ void __launch_bounds__(512) k_dy3_top_fwd(Dev p, const Ctl* __restric
     cglbp<T> db = (cglbp<T>)d_;
     const int lo = threadIdx.x & 15, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     lT* wf = wl + L::WK::N;
+    // a task's x and d rows are read before the wait for the stage image (the first task's
+    // while the image is in flight, the next task's behind the current one's products)
+    T x[RX][4], d[RU][4];
+    auto load = [&](const Dy3Stage& st, int tk) {
+        const int task = tk / C;
+        const int i = st.i0 + 16 * task + lo;
+        const bool live = i < st.i1;
+        if (i == 0) ld_rows<T, NX>((cglbp<T>)x0_, true, x);  // x_0 = x0bar (cache.py:283)
+        else ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
+        ld_rows<T, NU>(db + (size_t)i * NU, live, d);
+    };
     for (int si = 0; si < tp.ts; ++si) {
         const Dy3Stage st = tp.st[si];
-        dma((ldsd*)dsm_, img0 + (size_t)si * L::fwd_n(C) * sizeof(T) / 8, L::fwd_n(C) * (int)sizeof(T) / 8);
+        const int ntile = (st.i1 - st.i0 + 15) >> 4, ntask = ntile * C;
+        // the slot tables [A_k | B_k] stay in LDS after the first stage when the kinds agree
+        const int nload = tp.same_kinds && si > 0 ? L::WK::N : L::fwd_n(C);
+        dma((ldsd*)dsm_, img0 + (size_t)si * L::fwd_n(C) * sizeof(T) / 8, nload * (int)sizeof(T) / 8);
+        if (wv < ntask) load(st, wv);
         dma_wait();
         __syncthreads();
         const typename L::WK wk{wl};
-        const int ntile = (st.i1 - st.i0 + 15) >> 4, ntask = ntile * C;
         for (int tk = wv; tk < ntask; tk += nwv) {
             const int task = tk / C, ks = tk - task * C;
             const int i = st.i0 + 16 * task + lo;
             const bool live = i < st.i1;
-            T x[RX][4], d[RU][4];
-            if (i == 0) {
-                ld_rows<T, NX>((cglbp<T>)x0_, true, x);  // x_0 = x0bar (cache.py:283)
-                if (ks == 0) st_rows<T, NX>(z + p.X0, true, x);
-            } else {
-                ld_rows<T, NX>((cglbp<T>)z + p.X0 + (size_t)i * NX, live, x);
-            }
-            ld_rows<T, NU>(db + (size_t)i * NU, live, d);
+            T xc[RX][4], dc[RU][4];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) xc[rt][e] = x[rt][e];
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) dc[rt][e] = d[rt][e];
+            if (tk + nwv < ntask) load(st, tk + nwv);
+            if (i == 0 && ks == 0) st_rows<T, NX>(z + p.X0, true, xc);
             v4 ku[RU];
             _Pragma("unroll") for (int r = 0; r < RU; ++r) ku[r] = v4{0, 0, 0, 0};
-            mmts(wk, x, ku);
+            mmts(wk, xc, ku);
             T u[RU][4];
-            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) u[rt][e] = ku[rt][e] + d[rt][e];
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) u[rt][e] = ku[rt][e] + dc[rt][e];
             if (ks == 0) st_rows<T, NU>(z + p.U0 + (size_t)i * NU, live, u);
             const int j = 1 + C * (live ? i : st.i0) + ks;
             const typename L::WA wa{wf + ks * (L::WA::N + L::WG::N)};
             const typename L::WG wb{wf + ks * (L::WA::N + L::WG::N) + L::WA::N};
             v4 xa[RX];
             _Pragma("unroll") for (int r = 0; r < RX; ++r) xa[r] = v4{0, 0, 0, 0};
-            mmts(wa, x, xa);
-            mmts(wb, d, xa);
+            mmts(wa, xc, xa);
+            mmts(wb, u, xa);
             T xj[RX][4];
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) xj[rt][e] = xa[rt][e];
             st_rows<T, NX>(z + p.X0 + (size_t)j * NX, live, xj);
         }
-        __syncthreads();  // the children's x rows are the next stage's inputs
+        __syncthreads();  // the children's x rows are the next stage's inputs; the image is rewritten
     }
 }

@@ -11,6 +11,14 @@
 //   [Tc, Tc + Tl)    leaf tiles: eta11_l = sqrtPf x_l, eta12 = eta13 = s_l / 2, eta14_l = x_l
 //   [.., + Tp)       parent chunks of 64 rows of the flat list [eta7 rows | eta1 | eta2]
 
+// waves per SIMD the compiler budgets k_ell3 / k_ellt3's registers for (build-time
+// -DELL3_WPE=...): 3 = at most 168 registers (<double, 32, 12>: 146, no spills, from 156 + 24
+// AGPRs at two waves); nx = 64 asks for two waves in fp32 and none in fp64 (its tiles spill
+// at 168 and 256 registers)
+#ifndef ELL3_WPE
+#define ELL3_WPE 3
+#endif
+#define ELL3_WPE_OF(T, NX) ((NX) >= 64 ? (sizeof(T) == 8 ? 1 : 2) : ELL3_WPE)
 // weights of one table, k-permuted: b[rt][s] = M[row 16 rt + lo][KC h + s]; R rows, K cols
 template <class T, int R, int K>
 struct WPerm {
@@ -130,7 +138,8 @@ __device__ __forceinline__ int o14_of(const Dev& p, int l, int bx) {
 // wave's next tile, then the MFMAs and stores: vmcnt is in order, so an operand loaded after
 // the prefetch would make the epilogue wait for the prefetched tile too.
 template <class T, int NX, int NU>
-__global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ z_, double* __restrict__ eta_, int C, int bx) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ELL3_WPE_OF(T, NX))))
+k_ell3(Dev p, const double* __restrict__ z_, double* __restrict__ eta_, int C, int bx) {
     typedef typename MF<T>::v4 v4;
     constexpr int nx = NX, nu = NU, RTX = (NX + 15) / 16, RTU = (NU + 15) / 16;
     const int n = p.n, m = p.m;
@@ -327,7 +336,8 @@ __global__ void __launch_bounds__(256) k_ell3(Dev p, const double* __restrict__ 
 //   [.., + Tf)     flat chunks of 64 rows of [y | s | tau_1..]: y_i = eta1_i - b_i eta2_i,
 //                  s_i = eta2_i (nonleaf), s_l = (eta12_l + eta13_l) / 2, tau_j = (eta5_j + eta6_j) / 2
 template <class T, int NX, int NU, int QM>  // QM = 4 / C parents per lane (compile time: register arrays)
-__global__ void __launch_bounds__(256) k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C, int bx) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ELL3_WPE_OF(T, NX))))
+k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C, int bx) {
     typedef typename MF<T>::v4 v4;
     constexpr int nx = NX, nu = NU, RTX = (NX + 15) / 16, RTU = (NU + 15) / 16;
     const int n = p.n, m = p.m;

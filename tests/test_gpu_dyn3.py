@@ -141,9 +141,10 @@ def test_kernel_info_lists_the_projection_launches():
 
 @pytest.mark.parametrize("cfg,dtype", [(4, "float64"), (2, "float64"), (5, "float32")])
 def test_top_stages_in_one_workgroup_bit_identical(cfg, dtype):
-    """k_dy3_top_back / k_dy3_top_fwd (the top stages back to back in one workgroup) sum the
-    child slots in the order of the slot-parallel per-stage launches they replace
-    (RAOCP_DY3_TOP=0): the projection and a 12-iteration CP loop are bit-identical."""
+    """k_dy3_top_back / k_dy3_top_fwd (the top stages back to back in one workgroup, the
+    child-slot tables kept in LDS across stages) sum the child slots in the order of the
+    slot-parallel per-stage launches they replace (RAOCP_DY3_TOP=0): the projection and a
+    12-iteration CP loop are bit-identical (stage 3 of configs 4 and 5 takes two rounds)."""
     r = recipe_config(cfg)
     prob = build_problem(r)[1]
     env = {"RAOCP_DYN3": "1"} if cfg == 2 else {}

@@ -10,6 +10,8 @@
 #   dyn         dynamics projection timings at config 2 (tools/dyn_time.py, variants in $DYN_VARIANTS)
 #   stamps      in-kernel stamps of the regular-tree sweep at config 2 (tools/dr_stamps.py)
 #   cp          CP kernel / dynamics / loop timings (tools/cp3_time.py)
+#   lsweep      standalone L / L^T at configs 2, 4 (3 buffer sets) and 5 fp32 (2 sets)
+#   dy3trace    per-launch trace of the config-4 / config-5 dynamics (rocprofv3 kernel trace, tools/trace_seq.py)
 #   bench20     bench.py --steps 20 --warmup 5 (the driver's K)
 #   bench       bench.py default run
 #   prof        rocprofv3 --kernel-trace --stats of bench.py (eager launches)
@@ -43,6 +45,13 @@ for step in "$@"; do
           cat $out/stamps_c2.log ;;
     cp) timeout -k 10 500 python -u tools/cp3_time.py ${CP_ARGS:-} > $out/cp3_time.log 2>&1 || fail $step $out/cp3_time.log
           cat $out/cp3_time.log ;;
+    lsweep) for a in "2 float64 1" "4 float64 3" "5 float32 2"; do
+              timeout -k 10 200 python -u tools/l_sweep.py $a >> $out/l_sweep.log 2>&1 || fail $step $out/l_sweep.log
+            done; grep config $out/l_sweep.log ;;
+    dy3trace) for cfg in 4 5; do
+                timeout -k 10 240 rocprofv3 --kernel-trace -d $out/tr$cfg -o tr --output-format csv -- python3 tools/dyn_time.py child $cfg trace > $out/tr$cfg.log 2>&1 || fail $step $out/tr$cfg.log
+                python3 tools/trace_seq.py $out/tr$cfg 30 > $out/dy3_stages_c$cfg.log; cat $out/dy3_stages_c$cfg.log
+              done ;;
     bench20) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $out/bench_k20.log 2>&1 || fail $step $out/bench_k20.log
           tail -1 $out/bench_k20.log > $out/bench_k20.json; cut -c1-400 $out/bench_k20.json ;;
     bench) timeout -k 10 500 python -u bench.py > $out/bench.log 2>&1 || fail $step $out/bench.log

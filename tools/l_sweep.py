@@ -1,5 +1,7 @@
-"""L / L^T launch times (op_bench: graph of back-to-back launches, HIP events) at a config,
-fp64 or fp32. python tools/l_sweep.py <config> [float32]"""
+"""Standalone L / L^T at a config, as bench.py's l_sweep measures them (op_pair: HIP events
+over a graph of back-to-back launches cycling over nsets buffer sets, beyond the 256 MiB
+Infinity Cache for nsets * bytes > 256 MiB). python tools/l_sweep.py <config> [dtype] [nsets]"""
+import json
 import os
 import sys
 
@@ -7,14 +9,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "raocp-toolbox_amd"), ROOT]
 import raocp.core as core  # noqa: E402
 from raocp.problems import build_problem, recipe_config  # noqa: E402
-from bench import active_sizes  # noqa: E402
+from bench import op_pair  # noqa: E402
 
 cfg = int(sys.argv[1])
 dt = sys.argv[2] if len(sys.argv) > 2 else "float64"
+nsets = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 c = core.Cache(build_problem(recipe_config(cfg))[1], dtype=dt)
-P, D = active_sizes(c)
-w = 4 if dt == "float32" else 8
-for op, name in ((0, "L"), (1, "L^T")):
-    ms = c.native.op_bench(op, 200)
-    print(f"config {cfg} {dt} {name}: {1e3 * ms:.2f} us, {w * (P + D) / (ms * 1e-3) / 1e9:.0f} GB/s "
-          f"({w * (P + D) / 1e6:.1f} MB per launch)", flush=True)
+res = op_pair(c.native, c, 4 if dt == "float32" else 8, 200, nsets)
+for k in ("L", "L_transpose"):
+    r = res[k]
+    print(f"config {cfg} {dt} {k:12s} {r['kernel']:34s} {r['us_per_launch']:8.2f} us  frac {r['frac']:.3f}", flush=True)
+print(json.dumps(res))
