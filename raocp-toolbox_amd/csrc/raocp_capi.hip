@@ -60,8 +60,10 @@ struct raocp_ctx {
     int ellt3_grid = 0;
     bool cp3 = false;            // the CP iteration after the dynamics as one streaming kernel (raocp_cp3.hip)
     bool cp4 = false;            // ... with every operand of a tile loaded at its start (raocp_cp4.hip; RAOCP_CP4=0: off)
-    int cp4_wpb = 1;             // k_cp4's waves per workgroup (one task per wave; RAOCP_CP4_WAVES): one
-                                 // spreads the tasks' load bursts over all CUs (config 2: 16.7 vs 18.5 us at four)
+    int cp4_wpb = 2;             // k_cp4's waves per workgroup, one task per workgroup: 2 = helper mode (wave 1
+                                 // takes a leaf-parent tile's leaf children), 1 = one wave (RAOCP_CP4_HELPER=0);
+                                 // one task per workgroup spreads the load bursts over all CUs (round 4: one
+                                 // task per wave at four waves per workgroup 18.5 vs 16.7 us at one)
     int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
     int cp3_split = 0;           // leaves as tasks of their own (small trees: more waves, shorter chains)
@@ -2712,8 +2714,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             c->cp4 = raocp::cp4_supported(c->f32, nx, nu, c->unif_C, c->box_mode);
             if (const char* e = getenv("RAOCP_CP4")) c->cp4 = c->cp4 && atoi(e) != 0;
             if (c->cp4) {  // k_cp4: cp4_wpb waves per workgroup, the same waves over more CUs
-                if (const char* e = getenv("RAOCP_CP4_WAVES")) c->cp4_wpb = std::max(1, std::min(4, atoi(e)));
-                c->cp3_grid = c->cp3_grid * 4 / c->cp4_wpb;
+                if (const char* e = getenv("RAOCP_CP4_HELPER")) c->cp4_wpb = atoi(e) ? 2 : 1;
+                c->cp3_grid = c->cp3_grid * 4;  // one task per workgroup
                 if (c->cp3_grid > c->red_rows) {
                     c->red_rows = c->cp3_grid;
                     if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);

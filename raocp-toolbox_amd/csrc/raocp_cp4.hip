@@ -288,8 +288,13 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
     const int m = p.m;
     const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4, wv = threadIdx.x >> 6;
     const int gw = blockIdx.x * (blockDim.x >> 6) + wv, nwv = gridDim.x * (blockDim.x >> 6);
+    // helper mode (two-wave workgroups, one task each): wave 0 runs the task; on a tile of
+    // leaf parents wave 1 runs the leaf children's work (the parent-side s_l into its scratch,
+    // read by wave 0 in phase 5), off wave 0's chain. Else one task per wave.
+    const bool hm = blockDim.x == 128;
     typedef __attribute__((address_space(3))) KpScratch<T> lkps;
     lkps& ks = *(lkps*)&kps_[wv];
+    const lkps& kh = *(const lkps*)&kps_[1];  // helper mode: wave 1's scratch
     cglbp<T> pz = (cglbp<T>)bf.z0;  // p
     cglbp<T> zp = (cglbp<T>)bf.z1;  // z+
     glbp<T> out = (glbp<T>)bf.z2;   // next half step
@@ -448,12 +453,13 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
         FamIn<T, NX, NU, C, BXN, LEAFP> in;
         LeafIn<T, NX, BXL> lf[LEAFP ? C : 1];
         // ---- every operand of the tile, in first-use order (vmcnt retires in issue order)
-        if (LEAFP)
+        if (LEAFP && !hm)
             _Pragma("unroll") for (int k = 0; k < C; ++k) lf[k].load(p, zp, pz, d, 1 + C * i + k, live, !split);
         in.load(p, zp, pz, d, cond, i, live);
         stamp();  // loads issued
         // ---------------- phase 4 (parents of leaves): leaf children; their s_l to the scratch
-        if (LEAFP)
+        // (helper mode: wave 1 of the workgroup)
+        if (LEAFP && !hm)
             _Pragma("unroll") for (int k = 0; k < C; ++k) leaf_work(lf[k], 1 + C * i + k, k, live, !split, true);
         stamp();
         // ---------------- phase 1: the parent's rows
@@ -685,6 +691,11 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
         }
         stamp();
         // ---------------- phase 5: AVaR kernel projection of the family (cache.py:290-317)
+        if (hm) {
+            __syncthreads();  // the helper's leaf children are done
+            if (LEAFP)
+                _Pragma("unroll") for (int k = 0; k < C; ++k) ks.s[lo][k] = kh.s[lo][k];
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -717,13 +728,33 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
             if (h == 0) out[p.Y0 + yo + 2 * C] = y2c - sw;
         }
         __builtin_amdgcn_wave_barrier();
+        if (hm) __syncthreads();  // the helper's scratch is rewritten by the next task
         stamp();
     };
     const int split = tk.split;
     const int nTL = (tk.l1 - tk.l0 + 15) >> 4;  // leaf tiles (split), then the parent ranges' tiles
     // diagnostics: every wave's [first task start, last task end] at stamps[32 + 2 gw]
     const unsigned long long w_t0 = p.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    for (int tt = gw; tt < nTL + tk.t0[tk.nr]; tt += nwv) {
+    for (int tt = hm ? (int)blockIdx.x : gw; tt < nTL + tk.t0[tk.nr]; tt += hm ? (int)gridDim.x : nwv) {
+        if (hm && wv == 1) {
+            // the helper: a leaf-parent tile's leaf children (phase 4 of the family), then the
+            // task's two barriers
+            if (tt >= nTL) {
+                const int task = tt - nTL;
+                int r = 0;
+                while (r + 1 < tk.nr && task >= tk.t0[r + 1]) ++r;
+                if (tk.lo[r] >= tk.mL) {
+                    const int i = tk.lo[r] + 16 * (task - tk.t0[r]) + lo;
+                    const bool live = i < tk.hi[r];
+                    LeafIn<T, NX, BXL> lf[C];
+                    _Pragma("unroll") for (int k = 0; k < C; ++k) lf[k].load(p, zp, pz, d, 1 + C * i + k, live, !split);
+                    _Pragma("unroll") for (int k = 0; k < C; ++k) leaf_work(lf[k], 1 + C * i + k, k, live, !split, true);
+                }
+            }
+            __syncthreads();
+            __syncthreads();
+            continue;
+        }
         if (tt < nTL) {
             // a tile of 16 consecutive leaves (split): everything of the leaf but s_l
             const int l = tk.l0 + 16 * tt + lo;
@@ -731,6 +762,10 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
             LeafIn<T, NX, BXL> cur;
             cur.load(p, zp, pz, d, l, live, true);
             leaf_work(cur, l, 0, live, true, false);
+            if (hm) {
+                __syncthreads();
+                __syncthreads();
+            }
             continue;
         }
         const int task = tt - nTL;

@@ -10,7 +10,8 @@ level: the two kernels agree to 1e-12 (residual histories per entry, final prima
 against the oracle 1e-8 per residual entry (BASELINE.json north_star) and 1e-10 on the
 iterate. Cases: config 2 with its
 boxes, without boxes, with leaf boxes only; the leaves inside their families' tiles
-(RAOCP_CP3_SPLIT=0); a graph batch boundary (30 iterations) and an early stop.
+(RAOCP_CP3_SPLIT=0); one-wave workgroups (RAOCP_CP4_HELPER=0) against the default helper mode;
+a graph batch boundary (30 iterations) and an early stop.
 """
 import os
 
@@ -47,8 +48,9 @@ def _recipe(case):
 
 
 @pytest.mark.parametrize("case,env", [("boxed", {}), ("nobox", {}), ("leafbox", {}),
-                                      ("boxed", {"RAOCP_CP3_SPLIT": "0"})],
-                         ids=["boxed", "nobox", "leafbox", "nosplit"])
+                                      ("boxed", {"RAOCP_CP3_SPLIT": "0"}), ("boxed", {"RAOCP_CP4_HELPER": "0"}),
+                                      ("nobox", {"RAOCP_CP3_SPLIT": "0", "RAOCP_CP4_HELPER": "0"})],
+                         ids=["boxed", "nobox", "leafbox", "nosplit", "onewave", "nosplit-onewave"])
 def test_cp4_matches_cp3_bit_for_bit_and_oracle(case, env):
     from oracle.raocp_oracle import OracleProblem
     r = _recipe(case)
@@ -86,3 +88,23 @@ def test_cp4_early_stop_matches_cp3():
     assert out[0][0] == out[1][0]
     assert trace_rel_err(out[0][1], out[1][1]) <= 1e-12 and rel_err(out[0][3], out[1][3]) <= 1e-12
     assert out[0][0] == 0 and out[0][1].shape[0] <= 42
+
+
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_cp4_helper_wave_bit_identical(split):
+    """Helper mode (default: a two-wave workgroup per task, wave 1 running a leaf-parent tile's
+    leaf children) moves work between waves only: the 30-iteration loop equals the one-wave
+    workgroups (RAOCP_CP4_HELPER=0) bit for bit."""
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    env = {"RAOCP_CP3_SPLIT": split}
+    a = _with_env(env, lambda: core.Cache(prob))
+    b = _with_env({**env, "RAOCP_CP4_HELPER": "0"}, lambda: core.Cache(prob))
+    alpha = 0.999 / a.native.step_size()
+    out = []
+    for cache in (a, b):
+        st, err, derr = cache.native.cp_run(r["x0"], 30, 0.0, alpha)
+        out.append((st, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
+    for u, v in zip(out[0], out[1]):
+        assert np.array_equal(u, v)
+

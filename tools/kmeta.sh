@@ -1,13 +1,33 @@
 #!/bin/bash
 # Kernel resource metadata (VGPRs, AGPRs, spills, scratch, LDS) of the built library's gfx950
-# code object: tools/kmeta.sh [kernel-name-regex]
+# code objects: tools/kmeta.sh [kernel-name-regex]. The library links several HIP translation
+# units (raocp_capi, raocp_dynr, raocp_cp4): its .hip_fatbin section holds one offload bundle
+# per unit, each unbundled here.
 set -e
 LIB=${LIB:-/root/repo/raocp-toolbox_amd/raocp/core/libraocp_hip.so}
 D=$(mktemp -d)
 objcopy --dump-section .hip_fatbin=$D/fat.bin "$LIB"
-/opt/rocm/llvm/bin/clang-offload-bundler --type=o --unbundle --input=$D/fat.bin \
-  --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output=$D/gfx950.co
-/opt/rocm/llvm/bin/llvm-readelf --notes $D/gfx950.co > $D/notes.txt
+python3 - "$D" <<'PY'
+import sys
+d = sys.argv[1]
+data = open(f"{d}/fat.bin", "rb").read()
+magic = b"__CLANG_OFFLOAD_BUNDLE__"
+offs = []
+i = data.find(magic)
+while i >= 0:
+    offs.append(i)
+    i = data.find(magic, i + 1)
+offs.append(len(data))
+for n in range(len(offs) - 1):
+    open(f"{d}/b{n}.bin", "wb").write(data[offs[n]:offs[n + 1]])
+PY
+: > $D/notes.txt
+for b in $D/b*.bin; do
+  if /opt/rocm/llvm/bin/clang-offload-bundler --type=o --unbundle --input=$b \
+       --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output=$b.co 2>/dev/null; then
+    /opt/rocm/llvm/bin/llvm-readelf --notes $b.co >> $D/notes.txt 2>/dev/null || true
+  fi
+done
 python3 - "$D/notes.txt" "${1:-.}" <<'PY'
 import re, sys
 txt = open(sys.argv[1]).read()
