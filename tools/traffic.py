@@ -44,5 +44,5 @@ for a, ks in alias.items():
         out[a] = dict(out[next(iter(ks))], alias_of=next(iter(ks)))
 json.dump({"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH x2 (gfx950), KB x1024",
            "kernels": out}, open(f"profiles/{tag}/traffic.json", "w"), indent=1)
-for k, v in sorted(out.items(), key=lambda kv: -kv[1]["traffic_bytes"]):
+for k, v in sorted(((k, v) for k, v in out.items() if "alias_of" not in v), key=lambda kv: -kv[1]["traffic_bytes"]):
     print(f"{k:28s} {v['traffic_bytes'] / 1e6:10.3f} MB/launch  ({v['launches']} launches)")
