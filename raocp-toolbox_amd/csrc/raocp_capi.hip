@@ -6,6 +6,7 @@
 #include "raocp_kernels.hip"
 #include "raocp_dynr.h"
 #include "raocp_cp4.h"
+#include "raocp_cp5.h"
 #include "../../include/raocp_hip.h"
 
 #include <dlfcn.h>
@@ -64,6 +65,10 @@ struct raocp_ctx {
                                  // takes a leaf-parent tile's leaf children), 1 = one wave (RAOCP_CP4_HELPER=0);
                                  // one task per workgroup spreads the load bursts over all CUs (round 4: one
                                  // task per wave at four waves per workgroup 18.5 vs 16.7 us at one)
+    bool cp5 = false;            // ... as a leaf launch and a family launch (raocp_cp5.hip: configs 3, 4, 5;
+                                 // RAOCP_CP5=0: off)
+    raocp::Cp3Tasks cp5_tk{};    // k_cp5_fam's task list (every parent, leaf parents first)
+    int cp5_gl = 0, cp5_gf = 0;  // grids of the two launches
     int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
     int cp3_split = 0;           // leaves as tasks of their own (small trees: more waves, shorter chains)
@@ -875,9 +880,10 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
     p.X0 = c->dev.X0;
     p.U0 = c->dev.U0;
     c->dr_block = block;
-    // diagnostics (tests/test_gpu_dynr.py): RAOCP_DR_FAULT=1 makes the deepest tier's first
-    // subtree skip its publish, so its parent's wait times out
-    if (const char* e = getenv("RAOCP_DR_FAULT")) p.fault = atoi(e);
+    // error-path test (tests/test_gpu_dynr.py): RAOCP_DR_FAULT=1 makes the deepest tier's first
+    // subtree skip its publish, so its parent's wait times out and the call fails; the
+    // timing-only bits (no DMA / arithmetic / write-out) exist in diagnostic builds only
+    if (const char* e = getenv("RAOCP_DR_FAULT")) p.fault = atoi(e) & (raocp::kDiag ? ~0 : 1);
     int rc;
     const double *bi = nullptr, *fi = nullptr;
     unsigned long long *gq = nullptr, *gx = nullptr;
@@ -1083,6 +1089,11 @@ int cp3_image(raocp_ctx* c) {
     return cp3_imaget<double, 32, 12>(c);
 }
 void launch_cp3(raocp_ctx* c, int part = 0) {
+    if (c->cp5 && c->sh_S == 0) {
+        raocp::cp5_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->m, c->n, c->cp5_gl, c->cp5_tk,
+                          c->cp5_gf, c->cp3img, c->stream);
+        return;
+    }
     if (c->cp4 && c->sh_S == 0) {
         raocp::cp4_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->cp3_ta, c->cp3img, c->cp3_grid,
                           c->cp4_wpb, c->stream);
@@ -1328,6 +1339,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             return s;
         }
         case 10:
+            if (c->cp5 && c->sh_S == 0) return raocp::cp5_name(c->f32, c->nx, c->nu, c->unif_C);
             if (c->cp4 && c->sh_S == 0) return raocp::cp4_name(c->f32, c->nx, c->nu);
             if (c->cp3) return "k_cp3<" + T + ", " + nn + (c->sh_S > 0 ? ", true> x2" : ", false>");
             return kernel_name(c, 2) + " + " + kernel_name(c, 6);
@@ -2715,7 +2727,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             if (const char* e = getenv("RAOCP_CP4")) c->cp4 = c->cp4 && atoi(e) != 0;
             if (c->cp4) {  // k_cp4: cp4_wpb waves per workgroup, the same waves over more CUs
                 if (const char* e = getenv("RAOCP_CP4_HELPER")) c->cp4_wpb = atoi(e) ? 2 : 1;
-                c->cp3_grid = c->cp3_grid * 4;  // one task per workgroup
+                c->cp3_grid = (int)std::max(1L, std::min(tiles, 8192L));  // one task per workgroup
+                if (const char* e = getenv("RAOCP_CP4_GRID")) c->cp3_grid = std::max(1, atoi(e));
                 if (c->cp3_grid > c->red_rows) {
                     c->red_rows = c->cp3_grid;
                     if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
@@ -2724,10 +2737,29 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 }
                 c->cp_rows = c->cp3_grid;
             }
+            // k_cp5: the leaf tiles and the family tiles as two launches with small register
+            // files (configs 3, 4, 5; k_cp4 keeps config 2)
+            c->cp5 = !c->cp4 && raocp::cp5_supported(c->f32, nx, nu, c->unif_C, c->box_mode, c->dev.nBnl, c->dev.nBl);
+            if (const char* e = getenv("RAOCP_CP5")) c->cp5 = c->cp5 && atoi(e) != 0;
+            if (c->cp5) {
+                if (cp3_tasks(c->cp5_tk, {{c->cp3_mL, m}, {0, c->cp3_mL}}, 0, 0, 1, c->cp3_mL) < 0)
+                    return bail(fail(RAOCP_ERR_ARG, "k_cp5 task list exceeds its parent-range slots"));
+                c->cp5_gl = raocp::cp5_leaf_grid(m, n);
+                c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk);
+                if (const char* e = getenv("RAOCP_CP5_LGRID")) c->cp5_gl = std::max(1, atoi(e));
+                if (const char* e = getenv("RAOCP_CP5_FGRID")) c->cp5_gf = std::max(1, atoi(e));
+                c->cp_rows = c->cp5_gl + c->cp5_gf;
+                if (c->cp_rows > c->red_rows) {
+                    c->red_rows = c->cp_rows;
+                    if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
+                    if (hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)) != hipSuccess)
+                        return bail(fail(RAOCP_ERR_HIP, "memset"));
+                }
+            }
         }
     }
-    c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics of the MFMA CP kernels
-    if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = atoi(e);
+    c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics (diagnostic builds only)
+    if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = raocp::kDiag ? atoi(e) : 0;
     if (const char* e = getenv("RAOCP_DEFER_CHECK")) c->no_defer_check = atoi(e) == 0;
     c->drp.zpage = c->dev.zpage;
     c->drp.x0 = c->x0;
@@ -3168,6 +3200,7 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
 // `cap` raw 100 MHz timestamps.
 int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
     DevGuard dg_(c);
+    if (!raocp::kDiag) return fail(RAOCP_ERR_ARG, "in-kernel stamps need a diagnostic build (make DIAG=1)");
     if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c || !out || cap <= 0) return fail(RAOCP_ERR_ARG, "bad argument");
     // the tiered sweep stamps 64 slots per launch (2 per tier + the top)

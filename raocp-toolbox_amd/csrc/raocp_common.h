@@ -11,6 +11,15 @@
 
 namespace raocp {
 
+// Diagnostic builds (make DIAG=1, -DRAOCP_DIAG) compile in the in-kernel timestamps and the
+// timing-only modes that skip work (RAOCP_CP2_DBG, RAOCP_DR_FAULT bits 2-5); a release build
+// folds every such test to false, so no product kernel carries a path that skips arithmetic.
+#ifdef RAOCP_DIAG
+constexpr bool kDiag = true;
+#else
+constexpr bool kDiag = false;
+#endif
+
 typedef unsigned long long u64;
 
 struct Ctl {

@@ -21,147 +21,13 @@
 // per workgroup; other trees read their node's table from global memory at its use.
 
 #include "raocp_cp4.h"
+#include "raocp_tile.h"
 
 namespace raocp {
 namespace {
 
-template <class U>
-using glbp = __attribute__((address_space(1))) U*;
-template <class U>
-using cglbp = const __attribute__((address_space(1))) U*;
-typedef __attribute__((address_space(3))) double lds_d;
-
-// ---- 16x16x4 MFMA in T (raocp_cp2.hip) -------------------------------------------------
-template <class T>
-struct MF;
-template <>
-struct MF<double> {
-    typedef double v4 __attribute__((ext_vector_type(4)));
-    static __device__ __forceinline__ v4 mma(double a, double b, v4 c) {
-        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
-    }
-};
-template <>
-struct MF<float> {
-    typedef float v4 __attribute__((ext_vector_type(4)));
-    static __device__ __forceinline__ v4 mma(float a, float b, v4 c) {
-        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
-    }
-};
-
-// weight fragments of one R x K table in LDS (k_cp3_image order, raocp_cp3.hip WL):
-// lds[(ro KS + s) 64 + lane]
-template <class T, int R, int K>
-struct WL {
-    static constexpr int RO = (R / 4 + 3) / 4, KS = K / 4, N = RO * KS * 64;
-    const __attribute__((address_space(3))) T* base;
-    __device__ __forceinline__ T get(int ro, int s) const { return base[(ro * KS + s) * 64 + (threadIdx.x & 63)]; }
-};
-template <class T, int R, int K>
-__device__ __forceinline__ void mmt(const WL<T, R, K>& W, const T (&b)[(K + 15) / 16][4],
-                                    typename MF<T>::v4 (&acc)[(R + 15) / 16]) {
-    _Pragma("unroll") for (int s = 0; s < WL<T, R, K>::KS; ++s)
-        _Pragma("unroll") for (int ro = 0; ro < WL<T, R, K>::RO; ++ro)
-            acc[ro] = MF<T>::mma(W.get(ro, s), b[s >> 2][s & 3], acc[ro]);
-}
-
-template <class T>
-struct V4a {
-    typedef T type __attribute__((ext_vector_type(4), aligned(sizeof(T))));
-};
-template <int R>
-__device__ __forceinline__ constexpr bool tok(int rt, int e) {
-    return 4 * rt + e < R / 4;
-}
-// row-layout load / store of an R-row node vector (raocp_cp3.hip): a[rt][e] = v[R/4 h + 4 rt + e]
-template <class T, int R>
-// (v must be a valid row address even when !live: every load is issued unconditionally and
-// the value selected after it — a load under a runtime condition makes the compiler branch
-// around it and wait for it on its own, one memory round trip per load)
-__device__ __forceinline__ void ld_rows(cglbp<T> v, bool live, T (&a)[(R + 15) / 16][4]) {
-    typedef typename V4a<T>::type vt;
-    constexpr int KC = R / 4;
-    cglbp<T> b = v + KC * ((threadIdx.x & 63) >> 4);
-    _Pragma("unroll") for (int rt = 0; rt < (R + 15) / 16; ++rt) {
-        if (4 * rt + 3 < KC) {
-            const vt w = *(const __attribute__((address_space(1))) vt*)(b + 4 * rt);
-            _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = live ? w[e] : T(0);
-        } else {
-            _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                T w = T(0);
-                if (tok<R>(rt, e)) w = b[4 * rt + e];
-                a[rt][e] = live ? w : T(0);
-            }
-        }
-    }
-}
-// one scalar at a valid address, zero when !live (unconditional load, see ld_rows)
-template <class T>
-__device__ __forceinline__ T ldz(cglbp<T> v, bool live) {
-    const T w = *v;
-    return live ? w : T(0);
-}
-template <class T, int R>
-__device__ __forceinline__ void st_rows(glbp<T> v, bool live, const T (&a)[(R + 15) / 16][4]) {
-    typedef typename V4a<T>::type vt;
-    constexpr int KC = R / 4;
-    glbp<T> b = v + KC * ((threadIdx.x & 63) >> 4);
-    _Pragma("unroll") for (int rt = 0; rt < (R + 15) / 16; ++rt) {
-        if (!live) continue;
-        if (4 * rt + 3 < KC) {
-            vt w;
-            _Pragma("unroll") for (int e = 0; e < 4; ++e) w[e] = a[rt][e];
-            *(__attribute__((address_space(1))) vt*)(b + 4 * rt) = w;
-        } else {
-            _Pragma("unroll") for (int e = 0; e < 4; ++e)
-                if (tok<R>(rt, e)) b[4 * rt + e] = a[rt][e];
-        }
-    }
-}
-// the same from LDS rows (the box bounds of one-table trees)
-template <class T, int R>
-__device__ __forceinline__ void ld_rows_lds(const __attribute__((address_space(3))) T* v, T (&a)[(R + 15) / 16][4]) {
-    constexpr int KC = R / 4;
-    const __attribute__((address_space(3))) T* b = v + KC * ((threadIdx.x & 63) >> 4);
-    _Pragma("unroll") for (int rt = 0; rt < (R + 15) / 16; ++rt)
-        _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = tok<R>(rt, e) ? b[4 * rt + e] : T(0);
-}
-
-// sum over the 4 lane groups (the rows of one node)
-template <class T>
-__device__ __forceinline__ T sum_h(T v) {
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    return v;
-}
-
-template <class T>
-__device__ __forceinline__ T soc_apply_t(T v, bool is_t, T nf, T t) {
-    // SecondOrderCone.project (cones.py:113-132) for one coordinate of the block
-    if (nf <= t) return v;
-    if (nf <= -t) return T(0);
-    const T s = (nf + t) / T(2);
-    return is_t ? s : s * (v / nf);
-}
-template <class T>
-__device__ __forceinline__ T box_apply_t(T v, T lo, T hi, Ctl* ctl) {
-    // Rectangle._constrain (rectangle.py:50-59); a NaN raises ValueError on the host
-    if (lo <= v && v <= hi) return v;
-    if (v <= lo) return lo;
-    if (v >= hi) return hi;
-    atomicOr(&ctl->flags, 1);
-    return v;
-}
-
-// per-wave scratch of the kernel projection (raocp_cp3.hip KpScratch)
-template <class T>
-struct KpScratch {
-    T y[16][9];
-    T tau[16][4];
-    T s[16][4];
-};
-
-__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// (glbp / cglbp, MF, WL, mmt, ld_rows, ldz, st_rows, ld_rows_lds, sum_h, the cone and box
+// projections, KpScratch, dma_wait: raocp_tile.h)
 
 // ---- the operands of one leaf (a leaf tile's lane, or a leaf slot of a leaf-parent family)
 template <class T, int NX, int BXL>
@@ -442,7 +308,7 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
     bool stp_on = false;
     int stp_n = 0;
     auto stamp = [&]() {
-        if (stp_on && (threadIdx.x & 63) == 0 && stp_n < 16) p.stamps[stp_n++] = __builtin_amdgcn_s_memrealtime();
+        if (kDiag && stp_on && (threadIdx.x & 63) == 0 && stp_n < 16) p.stamps[stp_n++] = __builtin_amdgcn_s_memrealtime();
     };
     auto family = [&](auto leafp_tag, int i0, int iend, int split) {
         constexpr bool LEAFP = decltype(leafp_tag)::value;
@@ -734,7 +600,7 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
     const int split = tk.split;
     const int nTL = (tk.l1 - tk.l0 + 15) >> 4;  // leaf tiles (split), then the parent ranges' tiles
     // diagnostics: every wave's [first task start, last task end] at stamps[32 + 2 gw]
-    const unsigned long long w_t0 = p.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const unsigned long long w_t0 = kDiag && p.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
     for (int tt = hm ? (int)blockIdx.x : gw; tt < nTL + tk.t0[tk.nr]; tt += hm ? (int)gridDim.x : nwv) {
         if (hm && wv == 1) {
             // the helper: a leaf-parent tile's leaf children (phase 4 of the family), then the
@@ -769,14 +635,14 @@ __global__ void __launch_bounds__(256) k_cp4(Dev p, Ctl* __restrict__ ctl, Bufs 
             continue;
         }
         const int task = tt - nTL;
-        stp_on = p.stamps != nullptr && task == p.cp_dbg;  // (diagnostics: the stamped task)
+        stp_on = kDiag && p.stamps != nullptr && task == p.cp_dbg;  // (diagnostics: the stamped task)
         int r = 0;
         while (r + 1 < tk.nr && task >= tk.t0[r + 1]) ++r;
         const int i0 = tk.lo[r] + 16 * (task - tk.t0[r]), iend = tk.hi[r];
         if (tk.lo[r] >= tk.mL) family(std::true_type{}, i0, iend, split);
         else family(std::false_type{}, i0, iend, split);
     }
-    if (p.stamps && (threadIdx.x & 63) == 0 && gw < 2000) {
+    if (kDiag && p.stamps && (threadIdx.x & 63) == 0 && gw < 2000) {
         p.stamps[32 + 2 * gw] = w_t0;
         p.stamps[33 + 2 * gw] = __builtin_amdgcn_s_memrealtime();
     }

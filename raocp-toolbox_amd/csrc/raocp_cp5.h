@@ -1,0 +1,24 @@
+// raocp_cp5.h — host interface of k_cp5 (raocp_cp5.hip, its own translation unit): the fused
+// CP iteration of raocp_cp3.hip as TWO streaming launches with small register files, for the
+// large trees (configs 3, 4, 5): the leaf tiles, then the family tiles.
+#pragma once
+
+#include "raocp_common.h"
+
+namespace raocp {
+
+// the compiled (type, nx, nu, branching, box pattern) combinations; nbox_nl / nbox_l: the
+// distinct box tables of the nonleaf / leaf nodes (at most one each)
+bool cp5_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbox_l);
+// the two kernels as rocprofv3 names them, "leaf x1 + fam x1"
+const char* cp5_name(bool f32, int nx, int nu, int C);
+// grids of the two launches for n leaves in [l0, l1) and the family task list tk
+int cp5_leaf_grid(int l0, int l1);
+int cp5_fam_grid(const Cp3Tasks& tk);
+// the two launches on stream s: leaves [l0, l1) (residual partials in part[0, gl)), then the
+// families of tk (partials in part[gl, gl + gf)); img is k_cp3's weight image
+// ([sqrtQ | sqrtR | sqrtPf] fragments). hipGetLastError() after it is the caller's.
+void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, int l0, int l1, int gl,
+                const Cp3Tasks& tk, int gf, const double* img, hipStream_t s);
+
+}  // namespace raocp

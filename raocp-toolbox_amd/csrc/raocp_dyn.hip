@@ -406,7 +406,7 @@ __device__ __forceinline__ void zero_fill(PD dst, int count, int tid, int nthr) 
 // ---- per-stage path on padded global rows (any tree) ----------------------------------
 // gather: XQ[j] = x_j (padded KP), U[i] = u_i (padded NUP), XD[i] = [0 | 0 | 0]
 template <int NXc, int NUc>
-__global__ void __launch_bounds__(kBlock) k_dyn_gather(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+__global__ void __launch_bounds__(kBlock) k_dyn_gather(Dev p, Bufs bf, const Ctl* ctl, int zsel,
                                                         double* xq_, double* u_, double* xd_) {
     if (ctl && ctl->done) return;
     const Geo<NXc, NUc> g(p);
@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(kBlock) k_dyn_gather(Dev p, Bufs bf, const Ctl
 }
 
 template <int NXc, int NUc>
-__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_a(Dev p, const Ctl* __restrict__ ctl, const double* xq_,
+__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_a(Dev p, const Ctl* ctl, const double* xq_,
                                                          double* pb_, int cb, int ce, double sign) {
     if (ctl && ctl->done) return;
     const Geo<NXc, NUc> g(p);
@@ -430,7 +430,7 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_stage_a(Dev p, const Ctl* __r
 }
 
 template <int NXc, int NUc>
-__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_b(Dev p, const Ctl* __restrict__ ctl, double* xq_,
+__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_b(Dev p, const Ctl* ctl, double* xq_,
                                                          const double* u_, const double* pb_, double* xd_, double* d_,
                                                          int b, int e) {
     if (ctl && ctl->done) return;
@@ -463,7 +463,7 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_stage_b(Dev p, const Ctl* __r
 }
 
 template <int NXc, int NUc>
-__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_f(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+__global__ void __launch_bounds__(kDynBlock) k_dyn_stage_f(Dev p, Bufs bf, const Ctl* ctl, int zsel,
                                                          double* xd_, const double* x0_, int b, int e) {
     if (ctl && ctl->done) return;
     const Geo<NXc, NUc> g(p);
@@ -505,10 +505,10 @@ struct Prologue {
 
 // diagnostics: thread 0 records the 100 MHz clock in LDS; flushed at the end of the kernel
 __device__ __forceinline__ void tstamp(const Dev& p, Prologue& pl, int slot) {
-    if (p.stamps && threadIdx.x == 0 && slot < 64) pl.ts[slot] = __builtin_amdgcn_s_memrealtime();
+    if (kDiag && p.stamps && threadIdx.x == 0 && slot < 64) pl.ts[slot] = __builtin_amdgcn_s_memrealtime();
 }
 __device__ __forceinline__ void tflush(const Dev& p, const Prologue& pl, int n) {
-    if (p.stamps && threadIdx.x == 0 && blockIdx.x == 0)
+    if (kDiag && p.stamps && threadIdx.x == 0 && blockIdx.x == 0)
         for (int k = 0; k < n && k < 64; ++k) p.stamps[k] = pl.ts[k];
 }
 
@@ -647,7 +647,7 @@ struct TabSize {
 // FOLD (one-phase levels): W -> WT (pairs p0..p1), no P rows.
 // The boundary level (s1) holds the leaves' x (q = -x) or q of the next tier's roots.
 template <int NXc, int NUc, bool FOLD>
-__global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+__global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, const Ctl* ctl, int zsel,
                                                                 double* qbuf_, double* dbuf_, int s, int s1, int maxch,
                                                                 int c0, int c1, int p0, int p1,
                                                                 const Rec* __restrict__ sub_lv, TierArg ta, ChkArg ck) {
@@ -755,7 +755,7 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_back(Dev p, Bufs bf, c
 // ta.pl0[l + 1]), restaged before each level — a deep tier whose whole F does not fit LDS
 // reads its rows from LDS anyway, for one LDS round trip per level.
 template <int NXc, int NUc, int FM>
-__global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+__global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, const Ctl* ctl, int zsel,
                                                                const double* dbuf_, int s, int s1, int c0, int c1,
                                                                int p0, int p1, const Rec* __restrict__ sub_lv,
                                                                TierArg ta) {
@@ -861,7 +861,7 @@ __global__ void __launch_bounds__(kDynBlock) k_dyn_bottom_fwd(Dev p, Bufs bf, co
 //    P (maxch, PS) | NL (T) | CH (T + nb - 1)]
 // FOLD (one-phase backward levels): W -> WT (pairs 0..p1), no P rows.
 template <int NXc, int NUc, bool FL, bool FOLD>
-__global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+__global__ void __launch_bounds__(kDynBlock) k_dyn_top(Dev p, Bufs bf, const Ctl* ctl, int zsel,
                                                         const double* qbuf_, const double* x0_, int s, int maxch,
                                                         int c1, int p1, int T, int nb) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];

@@ -28,7 +28,7 @@ __device__ __forceinline__ int tile_node(const DynTile& t, const int* __restrict
 }
 
 template <class T, int RT, int KSM>
-__global__ void __launch_bounds__(256) k_d2_prod(Dev p, const Ctl* __restrict__ ctl, const DynTile* __restrict__ tiles,
+__global__ void __launch_bounds__(256) k_d2_prod(Dev p, const Ctl* ctl, const DynTile* __restrict__ tiles,
                                                  int ntiles, const int* __restrict__ idx, const double* __restrict__ W_,
                                                  const double* __restrict__ src_, int src_base, T sign,
                                                  double* __restrict__ pa_) {
@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256) k_d2_prod(Dev p, const Ctl* __restrict__ 
 }
 
 template <class T, int RT, int KSM>
-__global__ void __launch_bounds__(256) k_d2_node(Dev p, const Ctl* __restrict__ ctl, const DynTile* __restrict__ tiles,
+__global__ void __launch_bounds__(256) k_d2_node(Dev p, const Ctl* ctl, const DynTile* __restrict__ tiles,
                                                  int ntiles, const int* __restrict__ idx, const double* __restrict__ RG_,
                                                  const double* __restrict__ z_, const double* __restrict__ pa_,
                                                  double* __restrict__ q_, double* __restrict__ d_) {
@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) k_d2_node(Dev p, const Ctl* __restrict__ 
 
 // forward (U): u_i = K x_i + d_i ; (X): x_j = F [x_anc(j) ; d_anc(j)]
 template <class T, int RT, int KSM, bool XROWS>
-__global__ void __launch_bounds__(256) k_d2_fwd(Dev p, const Ctl* __restrict__ ctl, const DynTile* __restrict__ tiles,
+__global__ void __launch_bounds__(256) k_d2_fwd(Dev p, const Ctl* ctl, const DynTile* __restrict__ tiles,
                                                 int ntiles, const int* __restrict__ idx, const double* __restrict__ M_,
                                                 double* __restrict__ z_, const double* __restrict__ d_) {
     if (ctl && ctl->done) return;
@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) k_d2_fwd(Dev p, const Ctl* __restrict__ c
 }
 
 template <class T>
-__global__ void k_d2_x0(const Ctl* __restrict__ ctl, double* __restrict__ z_, int X0, const double* __restrict__ x0_,
+__global__ void k_d2_x0(const Ctl* ctl, double* __restrict__ z_, int X0, const double* __restrict__ x0_,
                         int nx) {
     if (ctl && ctl->done) return;
     if ((int)threadIdx.x < nx) ((T*)z_)[X0 + threadIdx.x] = ((const T*)x0_)[threadIdx.x];

@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(512) k_dy3_image(Dy3Stage st, int C, const dou
 }
 
 template <class T, int NX, int NU>
-__global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__ ctl, ChkArg ck, double* __restrict__ z_,
+__global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* ctl, ChkArg ck, double* __restrict__ z_,
                                                   double* __restrict__ q_, double* __restrict__ d_, Dy3Stage st, int C,
                                                   const double* __restrict__ img, int sp) {
     typedef typename MF<T>::v4 v4;
@@ -290,7 +290,7 @@ __global__ void __launch_bounds__(512) k_dy3_back(Dev p, const Ctl* __restrict__
 }
 
 template <class T, int NX, int NU>
-__global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* __restrict__ ctl, double* __restrict__ z_,
+__global__ void __launch_bounds__(512) k_dy3_fwd(Dev p, const Ctl* ctl, double* __restrict__ z_,
                                                  const double* __restrict__ d_, const double* __restrict__ x0_, Dy3Stage st,
                                                  int C, const double* __restrict__ img, int sp) {
     typedef typename MF<T>::v4 v4;
@@ -372,7 +372,7 @@ struct Dy3Top {
 // slot w % C (the slot order of the sp launches: bit-identical sums), the slot sums of
 // slots >= 1 through LDS to the tile's slot-0 wave, which finishes the tile (v, d, q)
 template <class T, int NX, int NU>
-__global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* __restrict__ ctl, double* __restrict__ z_,
+__global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* ctl, double* __restrict__ z_,
                                                       double* __restrict__ q_, double* __restrict__ d_, Dy3Top tp, int C,
                                                       const double* __restrict__ img0) {
     typedef typename MF<T>::v4 v4;
@@ -481,7 +481,7 @@ __global__ void __launch_bounds__(512) k_dy3_top_back(Dev p, const Ctl* __restri
 // forward, t = 0 .. ts - 1: the (tile, child slot) tasks of a stage over the waves (the sp
 // launches' task order), slot 0 also writing u
 template <class T, int NX, int NU>
-__global__ void __launch_bounds__(512) k_dy3_top_fwd(Dev p, const Ctl* __restrict__ ctl, double* __restrict__ z_,
+__global__ void __launch_bounds__(512) k_dy3_top_fwd(Dev p, const Ctl* ctl, double* __restrict__ z_,
                                                      const double* __restrict__ d_, const double* __restrict__ x0_,
                                                      Dy3Top tp, int C, const double* __restrict__ img0) {
     typedef typename MF<T>::v4 v4;

@@ -51,7 +51,7 @@ struct FuseArg {
 
 // diagnostics: thread 0 stamps the next slot of this workgroup's path (p.stamps != nullptr)
 __device__ __forceinline__ void fz_stamp(const Dev& p, Prologue& pl) {
-    if (p.stamps && threadIdx.x == 0) pl.ts[pl.nts++ & 63] = __builtin_amdgcn_s_memrealtime();
+    if (kDiag && p.stamps && threadIdx.x == 0) pl.ts[pl.nts++ & 63] = __builtin_amdgcn_s_memrealtime();
 }
 
 __device__ __forceinline__ unsigned ld_u32_sc1(const unsigned* p) {
@@ -432,7 +432,7 @@ __device__ __forceinline__ bool fz_wait_eq(const unsigned* f, unsigned v, const 
 }
 
 template <int NXc, int NUc>
-__global__ void __launch_bounds__(kFuseBlock) k_dyn_up(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+__global__ void __launch_bounds__(kFuseBlock) k_dyn_up(Dev p, Bufs bf, const Ctl* ctl, int zsel,
                                                        double* qbuf_, double* dbuf_, FuseArg fa) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_up(Dev p, Bufs bf, const Ctl
         fz_stamp(p, pl);
         fz_release_add(tt.cnt + b / tt.r);
         fz_stamp(p, pl);
-        if (p.stamps && tid == 0 && b == 0 && (k == 0 || k == D))  // diagnostics: tier 0 / deepest, subtree 0
+        if (kDiag && p.stamps && tid == 0 && b == 0 && (k == 0 || k == D))  // diagnostics: tier 0 / deepest, subtree 0
             for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
     } else {  // the top
         fz_top_stage<NXc, NUc, false>(p, z, fa, smem, pl, true);
@@ -479,7 +479,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_up(Dev p, Bufs bf, const Ctl
         if (work) fz_top_run<NXc, NUc, false>(p, z, qbuf_, nullptr, fa, smem, pl, (glbd*)dbuf_);
         fz_stamp(p, pl);
         fz_release_store(fa.epoch, e + 1u);
-        if (p.stamps && tid == 0)
+        if (kDiag && p.stamps && tid == 0)
             for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[q] = pl.ts[q];
     }
 }
@@ -551,7 +551,7 @@ __device__ void fz_xd_stage(const Dev& p, const double* dbuf_, const FuseTier& t
 }
 
 template <int NXc, int NUc, bool FL>
-__global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const Ctl* __restrict__ ctl, int zsel,
+__global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const Ctl* ctl, int zsel,
                                                          const double* dbuf_, const double* x0_, FuseArg fa) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Prologue pl;
@@ -571,7 +571,7 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const C
         if (!ctl_done(ctl)) fz_top_fwd<NXc, NUc, FL>(p, z, dbuf_, x0_, fa, smem, pl);
         fz_stamp(p, pl);
         fz_release_store(fa.t[0].flag, tag);
-        if (p.stamps && tid == 0)
+        if (kDiag && p.stamps && tid == 0)
             for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[q] = pl.ts[q];
         return;
     }
@@ -594,6 +594,6 @@ __global__ void __launch_bounds__(kFuseBlock) k_dyn_down(Dev p, Bufs bf, const C
     if (k < D) {
         fz_release_store(fa.t[k + 1].flag + b, tag);
     }
-    if (p.stamps && tid == 0 && b == 0)  // diagnostics: tier 0 / deepest, subtree 0
+    if (kDiag && p.stamps && tid == 0 && b == 0)  // diagnostics: tier 0 / deepest, subtree 0
         for (int q = 0; q < pl.nts && q < 64; ++q) p.stamps[(k == 0 ? 64 : 128) + q] = pl.ts[q];
 }

@@ -39,8 +39,9 @@ struct DrPlan {
     unsigned* sync;           // [0] epoch (the tag of the last projection), [1] error word
     long long timeout;        // per wait, 100 MHz ticks
     unsigned long long* stamps;  // diagnostics (nullptr = off): 32 slots per tier
-    int fault;                // diagnostics: bit 0 the deepest tier's subtree 0 never publishes;
-                              // timing only (wrong results): bit 2 no table DMAs, bit 3 no
+    int fault;                // error-path test: bit 0 the deepest tier's subtree 0 never publishes
+                              // (the wait times out, the call fails with RAOCP_ERR_STATE); timing
+                              // only, diagnostic builds (kDiag) only: bit 2 no table DMAs, bit 3 no
                               // write-out, bit 4 no level arithmetic, bit 5 no row DMAs
 };
 

@@ -109,7 +109,13 @@ struct Dma {
 };
 
 // every lane polls granules g = tid + i * blockDim (g < n) of src until each carries tag, and
-// puts their halves at dst[g]; false (error word set) on a timeout
+// puts their halves at dst[g]; false (error word set) on a timeout, or as soon as another
+// workgroup has set the error word (a missing hand-off then costs one timeout, not one per tier)
+//
+// k_dr assumes its grid has the device's CUs to itself: the host checks that the grid is
+// resident (occupancy x CUs), which another kernel running beside it on the same device (a
+// second context's stream) can break; a workgroup that is never scheduled turns into the
+// bounded wait's RAOCP_ERR_STATE, not a hang
 //
 // The wait itself is one wave's: its lanes poll the last granule of each of the rows rows
 // (sleeping between rounds) while the other waves sit at the barrier; then every lane reads
@@ -125,7 +131,8 @@ __device__ __forceinline__ bool poll_gran(const unsigned long long* src, int n, 
             for (;;) {
                 const bool ok = r >= rows || (unsigned)(ld_gran(src + (size_t)r * G + G - 1) >> 32) == tag;
                 if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+                // another workgroup's timeout (the error word): this wait cannot complete either
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout || ld_u32(sync + 1) != 0u) {
                     bad = true;
                     break;
                 }
@@ -154,7 +161,7 @@ __device__ __forceinline__ bool poll_gran(const unsigned long long* src, int n, 
             }
         }
         if (all || bad) break;
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout || ld_u32(sync + 1) != 0u) {
             bad = true;
             break;
         }
@@ -180,7 +187,7 @@ struct Stamps {
     int n;
 };
 __device__ __forceinline__ void stamp(const DrPlan& pl, Stamps& s) {
-    if (pl.stamps && threadIdx.x == 0 && s.n < 30) {
+    if (kDiag && pl.stamps && threadIdx.x == 0 && s.n < 30) {
         if (s.n == 0) s.c0 = __builtin_amdgcn_s_memtime();
         s.ts[s.n++] = __builtin_amdgcn_s_memrealtime();
     }
@@ -188,7 +195,7 @@ __device__ __forceinline__ void stamp(const DrPlan& pl, Stamps& s) {
 // slots [32 k, 32 k + 30): the stamps; 32 k + 30: the end; 32 k + 31: cycles from the first
 // stamp to the end
 __device__ __forceinline__ void stamp_flush(const DrPlan& pl, const Stamps& s, int k, int o) {
-    if (pl.stamps && threadIdx.x == 0 && o == 0 && k < 4) {
+    if (kDiag && pl.stamps && threadIdx.x == 0 && o == 0 && k < 4) {
         const unsigned long long c1 = __builtin_amdgcn_s_memtime(), t1 = __builtin_amdgcn_s_memrealtime();
         for (int q = 0; q < 30; ++q) pl.stamps[32 * k + q] = q < s.n ? s.ts[q] : 0ull;
         pl.stamps[32 * k + 30] = t1;
@@ -368,7 +375,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     static_for<0, L + 1>([&](auto lc) { gl[lc.value] = pl.sbase[s0 + lc.value] + o * cpow(C, lc.value); });
     // ---- 1. rows, then the backward tables
     Dma dm;
-    if (!(pl.fault & 32)) {
+    if (!(kDiag && (pl.fault & 32))) {
         static_for<0, L>([&](auto lc) {
             constexpr int l = lc.value, cnt = cpow(C, l), off = (cnt - 1) / (C - 1);
             dm.rows(XD + off * SXD, SXD, (const double*)z + pl.X0 + (size_t)gl[l] * NX, NX, cnt, pl.zpage);
@@ -377,7 +384,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
         if (deepest) dm.range(XL, (const double*)z + pl.X0 + (size_t)gl[L] * NX, NB * NX);
     }
     if (top) dm.range(X0B, pl.x0, NX);
-    if (!(pl.fault & 4))
+    if (!(kDiag && (pl.fault & 4)))
         static_for<0, L>([&](auto ic) {
             constexpr int l = L - 1 - ic.value;
             TB::issue(SL + l * SLOT, pl.bimg + (size_t)(s0 + l) * TBN);
@@ -400,9 +407,9 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
         if (i > 0) {
             lds_sync();
             stamp(pl, stp);
-            if (top && !(pl.fault & 4)) TF::issue(SL + (l + 1) * SLOT, pl.fimg + (size_t)(s0 + i - 1) * TFN);
+            if (top && !(kDiag && (pl.fault & 4))) TF::issue(SL + (l + 1) * SLOT, pl.fimg + (size_t)(s0 + i - 1) * TFN);
         }
-        if (work && !(pl.fault & 16)) {
+        if (work && !(kDiag && (pl.fault & 16))) {
             const bool last = l == L - 1;
             back_level<NX, NU, C, BS, UMAX, cnt>(SL + l * SLOT, XD + off * SXD, last ? XL : XD + (off + cnt) * SXD,
                                            last ? NX : SXD, U + off * NU, (deepest && last) ? -1.0 : 1.0);
@@ -412,10 +419,10 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     stamp(pl, stp);
     // ---- 4./5. the root's q row up, its x row down (below the top the forward tables load
     // during that wait; the top issued them as its backward sweep freed the slots)
-    if (top && !(pl.fault & 4)) TF::issue(SL, pl.fimg + (size_t)(s0 + L - 1) * TFN);
+    if (top && !(kDiag && (pl.fault & 4))) TF::issue(SL, pl.fimg + (size_t)(s0 + L - 1) * TFN);
     if (!top) {
         if (!((pl.fault & 1) && deepest && o == 0)) publish(pl.gq + (size_t)(tt.w0 + o) * G, G, tag, (const ldsu*)XD);
-        if (!(pl.fault & 4))
+        if (!(kDiag && (pl.fault & 4)))
             static_for<0, L>([&](auto fc) {
                 constexpr int f = fc.value;
                 TF::issue(SL + (L - 1 - f) * SLOT, pl.fimg + (size_t)(s0 + f) * TFN);
@@ -434,7 +441,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
         wait_vm_c<(L - 1 - f) * TF::IPW>();
         lds_sync();
         stamp(pl, stp);
-        if (work && !(pl.fault & 16)) {
+        if (work && !(kDiag && (pl.fault & 16))) {
             const bool last = f == L - 1;
             fwd_level<NX, NU, C, BS, UMAX, cnt>(SL + (L - 1 - f) * SLOT, XD + off * SXD, last ? XL : XD + (off + cnt) * SXD,
                                           last ? NX : SXD, U + off * NU);
@@ -444,7 +451,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     stamp(pl, stp);
     // ---- 7. the boundary x rows to the child subtrees, then x and u to the iterate
     if (!deepest) publish(pl.gx + (size_t)(pl.t[k + 1].w0 + o * NB) * G, NB * G, tag, (const ldsu*)XL);
-    if (work && !(pl.fault & 8)) {
+    if (work && !(kDiag && (pl.fault & 8))) {
         static_for<0, L + 1>([&](auto lc) {
             constexpr int l = lc.value, cnt = cpow(C, l), off = (cnt - 1) / (C - 1);
             if (l == 0 && !top) return;  // the parent writes this subtree's root row
@@ -473,7 +480,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
 // 128 / 256 VGPRs and the scheduler keeps a level's LDS reads in flight together)
 template <int NX, int NU, int C, int BS, int LMAX>
 __global__ void __launch_bounds__(BS) __attribute__((amdgpu_waves_per_eu(LMAX <= 4 ? 4 : 2, LMAX <= 4 ? 4 : 2)))
-k_dr(DrPlan pl, Bufs bf, int zsel, const Ctl* __restrict__ ctl, ChkArg ck) {
+k_dr(DrPlan pl, Bufs bf, int zsel, const Ctl* ctl, ChkArg ck) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Stamps stp;
     __shared__ int s_ok;

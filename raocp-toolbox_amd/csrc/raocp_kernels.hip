@@ -21,7 +21,7 @@ constexpr int kBlock = 256;
 
 // diagnostic timestamp (100 MHz constant clock), thread 0 only, when enabled
 __device__ __forceinline__ void stamp(const Dev& p, int slot) {
-    if (p.stamps && threadIdx.x == 0 && blockIdx.x == 0) p.stamps[slot] = __builtin_amdgcn_s_memrealtime();
+    if (kDiag && p.stamps && threadIdx.x == 0 && blockIdx.x == 0) p.stamps[slot] = __builtin_amdgcn_s_memrealtime();
 }
 
 

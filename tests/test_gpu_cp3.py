@@ -69,9 +69,10 @@ def test_cp3_matches_two_kernel_path_and_oracle(cfg):
     tree, prob = build_problem(r)
     fused = core.Cache(prob)
     two = _with_env({"RAOCP_CP3": "0"}, lambda: core.Cache(prob))
-    # the fused iteration: k_cp4 (tile-start loads, config 2) or k_cp3
-    assert fused.native.kernel_info(10).startswith(("k_cp3<double", "k_cp4<double"))
-    assert not two.native.kernel_info(10).startswith(("k_cp3", "k_cp4"))
+    # the fused iteration: k_cp4 (tile-start loads, config 2), k_cp5 (leaf + family launches,
+    # configs 3 / 4 and C = 4 at 20 / 8) or k_cp3
+    assert fused.native.kernel_info(10).startswith(("k_cp3<double", "k_cp4<double", "k_cp5_leaf<double"))
+    assert not two.native.kernel_info(10).startswith(("k_cp3", "k_cp4", "k_cp5"))
     alpha = 0.999 / fused.native.step_size()
     K = 12 if cfg == "c4" else 20
     out = []
@@ -115,8 +116,8 @@ def test_cp3_split_matches_fused(cfg):
     tiles: the same arithmetic per entry, so the runs agree to rounding (1e-10)."""
     r = _recipe(cfg)
     tree, prob = build_problem(r)
-    a = _with_env({"RAOCP_CP3_SPLIT": "1"}, lambda: core.Cache(prob))
-    b = _with_env({"RAOCP_CP3_SPLIT": "0"}, lambda: core.Cache(prob))
+    a = _with_env({"RAOCP_CP3_SPLIT": "1", "RAOCP_CP5": "0"}, lambda: core.Cache(prob))
+    b = _with_env({"RAOCP_CP3_SPLIT": "0", "RAOCP_CP5": "0"}, lambda: core.Cache(prob))
     alpha = 0.999 / a.native.step_size()
     K = 10 if cfg == "c4" else 20
     out = []
@@ -128,14 +129,15 @@ def test_cp3_split_matches_fused(cfg):
     assert rel_err(z1, z2) <= 1e-11 and rel_err(y1, y2) <= 1e-11
 
 
-@pytest.mark.parametrize("cfg", ["c2", "c4", "c5"])
+@pytest.mark.parametrize("cfg", ["c2", "c4", "c5", "c5-cp3"])
 def test_cp3_fp32_drift_vs_fp64(cfg):
-    """30 fp32 CP iterations (k_cp3<float, ...>) against the fp64 run of the same problem and
-    step size (fp64: the k_cp3 / k_cpd2 + k_cpp2 path pinned to the oracle above)."""
-    r = recipe_config(int(cfg[1:]))
+    """30 fp32 CP iterations (k_cp3<float, ...>; config 5: k_cp5<float> by default, k_cp3 with
+    RAOCP_CP5=0) against the fp64 run of the same problem and step size (fp64: the k_cp3 /
+    k_cpd2 + k_cpp2 path pinned to the oracle above)."""
+    r = recipe_config(int(cfg[1]))
     tree, prob = build_problem(r)
-    c32 = core.Cache(prob, dtype="float32")
-    assert c32.native.kernel_info(10).startswith("k_cp3<float")
+    c32 = _with_env({"RAOCP_CP5": "0"} if cfg.endswith("cp3") else {}, lambda: core.Cache(prob, dtype="float32"))
+    assert c32.native.kernel_info(10).startswith("k_cp5_leaf<float" if cfg == "c5" else "k_cp3<float")
     c64 = core.Cache(prob)
     alpha = 0.999 / c64.native.step_size()
     K = 29

@@ -58,8 +58,8 @@ def cp_kernels(mode):
     fused streaming k_cp3 on uniform trees of the benchmark sizes, else scalar below ~4k node
     tiles and MFMA above), the two-launch MFMA kernels (raocp_cp2.hip) or the scalar ones
     (raocp_cp.hip)."""
-    with _env("RAOCP_CP_V1", {"auto": None, "mfma": "0", "scalar": "1"}[mode]), \
-            _env("RAOCP_CP3", None if mode == "auto" else "0"):
+    with _env("RAOCP_CP_V1", {"auto": None, "cp3": None, "mfma": "0", "scalar": "1"}[mode]), \
+            _env("RAOCP_CP3", None if mode in ("auto", "cp3") else "0"), _env("RAOCP_CP5", "0" if mode == "cp3" else None):
         yield
 
 
@@ -361,7 +361,7 @@ def test_projections_full_size_vs_oracle_and_idempotent(cfg, dyn):
     assert rel_err(nat.get_primal(), z2) <= 1e-12
 
 
-@pytest.mark.parametrize("cfg,cpk", [(3, "auto"), (4, "auto"), (3, "scalar"), ("4-modes", "auto")])
+@pytest.mark.parametrize("cfg,cpk", [(3, "auto"), (4, "auto"), (4, "cp3"), (3, "scalar"), ("4-modes", "auto")])
 def test_large_cp_trace_vs_oracle(cfg, cpk):
     """The whole CP loop (solver.py:124-161) at the HBM-sized configs (SURVEY.md 8(d)
     config 3: Markov 4 modes, 87,381 nodes, nx = 20; config 4: branching 3, 88,573 nodes,

@@ -40,9 +40,10 @@ def _kern_cache(prob, kern, dtype=None):
     """A context on the fused CP kernel k_cp3 ("fused", the default) or the two-launch
     k_cpd* / k_cpp* ("two", RAOCP_CP3=0)."""
     # the dynamics a shard runs (the tiered sweep; fp32 / config 4: dyn3) and the CP kernel it
-    # runs (k_cp3: a shard's task list; the unsharded default at config 2 is k_cp4, the same
-    # arithmetic with a different FMA contraction, test_gpu_cp4.py)
-    env = {"RAOCP_DR": "0", "RAOCP_CP4": "0"}
+    # runs (k_cp3: a shard's task list; the unsharded defaults at config 2 / configs 4, 5 are
+    # k_cp4 / k_cp5, the same arithmetic with a different FMA contraction, test_gpu_cp4.py,
+    # test_gpu_cp5.py)
+    env = {"RAOCP_DR": "0", "RAOCP_CP4": "0", "RAOCP_CP5": "0"}
     if kern == "two":
         env["RAOCP_CP3"] = "0"
     old = {k: os.environ.get(k) for k in env}
@@ -161,7 +162,7 @@ def test_rccl_transport_single_rank():
 
 
 @pytest.mark.parametrize("kern", ["fused", "two"])
-@pytest.mark.parametrize("R", [2, 4])
+@pytest.mark.parametrize("R", [2, 4, 8])
 def test_fp32_sharded_config5_matches_unsharded(R, kern):
     """BASELINE configs[4] ("fp32, 8 x MI355X"): one config-5 tree in fp32 split across R
     shards. The per-stage streaming sweep (raocp_dyn3.hip) runs the owned parents of every

@@ -1,9 +1,11 @@
-# Round-4 GPU runner (one script for every GPU call of the round):
-#   gpurun -- 'bash tools/gpu_r04.sh <tag> <step> [<step> ...]'
+# Round-5 GPU runner (one script for every GPU call of the round):
+#   gpurun -- 'bash tools/gpu_r05.sh <tag> <step> [<step> ...]'
 # Steps run in order, each under its own time limit, output under gpurun_out/<tag>/; the
 # first failing step ends the call (no GPU step runs after a failure).
 #   dynr        tests/test_gpu_dynr.py (the regular-tree sweep)
 #   cp4         tests/test_gpu_cp4.py (k_cp4 against k_cp3 and the oracle)
+#   cp5         tests/test_gpu_cp5.py (k_cp5 against k_cp3 and the oracle)
+#   cptests     the CP-kernel test files (cp3, cp4, cp5, fp32)
 #   dyntests    the dynamics test files (dynr, dyn_split, dyn3, variants)
 #   tests       the whole -m gpu suite
 #   smoke       __graft_entry__.smoke()
@@ -17,6 +19,10 @@
 #   prof        rocprofv3 --kernel-trace --stats of bench.py (eager launches)
 #   pmc         FETCH_SIZE / WRITE_SIZE passes of the same bench command
 #   asan        the host-ASan ABI driver on the GPU
+#   sqpmc       SQ counters (wave cycles split into waiting / issue-stalled / issuing, MFMA busy)
+#               of 20 eager CP iterations at configs $KPROF_CFGS, one rocprofv3 --pmc pass each
+#   kprof       rocprofv3 --kernel-trace --stats of 20 eager CP iterations at configs $KPROF_CFGS
+#               (default "4 5"; tools/prof_cp.py), the kernel statistics of each
 export TMPDIR=/tmp
 set -o pipefail
 tag=$1
@@ -33,6 +39,10 @@ for step in "$@"; do
           tail -3 $out/pytest_dynr.log ;;
     cp4) timeout -k 10 500 $PYT tests/test_gpu_cp4.py > $out/pytest_cp4.log 2>&1 || fail $step $out/pytest_cp4.log
           tail -3 $out/pytest_cp4.log ;;
+    cp5) timeout -k 10 600 $PYT tests/test_gpu_cp5.py > $out/pytest_cp5.log 2>&1 || fail $step $out/pytest_cp5.log
+          tail -3 $out/pytest_cp5.log ;;
+    cptests) timeout -k 10 900 $PYT tests/test_gpu_cp3.py tests/test_gpu_cp4.py tests/test_gpu_cp5.py tests/test_gpu_fp32.py > $out/pytest_cp.log 2>&1 || fail $step $out/pytest_cp.log
+          tail -3 $out/pytest_cp.log ;;
     dyntests) timeout -k 10 900 $PYT tests/test_gpu_dynr.py tests/test_gpu_dyn_split.py tests/test_gpu_dyn3.py tests/test_gpu_variants.py > $out/pytest_dyn.log 2>&1 || fail $step $out/pytest_dyn.log
           tail -3 $out/pytest_dyn.log ;;
     tests) timeout -k 10 1100 $PYT tests > $out/pytest_gpu.log 2>&1 || fail $step $out/pytest_gpu.log
@@ -43,7 +53,7 @@ for step in "$@"; do
           cat $out/dyn_time.log ;;
     stamps) timeout -k 10 200 python -u tools/dr_stamps.py 2 6 > $out/stamps_c2.log 2>&1 || fail $step $out/stamps_c2.log
           cat $out/stamps_c2.log ;;
-    cp) timeout -k 10 500 python -u tools/cp3_time.py ${CP_ARGS:-} > $out/cp3_time.log 2>&1 || fail $step $out/cp3_time.log
+    cp) timeout -k 10 600 python -u tools/cp3_time.py ${CP_ARGS:-} > $out/cp3_time.log 2>&1 || fail $step $out/cp3_time.log
           cat $out/cp3_time.log ;;
     lsweep) for a in "2 float64 1" "4 float64 3" "5 float32 2"; do
               timeout -k 10 200 python -u tools/l_sweep.py $a >> $out/l_sweep.log 2>&1 || fail $step $out/l_sweep.log
@@ -63,6 +73,14 @@ for step in "$@"; do
          done ;;
     asan) LSAN_OPTIONS=suppressions=tests/asan/lsan.supp timeout -k 10 120 ./build/asan_abi gpu > $out/asan_gpu.log 2>&1 || fail $step $out/asan_gpu.log
           tail -2 $out/asan_gpu.log ;;
+    kprof) for cfg in ${KPROF_CFGS:-4 5}; do
+             RAOCP_EAGER=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/kprof$cfg -o kp --output-format csv -- python3 tools/prof_cp.py $cfg 20 > $out/kprof$cfg.log 2>&1 || fail $step $out/kprof$cfg.log
+             find $out/kprof$cfg -name "*kernel_stats.csv" -exec cp {} $out/kprof${cfg}_stats.csv \; ; echo "config $cfg"; cut -d, -f1-4 $out/kprof${cfg}_stats.csv | head -12
+           done ;;
+    sqpmc) for cfg in ${KPROF_CFGS:-4 5}; do
+             RAOCP_EAGER=1 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES -d $out/sq$cfg -o sq --output-format csv -- python3 tools/prof_cp.py $cfg 20 > $out/sq$cfg.log 2>&1 || fail $step $out/sq$cfg.log
+             python3 tools/sq_summary.py $out/sq$cfg > $out/sq${cfg}_summary.txt 2>&1; head -40 $out/sq${cfg}_summary.txt
+           done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
