@@ -370,7 +370,7 @@ def iteration_kernels(nat, cache, w, reps, dev_ms_per_step):
     The roofline names the part with the larger device time per iteration."""
     kb = kernel_bytes(cache, w)
     name_cp, name_dyn = nat.kernel_info(10), nat.kernel_info(9)
-    fused = name_cp.startswith(("k_cp3", "k_cp4"))
+    fused = name_cp.startswith(("k_cp3", "k_cp4", "k_cp5", "k_cp6"))
     t_cp = 1e3 * nat.op_bench(10, reps)
     t_dyn = 1e3 * nat.op_bench(9, max(1, reps // 4))
     kernels = {"cp": dict(_rate(kb["cp_fused" if fused else "cp_two"], t_cp), kernel=name_cp, in_cp_iteration=True),

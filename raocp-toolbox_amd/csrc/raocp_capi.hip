@@ -67,7 +67,10 @@ struct raocp_ctx {
                                  // task per wave at four waves per workgroup 18.5 vs 16.7 us at one)
     bool cp5 = false;            // ... as a leaf launch and a family launch (raocp_cp5.hip: configs 3, 4, 5;
                                  // RAOCP_CP5=0: off)
-    raocp::Cp3Tasks cp5_tk{};    // k_cp5_fam's task list (every parent, leaf parents first)
+    bool cp6 = false;            // ... as one family tile per workgroup of 2 C waves (raocp_cp5.hip k_cp6: config
+                                 // 2; RAOCP_CP6=0: k_cp4)
+    int cp6_grid = 0;
+    raocp::Cp3Tasks cp5_tk{};    // k_cp5_fam's / k_cp6's task list (every parent, leaf parents first)
     int cp5_gl = 0, cp5_gf = 0;  // grids of the two launches
     int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
@@ -1089,6 +1092,10 @@ int cp3_image(raocp_ctx* c) {
     return cp3_imaget<double, 32, 12>(c);
 }
 void launch_cp3(raocp_ctx* c, int part = 0) {
+    if (c->cp6 && c->sh_S == 0) {
+        raocp::cp6_launch(c->dev, c->ctl, c->bufs, c->redpart, c->box_mode, c->cp5_tk, c->cp6_grid, c->cp3img, c->stream);
+        return;
+    }
     if (c->cp5 && c->sh_S == 0) {
         raocp::cp5_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->m, c->n, c->cp5_gl, c->cp5_tk,
                           c->cp5_gf, c->cp3img, c->stream);
@@ -1339,6 +1346,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             return s;
         }
         case 10:
+            if (c->cp6 && c->sh_S == 0) return raocp::cp6_name();
             if (c->cp5 && c->sh_S == 0) return raocp::cp5_name(c->f32, c->nx, c->nu, c->unif_C);
             if (c->cp4 && c->sh_S == 0) return raocp::cp4_name(c->f32, c->nx, c->nu);
             if (c->cp3) return "k_cp3<" + T + ", " + nn + (c->sh_S > 0 ? ", true> x2" : ", false>");
@@ -2723,7 +2731,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             }
             c->cp_rows = c->cp3_grid;
             if ((rc = cp3_image(c))) return bail(rc);
-            c->cp4 = raocp::cp4_supported(c->f32, nx, nu, c->unif_C, c->box_mode);
+            c->cp6 = raocp::cp6_supported(c->f32, nx, nu, c->unif_C, c->box_mode, c->dev.nBnl, c->dev.nBl);
+            if (const char* e = getenv("RAOCP_CP6")) c->cp6 = c->cp6 && atoi(e) != 0;
+            c->cp4 = !c->cp6 && raocp::cp4_supported(c->f32, nx, nu, c->unif_C, c->box_mode);
             if (const char* e = getenv("RAOCP_CP4")) c->cp4 = c->cp4 && atoi(e) != 0;
             if (c->cp4) {  // k_cp4: cp4_wpb waves per workgroup, the same waves over more CUs
                 if (const char* e = getenv("RAOCP_CP4_HELPER")) c->cp4_wpb = atoi(e) ? 2 : 1;
@@ -2739,8 +2749,21 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             }
             // k_cp5: the leaf tiles and the family tiles as two launches with small register
             // files (configs 3, 4, 5; k_cp4 keeps config 2)
-            c->cp5 = !c->cp4 && raocp::cp5_supported(c->f32, nx, nu, c->unif_C, c->box_mode, c->dev.nBnl, c->dev.nBl);
+            c->cp5 = !c->cp4 && !c->cp6 && raocp::cp5_supported(c->f32, nx, nu, c->unif_C, c->box_mode, c->dev.nBnl, c->dev.nBl);
             if (const char* e = getenv("RAOCP_CP5")) c->cp5 = c->cp5 && atoi(e) != 0;
+            if (c->cp6) {
+                if (cp3_tasks(c->cp5_tk, {{c->cp3_mL, m}, {0, c->cp3_mL}}, 0, 0, 1, c->cp3_mL) < 0)
+                    return bail(fail(RAOCP_ERR_ARG, "k_cp6 task list exceeds its parent-range slots"));
+                c->cp6_grid = raocp::cp6_grid(c->cp5_tk);
+                if (const char* e = getenv("RAOCP_CP6_GRID")) c->cp6_grid = std::max(1, atoi(e));
+                c->cp_rows = c->cp6_grid;
+                if (c->cp_rows > c->red_rows) {
+                    c->red_rows = c->cp_rows;
+                    if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
+                    if (hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)) != hipSuccess)
+                        return bail(fail(RAOCP_ERR_HIP, "memset"));
+                }
+            }
             if (c->cp5) {
                 if (cp3_tasks(c->cp5_tk, {{c->cp3_mL, m}, {0, c->cp3_mL}}, 0, 0, 1, c->cp3_mL) < 0)
                     return bail(fail(RAOCP_ERR_ARG, "k_cp5 task list exceeds its parent-range slots"));

@@ -21,4 +21,13 @@ int cp5_fam_grid(const Cp3Tasks& tk);
 void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, int l0, int l1, int gl,
                 const Cp3Tasks& tk, int gf, const double* img, hipStream_t s);
 
+// k_cp6 (raocp_cp5.hip): the small trees' fused CP iteration, one family tile per workgroup of
+// 2 C waves splitting the tile's roles (config 2); the task list as k_cp5_fam's, the grid one
+// workgroup per tile, the residual partials one row per workgroup
+bool cp6_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbox_l);
+const char* cp6_name();
+int cp6_grid(const Cp3Tasks& tk);
+void cp6_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, const Cp3Tasks& tk, int grid, const double* img,
+                hipStream_t s);
+
 }  // namespace raocp

@@ -69,10 +69,11 @@ def test_cp3_matches_two_kernel_path_and_oracle(cfg):
     tree, prob = build_problem(r)
     fused = core.Cache(prob)
     two = _with_env({"RAOCP_CP3": "0"}, lambda: core.Cache(prob))
-    # the fused iteration: k_cp4 (tile-start loads, config 2), k_cp5 (leaf + family launches,
-    # configs 3 / 4 and C = 4 at 20 / 8) or k_cp3
-    assert fused.native.kernel_info(10).startswith(("k_cp3<double", "k_cp4<double", "k_cp5_leaf<double"))
-    assert not two.native.kernel_info(10).startswith(("k_cp3", "k_cp4", "k_cp5"))
+    # the fused iteration: k_cp6 (a workgroup per family tile, config 2 boxed / unboxed), k_cp4
+    # (tile-start loads, C = 2 at 20 / 8 otherwise), k_cp5 (leaf + family launches, configs 3 / 4
+    # and C = 4 at 20 / 8) or k_cp3
+    assert fused.native.kernel_info(10).startswith(("k_cp3<double", "k_cp4<double", "k_cp5_leaf<double", "k_cp6<double"))
+    assert not two.native.kernel_info(10).startswith(("k_cp3", "k_cp4", "k_cp5", "k_cp6"))
     alpha = 0.999 / fused.native.step_size()
     K = 12 if cfg == "c4" else 20
     out = []
@@ -116,8 +117,8 @@ def test_cp3_split_matches_fused(cfg):
     tiles: the same arithmetic per entry, so the runs agree to rounding (1e-10)."""
     r = _recipe(cfg)
     tree, prob = build_problem(r)
-    a = _with_env({"RAOCP_CP3_SPLIT": "1", "RAOCP_CP5": "0"}, lambda: core.Cache(prob))
-    b = _with_env({"RAOCP_CP3_SPLIT": "0", "RAOCP_CP5": "0"}, lambda: core.Cache(prob))
+    a = _with_env({"RAOCP_CP3_SPLIT": "1", "RAOCP_CP5": "0", "RAOCP_CP6": "0"}, lambda: core.Cache(prob))
+    b = _with_env({"RAOCP_CP3_SPLIT": "0", "RAOCP_CP5": "0", "RAOCP_CP6": "0"}, lambda: core.Cache(prob))
     alpha = 0.999 / a.native.step_size()
     K = 10 if cfg == "c4" else 20
     out = []

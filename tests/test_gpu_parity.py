@@ -59,7 +59,8 @@ def cp_kernels(mode):
     tiles and MFMA above), the two-launch MFMA kernels (raocp_cp2.hip) or the scalar ones
     (raocp_cp.hip)."""
     with _env("RAOCP_CP_V1", {"auto": None, "cp3": None, "mfma": "0", "scalar": "1"}[mode]), \
-            _env("RAOCP_CP3", None if mode in ("auto", "cp3") else "0"), _env("RAOCP_CP5", "0" if mode == "cp3" else None):
+            _env("RAOCP_CP3", None if mode in ("auto", "cp3") else "0"), _env("RAOCP_CP5", "0" if mode == "cp3" else None), \
+            _env("RAOCP_CP6", "0" if mode == "cp3" else None):
         yield
 
 

@@ -41,9 +41,9 @@ def _kern_cache(prob, kern, dtype=None):
     k_cpd* / k_cpp* ("two", RAOCP_CP3=0)."""
     # the dynamics a shard runs (the tiered sweep; fp32 / config 4: dyn3) and the CP kernel it
     # runs (k_cp3: a shard's task list; the unsharded defaults at config 2 / configs 4, 5 are
-    # k_cp4 / k_cp5, the same arithmetic with a different FMA contraction, test_gpu_cp4.py,
+    # k_cp6 / k_cp5, the same arithmetic with a different FMA contraction, test_gpu_cp6.py,
     # test_gpu_cp5.py)
-    env = {"RAOCP_DR": "0", "RAOCP_CP4": "0", "RAOCP_CP5": "0"}
+    env = {"RAOCP_DR": "0", "RAOCP_CP4": "0", "RAOCP_CP5": "0", "RAOCP_CP6": "0"}
     if kern == "two":
         env["RAOCP_CP3"] = "0"
     old = {k: os.environ.get(k) for k in env}
