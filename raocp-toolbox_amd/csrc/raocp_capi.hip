@@ -7,6 +7,7 @@
 #include "raocp_dynr.h"
 #include "raocp_cp4.h"
 #include "raocp_cp5.h"
+#include "raocp_dyn4.h"
 #include "../../include/raocp_hip.h"
 
 #include <dlfcn.h>
@@ -67,6 +68,8 @@ struct raocp_ctx {
                                  // task per wave at four waves per workgroup 18.5 vs 16.7 us at one)
     bool cp5 = false;            // ... as a leaf launch and a family launch (raocp_cp5.hip: configs 3, 4, 5;
                                  // RAOCP_CP5=0: off)
+    bool cp5_fams = false;       // the family launch as k_cp5_fams (a workgroup of C waves per tile), else
+                                 // k_cp5_fam (a wave per tile; RAOCP_CP5_FAMS)
     bool cp6 = false;            // ... as one family tile per workgroup of 2 C waves (raocp_cp5.hip k_cp6: config
                                  // 2; RAOCP_CP6=0: k_cp4)
     int cp6_grid = 0;
@@ -93,6 +96,11 @@ struct raocp_ctx {
     double *d3img_b = nullptr, *d3img_f = nullptr;  // per-stage table images (k_dy3_image)
     std::vector<raocp::Dy3Stage> d3own;  // a shard's stages (owned parent ranges below its cut)
     int d3ts = 0;  // the top stages k_dy3_top_back / k_dy3_top_fwd run in one workgroup (0: none)
+    size_t d3nb = 0, d3nf = 0;  // doubles per stage image (backward, forward)
+    bool dy4 = false;           // the same sweep in ONE launch of dataflow tile tasks (raocp_dyn4.hip;
+                                // opt-in RAOCP_DY4=1)
+    raocp::Dy4Plan dy4p{};
+    size_t dy4_lds = 0;
     int wsz = 8;                 // bytes per scalar of the iterate
     hipStream_t stream = nullptr;
     Dev dev{};
@@ -530,6 +538,8 @@ int dyn3_imagest(raocp_ctx* c) {
     typedef raocp::Dy3Lds<T, NX, NU> L;
     const int C = c->unif_branch, N = (int)c->d3st.size();
     const size_t nb = (size_t)L::back_n(C) * sizeof(T) / 8, nf = (size_t)L::fwd_n(C) * sizeof(T) / 8;
+    c->d3nb = nb;
+    c->d3nf = nf;
     int rc;
     if ((rc = c->alloc(&c->d3img_b, std::max<size_t>(1, N * nb))) || (rc = c->alloc(&c->d3img_f, std::max<size_t>(1, N * nf))))
         return rc;
@@ -706,6 +716,13 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
                          ck ? *ck : raocp::ChkArg{nullptr, nullptr, nullptr, 0, 0}, c->stream);
         return;
     }
+    if (c->dy4 && c->sh_S == 0 && part == 0) {  // the one-launch dataflow sweep (raocp_dyn4.hip)
+        double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
+        raocp::dy4_launch(c->dy4p, c->f32, c->nx, c->nu, c->dev, ctl,
+                          ck ? *ck : raocp::ChkArg{nullptr, nullptr, nullptr, 0, 0}, z, c->Q2, c->Dd2, c->x0,
+                          c->dy4_lds, c->stream);
+        return;
+    }
     if (c->dyn3) {
         double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
         launch_dyn3(c, z, ctl, ck, part);
@@ -723,6 +740,18 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
 // the fused sweep's error word (a hand-off wait timed out, raocp_dynf.hip): checked after
 // every synchronised run that may have launched it; the context is unusable afterwards
 int fuse_err(raocp_ctx* c) {
+    if (c->dy4 && c->sh_S == 0) {
+        unsigned e = 0;
+        HIPCHK(hipMemcpy(&e, c->dy4p.sync + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+        if (e) {
+            int nfl = c->dy4p.ftop + 1;
+            HIPCHK(hipMemset(c->dy4p.sync, 0, 4 * sizeof(unsigned)));
+            HIPCHK(hipMemset(c->dy4p.flags, 0, (size_t)nfl * sizeof(unsigned)));
+            return fail(RAOCP_ERR_STATE, "dynamics sweep: a tile task's wait timed out (k_dy4); "
+                                         "RAOCP_DY4=0 selects the per-stage launches");
+        }
+        return RAOCP_OK;
+    }
     if (c->dr && c->sh_S == 0) {
         unsigned e = 0;
         HIPCHK(hipMemcpy(&e, c->drp.sync + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
@@ -743,6 +772,99 @@ int fuse_err(raocp_ctx* c) {
     if (e) HIPCHK(hipMemset(c->fuse_sync, 0, c->fuse_words * sizeof(unsigned)));  // clean protocol state
     if (e) return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dyn_up / k_dyn_down); "
                                         "RAOCP_DYN_SPLIT=0 selects the tier launches");
+    return RAOCP_OK;
+}
+
+// ---- the one-launch dataflow sweep (raocp_dyn4.hip) ------------------------------------------
+// The plan over k_dy3's stages and images (c->d3st, c->d3img_b / f): the top stages are the
+// leading stages of at most two tiles (one workgroup runs them back to back); every other
+// stage's tiles are tasks of the launch (4 per task on wide stages). With RAOCP_DY4=1, when
+// the grid (occupancy x CUs, one workgroup kept for the stopping test) is resident;
+// RAOCP_DY4_TS=t forces the top stages [0, t).
+int dy4_setup(raocp_ctx* c) {
+    const int C = c->unif_branch, N = (int)c->d3st.size();
+    if (N < 2 || N > raocp::kDy4MaxStages || !raocp::dy4_supported(c->f32, c->nx, c->nu, C)) return RAOCP_OK;
+    // opt-in (RAOCP_DY4=1): measured slower than the per-stage launches at configs 4 / 5
+    // (profiles/r05/cp_time_dy4.log: 145-170 vs 113 us, 336-341 vs 195 us)
+    const char* on = getenv("RAOCP_DY4");
+    if (!on || !atoi(on)) return RAOCP_OK;
+    raocp::Dy4Plan& p = c->dy4p;
+    memset(&p, 0, sizeof(p));
+    p.N = N;
+    p.C = C;
+    for (int t = 0; t < N; ++t) {
+        p.i0[t] = c->d3st[t].i0;
+        p.nt[t] = (c->d3st[t].i1 - c->d3st[t].i0 + 15) / 16;
+    }
+    p.i0[N] = c->d3st[N - 1].i1;
+    int ts = 0;
+    while (ts < N - 1 && p.nt[ts] <= 2) ++ts;
+    ts = std::max(ts, 1);
+    if (const char* e = getenv("RAOCP_DY4_TS")) ts = std::min(std::max(atoi(e), 1), N - 1);
+    p.ts = ts;
+    // stages of at least `wide` tiles run tasks of 4 tiles, a wave per tile (the slot sums in
+    // the MFMA registers); the others a tile per task, a wave per slot (RAOCP_DY4_WIDE)
+    int wide = 64;
+    if (const char* e = getenv("RAOCP_DY4_WIDE")) wide = std::max(1, atoi(e));
+    for (int t = 0; t < N; ++t) {
+        p.wide[t] = t >= ts && p.nt[t] >= wide;
+        p.nk[t] = p.wide[t] ? (p.nt[t] + 3) / 4 : p.nt[t];
+    }
+    int task = 0;
+    for (int t = N - 1; t >= ts; --t) {
+        p.tb[t] = task;
+        task += p.nk[t];
+    }
+    p.ttop = task++;
+    for (int t = ts; t < N; ++t) {
+        p.tf[t] = task;
+        task += p.nk[t];
+    }
+    p.ntask = task;
+    int fl = 0;
+    for (int t = ts; t < N; ++t) {
+        p.fb[t] = fl;
+        fl += p.nt[t];
+    }
+    for (int t = ts; t < N; ++t) {
+        p.ff[t] = fl;
+        fl += p.nt[t];
+    }
+    p.ftop = fl++;
+    p.same_kinds = 1;
+    for (int t = 1; t < N; ++t)
+        for (int k = 0; k < C; ++k) p.same_kinds &= c->d3st[t].kind[k] == c->d3st[0].kind[k];
+    p.bimg = c->d3img_b;
+    p.fimg = c->d3img_f;
+    p.bstride = (int)c->d3nb;
+    p.fstride = (int)c->d3nf;
+    p.X0 = c->dev.X0;
+    p.U0 = c->dev.U0;
+    const size_t lds = raocp::dy4_lds(c->f32, c->nx, c->nu, C);
+    const int occ = lds <= 160 * 1024 ? raocp::dy4_occupancy(c->f32, c->nx, c->nu, C, lds) : 0;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+        cus = 256;
+    if (occ < 1) return RAOCP_OK;
+    p.nwg = std::max(1, std::min(p.ntask, occ * cus - 1));  // resident, with room for the stopping test
+    if (const char* e = getenv("RAOCP_DY4_GRID")) p.nwg = std::max(1, std::min(p.nwg, atoi(e)));
+    int rc;
+    unsigned *fw = nullptr, *sy = nullptr;
+    if ((rc = c->alloc(&fw, (size_t)fl)) || (rc = c->alloc(&sy, 4))) return rc;
+    HIPCHK(hipMemset(fw, 0, (size_t)fl * sizeof(unsigned)));
+    HIPCHK(hipMemset(sy, 0, 4 * sizeof(unsigned)));
+    p.flags = fw;
+    p.sync = sy;
+    long long ms = 1000;  // a wait normally lasts microseconds
+    if (const char* e = getenv("RAOCP_FUSE_TIMEOUT_MS")) ms = std::max(1, atoi(e));
+    p.timeout = ms * 100000LL;  // 100 MHz ticks
+    if (const char* e = getenv("RAOCP_DY4_FAULT")) p.fault = atoi(e) & 1;
+    c->dy4 = true;
+    c->dy4_lds = lds;
+    if (getenv("RAOCP_DYN_VERBOSE"))
+        fprintf(stderr, "[raocp] dataflow sweep: %d stages, top [0,%d), %d tasks on %d workgroups (occupancy %d), LDS %zu B\n",
+                N, ts, p.ntask, p.nwg, occ, lds);
     return RAOCP_OK;
 }
 
@@ -1098,7 +1220,7 @@ void launch_cp3(raocp_ctx* c, int part = 0) {
     }
     if (c->cp5 && c->sh_S == 0) {
         raocp::cp5_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->m, c->n, c->cp5_gl, c->cp5_tk,
-                          c->cp5_gf, c->cp3img, c->stream);
+                          c->cp5_gf, c->cp3img, c->cp5_fams, c->stream);
         return;
     }
     if (c->cp4 && c->sh_S == 0) {
@@ -1323,6 +1445,8 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             auto b = [](bool v) { return std::string(v ? "true" : "false"); };
             if (c->dr && c->sh_S == 0) {
                 return std::string(raocp::dr_name(c->nx, c->nu)) + " x1";
+            } else if (c->dy4 && c->sh_S == 0) {
+                return raocp::dy4_name(c->f32, c->nx, c->nu);
             } else if (c->dyn3) {  // a backward and a forward launch per nonleaf stage below the top
                 const int ts = c->sh_S == 0 ? c->d3ts : 0;
                 for (int t = ts; t < c->N; ++t) add("k_dy3_back<" + T + ", " + nn + ">");
@@ -1347,7 +1471,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
         }
         case 10:
             if (c->cp6 && c->sh_S == 0) return raocp::cp6_name();
-            if (c->cp5 && c->sh_S == 0) return raocp::cp5_name(c->f32, c->nx, c->nu, c->unif_C);
+            if (c->cp5 && c->sh_S == 0) return raocp::cp5_name(c->f32, c->nx, c->nu, c->unif_C, c->cp5_fams);
             if (c->cp4 && c->sh_S == 0) return raocp::cp4_name(c->f32, c->nx, c->nu);
             if (c->cp3) return "k_cp3<" + T + ", " + nn + (c->sh_S > 0 ? ", true> x2" : ", false>");
             return kernel_name(c, 2) + " + " + kernel_name(c, 6);
@@ -2057,7 +2181,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         }
         if (c->dyn3) {
             if ((rc = c->alloc(&c->Q2, (size_t)n * nx)) || (rc = c->alloc(&c->Dd2, (size_t)m * nu)) ||
-                (rc = dyn3_images(c)))
+                (rc = dyn3_images(c)) || (rc = dy4_setup(c)))
                 return bail(rc);
             c->dyn32 = c->f32;
         }
@@ -2768,7 +2892,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 if (cp3_tasks(c->cp5_tk, {{c->cp3_mL, m}, {0, c->cp3_mL}}, 0, 0, 1, c->cp3_mL) < 0)
                     return bail(fail(RAOCP_ERR_ARG, "k_cp5 task list exceeds its parent-range slots"));
                 c->cp5_gl = raocp::cp5_leaf_grid(m, n);
-                c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk);
+                // k_cp5_fams where it measured faster (profiles/r05/cp_time_fams.log: config 4
+                // 102.0 -> 91.7 us, config 5 334.5 -> 330.2 us; config 3's 20 / 8, C = 4 tiles
+                // need 276 registers, one workgroup per CU: 60.6 -> 75.1 us, kept on k_cp5_fam)
+                c->cp5_fams = c->f32 || nx == 32;
+                if (const char* e = getenv("RAOCP_CP5_FAMS")) c->cp5_fams = atoi(e) != 0;
+                c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk, c->cp5_fams);
                 if (const char* e = getenv("RAOCP_CP5_LGRID")) c->cp5_gl = std::max(1, atoi(e));
                 if (const char* e = getenv("RAOCP_CP5_FGRID")) c->cp5_gf = std::max(1, atoi(e));
                 c->cp_rows = c->cp5_gl + c->cp5_gf;

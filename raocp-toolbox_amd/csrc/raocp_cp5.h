@@ -10,16 +10,17 @@ namespace raocp {
 // the compiled (type, nx, nu, branching, box pattern) combinations; nbox_nl / nbox_l: the
 // distinct box tables of the nonleaf / leaf nodes (at most one each)
 bool cp5_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbox_l);
-// the two kernels as rocprofv3 names them, "leaf x1 + fam x1"
-const char* cp5_name(bool f32, int nx, int nu, int C);
+// the two kernels as rocprofv3 names them, "leaf x1 + fam x1"; fs: the family launch is
+// k_cp5_fams (a workgroup of C waves per tile), else k_cp5_fam (a wave per tile)
+const char* cp5_name(bool f32, int nx, int nu, int C, bool fs);
 // grids of the two launches for n leaves in [l0, l1) and the family task list tk
 int cp5_leaf_grid(int l0, int l1);
-int cp5_fam_grid(const Cp3Tasks& tk);
+int cp5_fam_grid(const Cp3Tasks& tk, bool fs);
 // the two launches on stream s: leaves [l0, l1) (residual partials in part[0, gl)), then the
 // families of tk (partials in part[gl, gl + gf)); img is k_cp3's weight image
 // ([sqrtQ | sqrtR | sqrtPf] fragments). hipGetLastError() after it is the caller's.
 void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, int l0, int l1, int gl,
-                const Cp3Tasks& tk, int gf, const double* img, hipStream_t s);
+                const Cp3Tasks& tk, int gf, const double* img, bool fs, hipStream_t s);
 
 // k_cp6 (raocp_cp5.hip): the small trees' fused CP iteration, one family tile per workgroup of
 // 2 C waves splitting the tile's roles (config 2); the task list as k_cp5_fam's, the grid one

@@ -1533,19 +1533,9 @@ bool leaf_pf() {
     return v != 0;
 }
 
-// the family launch's form (RAOCP_CP5_FAMS): 1 = k_cp5_fams (a workgroup of C waves per tile,
-// two workgroups per CU), 0 = k_cp5_fam (a wave per tile)
-bool fams() {
-    static const int v = [] {
-        const char* e = getenv("RAOCP_CP5_FAMS");
-        return e ? atoi(e) : 0;
-    }();
-    return v != 0;
-}
-
 template <class T, int NX, int NU, int C>
 void launch_t(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, int l0, int l1, int gl, const Cp3Tasks& tk, int gf,
-              const double* img, hipStream_t s) {
+              const double* img, bool fs, hipStream_t s) {
     // the sqrtPf fragments follow [sqrtQ | sqrtR] in the image (16-B aligned: N multiples of 64)
     const double* imp = img + (size_t)(WL<T, NX, NX>::N + WL<T, NU, NU>::N) * sizeof(T) / 8;
     static const bool pf = [] {
@@ -1553,7 +1543,7 @@ void launch_t(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, int l0, int
         return e ? atoi(e) != 0 : false;
     }();
     const bool lpf = leaf_pf();
-    if (fams()) {
+    if (fs) {
         if (lpf) {
             if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
             else k_cp5_leaf<T, NX, C, 2, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
@@ -1588,10 +1578,10 @@ bool cp5_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbo
     if (!f32) return (nx == 20 && nu == 8 && C == 4) || (nx == 32 && nu == 12 && C == 3);
     return nx == 64 && nu == 16 && C == 4;
 }
-const char* cp5_name(bool f32, int nx, int nu, int C) {
+const char* cp5_name(bool f32, int nx, int nu, int C, bool fs) {
     (void)C;
     (void)nu;
-    if (fams()) {
+    if (fs) {
         if (f32) return "k_cp5_leaf<float, 64, 4> x1 + k_cp5_fams<float, 64, 16, 4> x1";
         if (nx == 20) return "k_cp5_leaf<double, 20, 4> x1 + k_cp5_fams<double, 20, 8, 4> x1";
         return "k_cp5_leaf<double, 32, 3> x1 + k_cp5_fams<double, 32, 12, 3> x1";
@@ -1606,8 +1596,8 @@ int cp5_leaf_grid(int l0, int l1) {
     const long tasks = (long)(std::max(l1 - l0, 0) + 15) / 16 + (l0 + 63) / 64;
     return (leaf_pf() ? 1 : 2) * resident_grid(tasks, 2);  // two workgroups per CU without the prefetch
 }
-int cp5_fam_grid(const Cp3Tasks& tk) {
-    if (fams()) return (int)std::max(1L, std::min((long)tk.t0[tk.nr], 2L * cu_count()));  // two workgroups per CU
+int cp5_fam_grid(const Cp3Tasks& tk, bool fs) {
+    if (fs) return (int)std::max(1L, std::min((long)tk.t0[tk.nr], 2L * cu_count()));  // two workgroups per CU
     return resident_grid(tk.t0[tk.nr], 1);
 }
 // k_cp6: fp64 at nx = 20, nu = 8 with C = 2 (config 2), boxes as for k_cp5
@@ -1624,10 +1614,10 @@ void cp6_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, const Cp3
     else k_cp6<double, 20, 8, 2, 2, 2><<<grid, 256, 0, s>>>(p, ctl, bf, part, tk, img);
 }
 void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, int l0, int l1, int gl,
-                const Cp3Tasks& tk, int gf, const double* img, hipStream_t s) {
-    if (p.nx == 20) launch_t<double, 20, 8, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, s);
-    else if (p.nx == 32) launch_t<double, 32, 12, 3>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, s);
-    else launch_t<float, 64, 16, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, s);
+                const Cp3Tasks& tk, int gf, const double* img, bool fs, hipStream_t s) {
+    if (p.nx == 20) launch_t<double, 20, 8, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, fs, s);
+    else if (p.nx == 32) launch_t<double, 32, 12, 3>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, fs, s);
+    else launch_t<float, 64, 16, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, fs, s);
     (void)C;
 }
 

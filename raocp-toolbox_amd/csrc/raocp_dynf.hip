@@ -391,10 +391,12 @@ __device__ void fz_top_run(const Dev& p, glbd* z, const double* qbuf_, const dou
 // stores before lane 0's release; the waiter's acquire after its poll orders the payload
 // reads after it)
 __device__ __forceinline__ void fz_release_add(unsigned* c) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores have reached the L2
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_fetch_add((gu32*)c, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ void fz_release_store(unsigned* f, unsigned v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's stores have reached the L2
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store((gu32*)f, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }

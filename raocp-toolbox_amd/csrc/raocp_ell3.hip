@@ -70,6 +70,34 @@ __device__ __forceinline__ void load_arow(cglbp<T> v, T (&a)[(K + 3) / 4]) {
     }
 }
 
+// the inverse of load_arow: v[KC h + s] = a[s] for k < K, as 16-B stores where a lane's KC
+// values are whole vectors (eta7 / eta14 rows: a lane writes KC consecutive elements of its
+// node's row; one element per lane and instruction scattered them over 64 rows)
+template <class T, int K>
+__device__ __forceinline__ void store_arow(glbp<T> v, const T (&a)[(K + 3) / 4]) {
+    constexpr int KC = (K + 3) / 4, V = Vec16<T>::V;
+    typedef typename Vec16<T>::type vt;
+    const int h = (threadIdx.x & 63) >> 4;
+    if constexpr (K % 4 == 0 && KC % V == 0) {
+        _Pragma("unroll") for (int s = 0; s < KC; s += V) {
+            vt w;
+            _Pragma("unroll") for (int u = 0; u < V; ++u) w[u] = a[s + u];
+            *(__attribute__((address_space(1))) vt*)(v + KC * h + s) = w;
+        }
+    } else if constexpr (K % 4 == 0 && V == 2 && KC % 2 == 1) {  // fp64, odd KC (nu = 12): pairs + one
+        _Pragma("unroll") for (int s = 0; s + 1 < KC; s += 2) {
+            vt w;
+            w[0] = a[s];
+            w[1] = a[s + 1];
+            *(__attribute__((address_space(1))) vt*)(v + KC * h + s) = w;
+        }
+        v[KC * h + KC - 1] = a[KC - 1];
+    } else {
+        _Pragma("unroll") for (int s = 0; s < KC; ++s)
+            if (KC * h + s < K) v[KC * h + s] = a[s];
+    }
+}
+
 template <class T, int R, int K>
 __device__ __forceinline__ void mma_perm(const WPerm<T, R, K>& w, const T (&a)[(K + 3) / 4],
                                          typename MF<T>::v4 (&acc)[(R + 15) / 16]) {
@@ -198,11 +226,8 @@ k_ell3(Dev p, const double* __restrict__ z_, double* __restrict__ eta_, int C, i
             }
             if (o7 >= 0) {
                 // eta7_i = [x_i; u_i] of a boxed parent from the A registers
-                constexpr int KX = (NX + 3) / 4, KU = (NU + 3) / 4;
-                _Pragma("unroll") for (int k = 0; k < KX; ++k)
-                    if (KX * h + k < nx) eg[o7 + KX * h + k] = ax[k];
-                _Pragma("unroll") for (int k = 0; k < KU; ++k)
-                    if (KU * h + k < nu) eg[o7 + nx + KU * h + k] = au[k];
+                store_arow<T, NX>(eg + o7, ax);
+                store_arow<T, NU>(eg + o7 + nx, au);
             }
             o7 = o7b;
             _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];
@@ -283,11 +308,7 @@ k_ell3(Dev p, const double* __restrict__ z_, double* __restrict__ eta_, int C, i
             mma_perm<T, NX, NX>(wq, ax, cx);
             store_tile<T, NX>(img, cx, cnt, eg + e11(p, l0));
             // eta14 = x (boxed leaves; a leaf's eta14 block is its x row), from the A registers
-            if (o14 >= 0) {
-                constexpr int KX = (NX + 3) / 4;
-                _Pragma("unroll") for (int k = 0; k < KX; ++k)
-                    if (KX * h + k < nx) eg[o14 + KX * h + k] = ax[k];
-            }
+            if (o14 >= 0) store_arow<T, NX>(eg + o14, ax);
             // eta12 = eta13 = s / 2
             if (lane < 2 * cnt) eg[((lane & 1) ? p.E13 : p.E12) + l0 + (lane >> 1)] = T(0.5) * sv;
             o14 = o14b;

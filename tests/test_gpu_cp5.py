@@ -139,7 +139,7 @@ def test_cp5_config5_fp32_matches_cp3():
     r = _recipe("c5")
     tree, prob = build_problem(r)
     c5, c3 = _pair(prob, "float32")
-    assert c5.native.kernel_info(10) == "k_cp5_leaf<float, 64, 4> x1 + k_cp5_fam<float, 64, 16, 4> x1"
+    assert c5.native.kernel_info(10).startswith("k_cp5_leaf<float, 64, 4> x1 + k_cp5_fam")
     alpha = 0.999 / c5.native.step_size(rtol=1e-7)
     K = 8
     a = _run(c5, r["x0"], K, alpha)
@@ -199,3 +199,26 @@ def test_cp5_nan_in_box_raises():
     alpha = 0.999 / cache.native.step_size()
     with pytest.raises(ValueError):
         cache.native.cp_run(x0, 5, 0.0, alpha)
+
+
+@pytest.mark.parametrize("case", ["q20", "t32", "t32-nobox", "q64", "c4"])
+def test_cp5_slot_parallel_family_matches_wave_family(case):
+    """k_cp5_fams (a workgroup of C waves per family tile, RAOCP_CP5_FAMS=1) against k_cp5_fam
+    (one wave per tile): the same entry arithmetic and slot-order sums, so the loops agree at
+    rounding level (1e-12 fp64, fp32: 1e-5 on the traces)."""
+    r = _recipe(case)
+    tree, prob = build_problem(r)
+    dt = "float32" if case == "q64" else None
+    mk = (lambda: core.Cache(prob, dtype=dt)) if dt else (lambda: core.Cache(prob))
+    a = _with_env({"RAOCP_CP5_FAMS": "1"}, mk)
+    b = _with_env({"RAOCP_CP5_FAMS": "0"}, mk)
+    assert " + k_cp5_fams<" in a.native.kernel_info(10) and " + k_cp5_fam<" in b.native.kernel_info(10)
+    alpha = 0.999 / a.native.step_size(rtol=1e-7 if dt else 1e-14)
+    K = 14 if case == "c4" else 30
+    ra = _run(a, r["x0"], K, alpha)
+    rb = _run(b, r["x0"], K, alpha)
+    tol = 1e-5 if dt else 1e-12
+    assert ra[0] == rb[0] == 1
+    assert trace_rel_err(ra[1], rb[1]) <= tol and trace_rel_err(ra[2], rb[2]) <= tol
+    assert rel_err(ra[3], rb[3]) <= tol and rel_err(ra[4], rb[4]) <= tol
+    print(f"{case}: bit-identical {all(np.array_equal(u, v) for u, v in zip(ra, rb))}")
