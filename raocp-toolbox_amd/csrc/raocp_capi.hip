@@ -2892,10 +2892,9 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 if (cp3_tasks(c->cp5_tk, {{c->cp3_mL, m}, {0, c->cp3_mL}}, 0, 0, 1, c->cp3_mL) < 0)
                     return bail(fail(RAOCP_ERR_ARG, "k_cp5 task list exceeds its parent-range slots"));
                 c->cp5_gl = raocp::cp5_leaf_grid(m, n);
-                // k_cp5_fams where it measured faster (profiles/r05/cp_time_fams.log: config 4
-                // 102.0 -> 91.7 us, config 5 334.5 -> 330.2 us; config 3's 20 / 8, C = 4 tiles
-                // need 276 registers, one workgroup per CU: 60.6 -> 75.1 us, kept on k_cp5_fam)
-                c->cp5_fams = c->f32 || nx == 32;
+                // k_cp5_fams (profiles/r05/cp_time_fams*.log: config 4 100.7 -> 90.9 us, config 5
+                // 335.3 -> 334.8 us, config 3 60.9 -> 57.4 us with the compacted slot sums)
+                c->cp5_fams = true;
                 if (const char* e = getenv("RAOCP_CP5_FAMS")) c->cp5_fams = atoi(e) != 0;
                 c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk, c->cp5_fams);
                 if (const char* e = getenv("RAOCP_CP5_LGRID")) c->cp5_gl = std::max(1, atoi(e));

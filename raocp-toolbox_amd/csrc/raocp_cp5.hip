@@ -164,6 +164,37 @@ __device__ __forceinline__ void lds_get(const __attribute__((address_space(3))) 
     }
 }
 
+// the same vector compacted: lane's R / 4 values at base[lane R / 4 ..] (no padded chunk
+// slots: nx = 20 keeps 5 of the 8 values a row-layout chunk pair holds), 16-B accesses where
+// R / 4 is even
+template <class T, int R>
+__device__ __forceinline__ void lds_putc(__attribute__((address_space(3))) T* base, const T (&a)[(R + 15) / 16][4]) {
+    constexpr int KC = R / 4;
+    __attribute__((address_space(3))) T* b = base + (threadIdx.x & 63) * KC;
+    if constexpr (KC % 2 == 0 && sizeof(T) == 8) {
+        typedef T v2 __attribute__((ext_vector_type(2)));
+        _Pragma("unroll") for (int t = 0; t < KC; t += 2) *(__attribute__((address_space(3))) v2*)(b + t) = v2{a[t >> 2][t & 3], a[(t + 1) >> 2][(t + 1) & 3]};
+    } else {
+        _Pragma("unroll") for (int t = 0; t < KC; ++t) b[t] = a[t >> 2][t & 3];
+    }
+}
+template <class T, int R>
+__device__ __forceinline__ void lds_getc(const __attribute__((address_space(3))) T* base, T (&a)[(R + 15) / 16][4]) {
+    constexpr int KC = R / 4;
+    const __attribute__((address_space(3))) T* b = base + (threadIdx.x & 63) * KC;
+    _Pragma("unroll") for (int rt = 0; rt < (R + 15) / 16; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) a[rt][e] = T(0);
+    if constexpr (KC % 2 == 0 && sizeof(T) == 8) {
+        typedef T v2 __attribute__((ext_vector_type(2)));
+        _Pragma("unroll") for (int t = 0; t < KC; t += 2) {
+            const v2 w = *(const __attribute__((address_space(3))) v2*)(b + t);
+            a[t >> 2][t & 3] = w[0];
+            a[(t + 1) >> 2][(t + 1) & 3] = w[1];
+        }
+    } else {
+        _Pragma("unroll") for (int t = 0; t < KC; ++t) a[t >> 2][t & 3] = b[t];
+    }
+}
+
 // ================================ k_cp5_leaf ================================
 // the operands of one leaf tile (lane lo = leaf)
 template <class T, int NX, int BXL>
@@ -756,7 +787,8 @@ __global__ void __launch_bounds__(64 * C, 2) k_cp5_fams(Dev p, Ctl* ctl, Bufs bf
     __shared__ KpScratch<T> ks_;
     __shared__ __attribute__((aligned(16))) T wlds_[WQ::N + WR::N];
     __shared__ __attribute__((aligned(16))) T blds_[2 * (NX + NU)];  // [lo_nl | hi_nl]
-    constexpr int SS = (RX + RU) * 256;  // one stream of one slot: [x chunks RX | u chunks RU] x 64 lanes x 4
+    // one stream of one slot, compacted: [x: 64 lanes x nx / 4 | u: 64 lanes x nu / 4]
+    constexpr int SX = NX / 4 * 64, SS = (NX + NU) / 4 * 64;
     __shared__ __attribute__((aligned(16))) T sums_[C * 3 * SS];
     const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4, wv = threadIdx.x >> 6;
     typedef __attribute__((address_space(3))) T lT;
@@ -892,9 +924,9 @@ __global__ void __launch_bounds__(64 * C, 2) k_cp5_fams(Dev p, Ctl* ctl, Bufs bf
                     eC[rt][e] = x2;
                 }
                 st_rows_o<T, NX>(eo, p.E3 + 1 + (j - 1) * NX, live, eA);
-                lds_put<T, NX>(sk, eA, false);
-                lds_put<T, NX>(sk + SS, eW, false);
-                lds_put<T, NX>(sk + 2 * SS, eC, false);
+                lds_putc<T, NX>(sk, eA);
+                lds_putc<T, NX>(sk + SS, eW);
+                lds_putc<T, NX>(sk + 2 * SS, eC);
             }
             {
                 T eA[RU][4], eW[RU][4], eC[RU][4];
@@ -906,9 +938,9 @@ __global__ void __launch_bounds__(64 * C, 2) k_cp5_fams(Dev p, Ctl* ctl, Bufs bf
                     eC[rt][e] = x2;
                 }
                 st_rows_o<T, NU>(eo, p.E4 + 1 + (j - 1) * NU, live, eA);
-                lds_put<T, NU>(sk + RX * 256, eA, false);
-                lds_put<T, NU>(sk + SS + RX * 256, eW, false);
-                lds_put<T, NU>(sk + 2 * SS + RX * 256, eC, false);
+                lds_putc<T, NU>(sk + SX, eA);
+                lds_putc<T, NU>(sk + SS + SX, eW);
+                lds_putc<T, NU>(sk + 2 * SS + SX, eC);
             }
             T ep5, x25, ep6, x26;
             rs.fin(d5, v5, so.first(v5), b5, ep5, x25);
@@ -977,12 +1009,12 @@ __global__ void __launch_bounds__(64 * C, 2) k_cp5_fams(Dev p, Ctl* ctl, Bufs bf
             }
             // the slots' rows of stream q summed per parent in slot order
             auto sums = [&](int q, T (&sx)[RX][4], T (&su)[RU][4]) {
-                lds_get<T, NX>(sb + q * SS, sx);
-                lds_get<T, NU>(sb + q * SS + RX * 256, su);
+                lds_getc<T, NX>(sb + q * SS, sx);
+                lds_getc<T, NU>(sb + q * SS + SX, su);
                 _Pragma("unroll") for (int kk = 1; kk < C; ++kk) {
                     T ax[RX][4], au[RU][4];
-                    lds_get<T, NX>(sb + (kk * 3 + q) * SS, ax);
-                    lds_get<T, NU>(sb + (kk * 3 + q) * SS + RX * 256, au);
+                    lds_getc<T, NX>(sb + (kk * 3 + q) * SS, ax);
+                    lds_getc<T, NU>(sb + (kk * 3 + q) * SS + SX, au);
                     _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) sx[rt][e] += ax[rt][e];
                     _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) su[rt][e] += au[rt][e];
                 }

@@ -18,7 +18,30 @@
 #ifndef ELL3_WPE
 #define ELL3_WPE 3
 #endif
-#define ELL3_WPE_OF(T, NX) ((NX) >= 64 ? (sizeof(T) == 8 ? 1 : 2) : ELL3_WPE)
+// output stores of k_ell3 (ELL3_NT) / k_ellt3 (ELLT3_NT): 1 = nontemporal (the rows are
+// streamed out, never re-read by the launch). Measured over rotating HBM-sized buffer sets
+// (profiles/r05/l_sweep_variants.log): L^T at config 4 27.1 -> 22.7 us with nontemporal
+// stores (config 5 unchanged), L 27.5 -> 38.4 us (its 16-node tiles replicated to the C
+// children through the per-wave LDS image): on for L^T only
+#ifndef ELL3_NT
+#define ELL3_NT 0
+#endif
+#ifndef ELLT3_NT
+#define ELLT3_NT 1
+#endif
+template <bool NT, class P, class V>
+__device__ __forceinline__ void ostn(P* p, V v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <class P, class V>
+__device__ __forceinline__ void ost(P* p, V v) {
+    ostn<ELL3_NT != 0>(p, v);
+}
+#ifndef ELL3_WPE64
+#define ELL3_WPE64 2
+#endif
+#define ELL3_WPE_OF(T, NX) ((NX) >= 64 ? (sizeof(T) == 8 ? 1 : ELL3_WPE64) : ELL3_WPE)
 // weights of one table, k-permuted: b[rt][s] = M[row 16 rt + lo][KC h + s]; R rows, K cols
 template <class T, int R, int K>
 struct WPerm {
@@ -82,14 +105,14 @@ __device__ __forceinline__ void store_arow(glbp<T> v, const T (&a)[(K + 3) / 4])
         _Pragma("unroll") for (int s = 0; s < KC; s += V) {
             vt w;
             _Pragma("unroll") for (int u = 0; u < V; ++u) w[u] = a[s + u];
-            *(__attribute__((address_space(1))) vt*)(v + KC * h + s) = w;
+            ost((__attribute__((address_space(1))) vt*)(v + KC * h + s), w);
         }
     } else if constexpr (K % 4 == 0 && V == 2 && KC % 2 == 1) {  // fp64, odd KC (nu = 12): pairs + one
         _Pragma("unroll") for (int s = 0; s + 1 < KC; s += 2) {
             vt w;
             w[0] = a[s];
             w[1] = a[s + 1];
-            *(__attribute__((address_space(1))) vt*)(v + KC * h + s) = w;
+            ost((__attribute__((address_space(1))) vt*)(v + KC * h + s), w);
         }
         v[KC * h + KC - 1] = a[KC - 1];
     } else {
@@ -133,12 +156,12 @@ __device__ __forceinline__ void store_tile(__attribute__((address_space(3))) T* 
             const int a = q / R, r = q - a * R, ia = rep == 1 ? a : a / rep;
             vt w;
             _Pragma("unroll") for (int u = 0; u < V; ++u) w[u] = img[ia * S + r + u];
-            *(__attribute__((address_space(1))) vt*)(dst + q) = w;
+            ost((__attribute__((address_space(1))) vt*)(dst + q), w);
         }
     } else {
         for (int q = lane; q < tot; q += 64) {
             const int a = q / R, r = q - a * R, ia = rep == 1 ? a : a / rep;
-            dst[q] = img[ia * S + r];
+            ost(&dst[q], (T)img[ia * S + r]);
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -419,7 +442,7 @@ k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C, 
                     T v = e7x[sl][rt];  // the reference starts from C7' eta7 or 0 (operators.py:73-78)
                     _Pragma("unroll") for (int e = 0; e < 4; ++e)
                         if (e / C == sl && e < Q * C) v += cx[rt][e];
-                    zg[p.X0 + (size_t)q * nx + r] = v;
+                    ostn<ELLT3_NT != 0>(&zg[p.X0 + (size_t)q * nx + r], v);
                 }
                 _Pragma("unroll") for (int rt = 0; rt < RTU; ++rt) {
                     const int r = 16 * rt + lo;
@@ -427,7 +450,7 @@ k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C, 
                     T v = e7u[sl][rt];
                     _Pragma("unroll") for (int e = 0; e < 4; ++e)
                         if (e / C == sl && e < Q * C) v += cu[rt][e];
-                    zg[p.U0 + (size_t)q * nu + r] = v;
+                    ostn<ELLT3_NT != 0>(&zg[p.U0 + (size_t)q * nu + r], v);
                 }
             }
             _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];
@@ -472,7 +495,7 @@ k_ellt3(Dev p, const double* __restrict__ eta_, double* __restrict__ z_, int C, 
                     if (r >= nx) continue;
                     T v = cx[rt][e];
                     if (b14[e]) v += e14[e][rt];
-                    zg[p.X0 + (size_t)l * nx + r] = v;
+                    ostn<ELLT3_NT != 0>(&zg[p.X0 + (size_t)l * nx + r], v);
                 }
             }
             _Pragma("unroll") for (int k = 0; k < (NX + 3) / 4; ++k) ax[k] = ax2[k];

@@ -10,11 +10,14 @@
 #   cptests     the CP-kernel test files (cp3, cp4, cp5, fp32)
 #   dyntests    the dynamics test files (dynr, dyn_split, dyn3, variants)
 #   tests       the whole -m gpu suite
+#   rest        the test files in $REST_TESTS (default tests/test_gpu_variants.py)
 #   smoke       __graft_entry__.smoke()
 #   dyn         dynamics projection timings at config 2 (tools/dyn_time.py, variants in $DYN_VARIANTS)
 #   stamps      in-kernel stamps of the regular-tree sweep at config 2 (tools/dr_stamps.py)
 #   cp          CP kernel / dynamics / loop timings (tools/cp3_time.py)
 #   lsweep      standalone L / L^T at configs 2, 4 (3 buffer sets) and 5 fp32 (2 sets)
+#   lsweepvar   the same at configs 4 and 5 for each variant library build/var/<v>.so in $LSWEEP_LIBS
+#               (tools/build_var.sh)
 #   dy3trace    per-launch trace of the config-4 / config-5 dynamics (rocprofv3 kernel trace, tools/trace_seq.py)
 #   bench20     bench.py --steps 20 --warmup 5 (the driver's K)
 #   bench       bench.py default run
@@ -51,6 +54,8 @@ for step in "$@"; do
           tail -3 $out/pytest_cp.log ;;
     dyntests) timeout -k 10 900 $PYT tests/test_gpu_dynr.py tests/test_gpu_dyn_split.py tests/test_gpu_dyn3.py tests/test_gpu_dyn4.py tests/test_gpu_variants.py > $out/pytest_dyn.log 2>&1 || fail $step $out/pytest_dyn.log
           tail -3 $out/pytest_dyn.log ;;
+    rest) timeout -k 10 900 $PYT ${REST_TESTS:-tests/test_gpu_variants.py} > $out/pytest_rest.log 2>&1 || fail $step $out/pytest_rest.log
+          tail -3 $out/pytest_rest.log ;;
     tests) timeout -k 10 1100 $PYT tests > $out/pytest_gpu.log 2>&1 || fail $step $out/pytest_gpu.log
           tail -3 $out/pytest_gpu.log ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || fail $step $out/smoke.log
@@ -64,6 +69,12 @@ for step in "$@"; do
     lsweep) for a in "2 float64 1" "4 float64 3" "5 float32 2"; do
               timeout -k 10 200 python -u tools/l_sweep.py $a >> $out/l_sweep.log 2>&1 || fail $step $out/l_sweep.log
             done; grep config $out/l_sweep.log ;;
+    lsweepvar) for v in ${LSWEEP_LIBS:-}; do
+                 for a in "4 float64 3" "5 float32 2"; do
+                   RAOCP_HIP_LIB=build/var/$v.so timeout -k 10 200 python -u tools/l_sweep.py $a >> $out/l_sweep_$v.log 2>&1 || fail $step $out/l_sweep_$v.log
+                 done
+                 echo "variant $v"; grep config $out/l_sweep_$v.log
+               done ;;
     dy3trace) for cfg in 4 5; do
                 timeout -k 10 240 rocprofv3 --kernel-trace -d $out/tr$cfg -o tr --output-format csv -- python3 tools/dyn_time.py child $cfg trace > $out/tr$cfg.log 2>&1 || fail $step $out/tr$cfg.log
                 python3 tools/trace_seq.py $out/tr$cfg 30 > $out/dy3_stages_c$cfg.log; cat $out/dy3_stages_c$cfg.log

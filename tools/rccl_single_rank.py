@@ -5,9 +5,10 @@ around X1). Run as its own process: torch must not be imported (see bench.py Soc
 import os, sys
 os.environ["RAOCP_SHARD_FORCE"] = "1"
 # the unsharded reference runs the kernels a shard runs: the tier launches (not k_dr) and
-# k_cp3 (not k_cp4, the same arithmetic with a different FMA contraction)
+# k_cp3 (not k_cp6 / k_cp4, the same arithmetic with a different FMA contraction)
 os.environ["RAOCP_DR"] = "0"
 os.environ["RAOCP_CP4"] = "0"
+os.environ["RAOCP_CP6"] = "0"
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raocp-toolbox_amd"))
 import numpy as np
 import raocp.core as core
