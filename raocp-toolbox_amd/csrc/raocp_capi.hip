@@ -2880,7 +2880,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                     return bail(fail(RAOCP_ERR_ARG, "k_cp6 task list exceeds its parent-range slots"));
                 c->cp6_grid = raocp::cp6_grid(c->cp5_tk);
                 if (const char* e = getenv("RAOCP_CP6_GRID")) c->cp6_grid = std::max(1, atoi(e));
-                c->cp_rows = c->cp6_grid;
+                c->cp_rows = raocp::cp6_rows(c->cp6_grid);
                 if (c->cp_rows > c->red_rows) {
                     c->red_rows = c->cp_rows;
                     if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
@@ -2899,7 +2899,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk, c->cp5_fams);
                 if (const char* e = getenv("RAOCP_CP5_LGRID")) c->cp5_gl = std::max(1, atoi(e));
                 if (const char* e = getenv("RAOCP_CP5_FGRID")) c->cp5_gf = std::max(1, atoi(e));
-                c->cp_rows = c->cp5_gl + c->cp5_gf;
+                c->cp_rows = raocp::cp5_rows(c->cp5_gl, c->cp5_gf, c->cp5_fams, c->unif_C);
                 if (c->cp_rows > c->red_rows) {
                     c->red_rows = c->cp_rows;
                     if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);

@@ -16,18 +16,23 @@ const char* cp5_name(bool f32, int nx, int nu, int C, bool fs);
 // grids of the two launches for n leaves in [l0, l1) and the family task list tk
 int cp5_leaf_grid(int l0, int l1);
 int cp5_fam_grid(const Cp3Tasks& tk, bool fs);
-// the two launches on stream s: leaves [l0, l1) (residual partials in part[0, gl)), then the
-// families of tk (partials in part[gl, gl + gf)); img is k_cp3's weight image
+// rows of residual partials the two launches write (one per workgroup; the family launch's
+// rows after the leaf launch's gl)
+int cp5_rows(int gl, int gf, bool fs, int C);
+// the two launches on stream s: leaves [l0, l1) (residual partials in rows [0, gl) of part),
+// then the families of tk (the rows after them, cp5_rows); img is k_cp3's weight image
 // ([sqrtQ | sqrtR | sqrtPf] fragments). hipGetLastError() after it is the caller's.
 void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, int l0, int l1, int gl,
                 const Cp3Tasks& tk, int gf, const double* img, bool fs, hipStream_t s);
 
 // k_cp6 (raocp_cp5.hip): the small trees' fused CP iteration, one family tile per workgroup of
 // 2 C waves splitting the tile's roles (config 2); the task list as k_cp5_fam's, the grid one
-// workgroup per tile, the residual partials one row per workgroup
+// workgroup per tile, the residual partials one row per workgroup (cp6_rows)
 bool cp6_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbox_l);
 const char* cp6_name();
 int cp6_grid(const Cp3Tasks& tk);
+// rows of residual partials a launch of `grid` workgroups writes
+int cp6_rows(int grid);
 void cp6_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, const Cp3Tasks& tk, int grid, const double* img,
                 hipStream_t s);
 

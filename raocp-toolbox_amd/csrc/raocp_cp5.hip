@@ -112,15 +112,32 @@ __device__ __forceinline__ void flag_nan(Ctl* ctl, bool nan) {
     if (__builtin_amdgcn_ballot_w64(nan) != 0 && (threadIdx.x & 63) == 0) atomicOr(&ctl->flags, 1);
 }
 
-// per-block residual maxima -> one row of `part` (plain stores, k_cp_check reduces)
+// per-block residual maxima -> one row of `part` (plain stores, k_cp_check reduces). A wave's
+// maxima by DPP steps within rows of 16 lanes (xor 1, xor 2, half-mirror, mirror), then the
+// row broadcasts 15 and 31 (GFX9 wave64 DPP): lane 63 ends with them (NaN-propagating nmax
+// throughout; the ds_bpermute butterfly it replaces cost k_cp6 ~0.7 us per workgroup)
+template <int CTRL, int RM>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(v), __double2loint(v), CTRL, RM, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(v), __double2hiint(v), CTRL, RM, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double wave_nmax(double v) {
+    v = nmax(v, dpp_d<0xB1, 0xF>(v));   // lane ^ 1
+    v = nmax(v, dpp_d<0x4E, 0xF>(v));   // lane ^ 2
+    v = nmax(v, dpp_d<0x141, 0xF>(v));  // row half-mirror: the 8-lane maxima
+    v = nmax(v, dpp_d<0x140, 0xF>(v));  // row mirror: the 16-lane maxima
+    v = nmax(v, dpp_d<0x142, 0xA>(v));  // row_bcast15 into rows 1 and 3
+    v = nmax(v, dpp_d<0x143, 0xC>(v));  // row_bcast31 into rows 2 and 3
+    return v;
+}
 template <class T>
 __device__ __forceinline__ void block_maxima(double* part, const Resid<T>& r) {
     __shared__ double s_red[6][16];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    double mm[6] = {r.m0.get(), r.m1.get(), r.m2.get(), r.m3.get(), r.m4.get(), r.m5.get()};
-    _Pragma("unroll") for (int q = 0; q < 6; ++q)
-        _Pragma("unroll") for (int off = 32; off > 0; off >>= 1) mm[q] = nmax(mm[q], __shfl_xor(mm[q], off, 64));
-    if (lane == 0) _Pragma("unroll") for (int q = 0; q < 6; ++q) s_red[q][wv] = mm[q];
+    const double mm[6] = {wave_nmax(r.m0.get()), wave_nmax(r.m1.get()), wave_nmax(r.m2.get()),
+                          wave_nmax(r.m3.get()), wave_nmax(r.m4.get()), wave_nmax(r.m5.get())};
+    const int wv = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 63) _Pragma("unroll") for (int q = 0; q < 6; ++q) s_red[q][wv] = mm[q];
     __syncthreads();
     if (threadIdx.x < 6) {
         double b = s_red[threadIdx.x][0];
@@ -1127,6 +1144,16 @@ __global__ void __launch_bounds__(128 * C) k_cp6(Dev p, Ctl* ctl, Bufs bf, doubl
     cglbp<T> cond = (cglbp<T>)p.cond;
     lT* bl_ = (lT*)blds_;
     const int m = p.m;
+    // diagnostics (diagnostic builds, RAOCP_STAMP_KERNEL=c): every wave of the workgroup whose
+    // first task is p.cp_dbg stamps [entry, prologue done, role done, barrier, streams done,
+    // exit] at stamps[8 wave + q]; every workgroup its [entry, exit] at stamps[64 + 2 block]
+    const unsigned long long t_in = kDiag && p.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    const bool stp_on = kDiag && p.stamps && (int)blockIdx.x == p.cp_dbg && lane == 0;
+    int stp_n = 0;
+    auto stamp = [&]() {
+        if (kDiag && stp_on && stp_n < 8) p.stamps[8 * wv + stp_n++] = __builtin_amdgcn_s_memrealtime();
+    };
+    stamp();
     {
         lds_fill((lds_d*)wlds_, img, (2 * WQ::N + WR::N) * (int)sizeof(T) / 16);  // [sqrtQ | sqrtR | sqrtPf]
         for (int e = threadIdx.x; e < 2 * (NX + NU) + 2 * NX; e += blockDim.x) {  // one box table each
@@ -1146,6 +1173,7 @@ __global__ void __launch_bounds__(128 * C) k_cp6(Dev p, Ctl* ctl, Bufs bf, doubl
     dma_wait();
     __syncthreads();
     if (done) return;  // uniform over the grid
+    stamp();
     const WQ wq{(const lT*)wlds_};
     const WR wr{(const lT*)wlds_ + WQ::N};
     const WP wp{(const lT*)wlds_ + WQ::N + WR::N};
@@ -1415,7 +1443,9 @@ __global__ void __launch_bounds__(128 * C) k_cp6(Dev p, Ctl* ctl, Bufs bf, doubl
             }
             st_rows_o<T, NX>(out, p.X0 + (live ? l : 0) * NX, live, ox);
         }
+        stamp();
         __syncthreads();  // the slots' rows, tau, s and y of the half step are in LDS
+        stamp();
         if (wv <= 1) {
             // ---------------- phase 3: L^T = Gamma' eta7 + sqrtQ' / sqrtR' (summed slot rows)
             // (operators.py:73-85); wave 0 the eta+ stream, wave 1 the (d - eta+) and xi2 streams
@@ -1532,10 +1562,16 @@ __global__ void __launch_bounds__(128 * C) k_cp6(Dev p, Ctl* ctl, Bufs bf, doubl
             }
             if (h == 0) *elw(out, p.Y0 + yo + 2 * C) = y2c - sw;
         }
+        stamp();
         __syncthreads();  // the LDS rows and the scratch are the next tile's
     }
     flag_nan(ctl, nanf);
     block_maxima(part, rs);
+    stamp();
+    if (kDiag && p.stamps && threadIdx.x == 0 && blockIdx.x < 2000) {
+        p.stamps[64 + 2 * blockIdx.x] = t_in;
+        p.stamps[65 + 2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    }
 }
 
 // resident grid: one 256-lane workgroup (one wave per SIMD) per CU, fewer when the tasks
@@ -1628,6 +1664,12 @@ int cp5_leaf_grid(int l0, int l1) {
     const long tasks = (long)(std::max(l1 - l0, 0) + 15) / 16 + (l0 + 63) / 64;
     return (leaf_pf() ? 1 : 2) * resident_grid(tasks, 2);  // two workgroups per CU without the prefetch
 }
+// rows of residual partials of the two launches (one per workgroup)
+int cp5_rows(int gl, int gf, bool fs, int C) {
+    (void)fs;
+    (void)C;
+    return gl + gf;
+}
 int cp5_fam_grid(const Cp3Tasks& tk, bool fs) {
     if (fs) return (int)std::max(1L, std::min((long)tk.t0[tk.nr], 2L * cu_count()));  // two workgroups per CU
     return resident_grid(tk.t0[tk.nr], 1);
@@ -1639,6 +1681,7 @@ bool cp6_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbo
     return !f32 && nx == 20 && nu == 8 && C == 2;
 }
 const char* cp6_name() { return "k_cp6<double, 20, 8, 2>"; }
+int cp6_rows(int grid) { return grid; }  // a residual row per workgroup
 int cp6_grid(const Cp3Tasks& tk) { return (int)std::max(1L, std::min((long)tk.t0[tk.nr], 4096L)); }
 void cp6_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, const Cp3Tasks& tk, int grid, const double* img,
                 hipStream_t s) {

@@ -18,6 +18,7 @@
 #   lsweep      standalone L / L^T at configs 2, 4 (3 buffer sets) and 5 fp32 (2 sets)
 #   lsweepvar   the same at configs 4 and 5 for each variant library build/var/<v>.so in $LSWEEP_LIBS
 #               (tools/build_var.sh)
+#   cp6stamps   k_cp6's in-kernel stamps at config 2 (diagnostic variant build/var/diag.so)
 #   dy3trace    per-launch trace of the config-4 / config-5 dynamics (rocprofv3 kernel trace, tools/trace_seq.py)
 #   bench20     bench.py --steps 20 --warmup 5 (the driver's K)
 #   bench       bench.py default run
@@ -75,6 +76,9 @@ for step in "$@"; do
                  done
                  echo "variant $v"; grep config $out/l_sweep_$v.log
                done ;;
+    cp6stamps) for wg in 200 50; do
+                 RAOCP_CP2_DBG=$wg RAOCP_HIP_LIB=build/var/diag.so timeout -k 10 120 python -u tools/cp6_stamps.py 3 >> $out/cp6_stamps.log 2>&1 || fail $step $out/cp6_stamps.log
+               done; cat $out/cp6_stamps.log ;;
     dy3trace) for cfg in 4 5; do
                 timeout -k 10 240 rocprofv3 --kernel-trace -d $out/tr$cfg -o tr --output-format csv -- python3 tools/dyn_time.py child $cfg trace > $out/tr$cfg.log 2>&1 || fail $step $out/tr$cfg.log
                 python3 tools/trace_seq.py $out/tr$cfg 30 > $out/dy3_stages_c$cfg.log; cat $out/dy3_stages_c$cfg.log
