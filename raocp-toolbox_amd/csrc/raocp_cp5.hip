@@ -1110,8 +1110,10 @@ __global__ void __launch_bounds__(64 * C, 2) k_cp5_fams(Dev p, Ctl* ctl, Bufs bf
 //   -- barrier --
 //   wave 0            L^T of the eta+ stream: Gamma' eta7 (box) + sqrtQ' / sqrtR' of the slots'
 //                     rows summed in slot order (k_cp3's order), x_i, u_i of the half step;
-//   wave 1            the (d - eta+) and xi2 streams and the residual terms of x_i, u_i;
-//   wave C            phase 5: the AVaR kernel projection of the family (cache.py:290-317).
+//   wave 1            the (d - eta+) stream; wave 2 C - 1 the xi2 stream, to LDS;
+//   wave C            phase 5: the AVaR kernel projection of the family (cache.py:290-317);
+//   -- barrier --
+//   wave 1            the residual terms of x_i, u_i from both streams.
 //
 // Every operand of a role is loaded at the tile's start (k_cp4's unconditional loads), through
 // 32-bit saddr offsets. Same arithmetic per entry as k_cp5 (results agree with k_cp4 / k_cp3 at
@@ -1131,6 +1133,7 @@ __global__ void __launch_bounds__(128 * C) k_cp6(Dev p, Ctl* ctl, Bufs bf, doubl
     // the slots' (eta+, d - eta+, xi2) rows: [slot][stream][x chunks RX | u chunks RU] x 64 lanes x 4
     constexpr int SS = (RX + RU) * 256;
     __shared__ __attribute__((aligned(16))) T sums_[C * 3 * SS];
+    __shared__ __attribute__((aligned(16))) T xch_[(RX + RU) * 256];  // the xi2 stream's L^T, wave 2 C - 1 -> wave 1
     const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4, wv = threadIdx.x >> 6;
     typedef __attribute__((address_space(3))) T lT;
     typedef __attribute__((address_space(3))) KpScratch<T> lkps;
@@ -1446,15 +1449,18 @@ __global__ void __launch_bounds__(128 * C) k_cp6(Dev p, Ctl* ctl, Bufs bf, doubl
         stamp();
         __syncthreads();  // the slots' rows, tau, s and y of the half step are in LDS
         stamp();
-        if (wv <= 1) {
+        lT* xch = (lT*)xch_;
+        T xp[RX][4], xz[RX][4], up[RU][4], uz[RU][4];  // wave 1: the parent's rows for the residual terms
+        v4 g1[RX], h1[RU];
+        if (wv <= 1 || wv == 2 * C - 1) {
             // ---------------- phase 3: L^T = Gamma' eta7 + sqrtQ' / sqrtR' (summed slot rows)
-            // (operators.py:73-85); wave 0 the eta+ stream, wave 1 the (d - eta+) and xi2 streams
-            T xz[RX][4], xp[RX][4], uz[RU][4], up[RU][4];
+            // (operators.py:73-85); wave 0 the eta+ stream, wave 1 the (d - eta+) stream, wave
+            // 2 C - 1 the xi2 stream
             ld_rows_o<T, NX>(zp, p.X0 + iq * NX, live, xz);
             ld_rows_o<T, NX>(pz, p.X0 + iq * NX, live, xp);
             ld_rows_o<T, NU>(zp, p.U0 + iq * NU, live, uz);
             ld_rows_o<T, NU>(pz, p.U0 + iq * NU, live, up);
-            v4 g0[RX], g1[RX], g2[RX], h0[RU], h1[RU], h2[RU];
+            v4 g0[RX], g2[RX], h0[RU], h2[RU];
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) g0[rt] = g1[rt] = g2[rt] = v4{0, 0, 0, 0};
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) h0[rt] = h1[rt] = h2[rt] = v4{0, 0, 0, 0};
             if (BXN == 1) {
@@ -1520,23 +1526,20 @@ __global__ void __launch_bounds__(128 * C) k_cp6(Dev p, Ctl* ctl, Bufs bf, doubl
                 _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                     ou[rt][e] = uz[rt][e] - alpha * h0[rt][e];
                 st_rows_o<T, NU>(out, p.U0 + iq * NU, live, ou);
+            } else if (wv == 1) {
+                T sx[RX][4], su[RU][4];
+                sums(1, sx, su);
+                mmt(wq.fresh(), sx, g1);
+                mmt(wr.fresh(), su, h1);
             } else {
-                {
-                    T sx[RX][4], su[RU][4];
-                    sums(1, sx, su);
-                    mmt(wq.fresh(), sx, g1);
-                    mmt(wr.fresh(), su, h1);
-                }
-                {
-                    T sx[RX][4], su[RU][4];
-                    sums(2, sx, su);
-                    mmt(wq.fresh(), sx, g2);
-                    mmt(wr.fresh(), su, h2);
-                }
+                T sx[RX][4], su[RU][4];
+                sums(2, sx, su);
+                mmt(wq.fresh(), sx, g2);
+                mmt(wr.fresh(), su, h2);
                 _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
-                    if (tok<NX>(rt, e)) rs.account(xp[rt][e], xz[rt][e], g1[rt][e], g2[rt][e]);
+                    xch[(rt * 64 + lane) * 4 + e] = g2[rt][e];
                 _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
-                    if (tok<NU>(rt, e)) rs.account(up[rt][e], uz[rt][e], h1[rt][e], h2[rt][e]);
+                    xch[((RX + rt) * 64 + lane) * 4 + e] = h2[rt][e];
             }
         } else if (wv == C && live) {
             // ---------------- phase 5: the AVaR kernel projection of the family (cache.py:290-317)
@@ -1562,8 +1565,15 @@ __global__ void __launch_bounds__(128 * C) k_cp6(Dev p, Ctl* ctl, Bufs bf, doubl
             }
             if (h == 0) *elw(out, p.Y0 + yo + 2 * C) = y2c - sw;
         }
+        __syncthreads();  // the xi2 stream's L^T is in LDS
+        if (wv == 1) {
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) rs.account(xp[rt][e], xz[rt][e], g1[rt][e], xch[(rt * 64 + lane) * 4 + e]);
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NU>(rt, e)) rs.account(up[rt][e], uz[rt][e], h1[rt][e], xch[((RX + rt) * 64 + lane) * 4 + e]);
+        }
         stamp();
-        __syncthreads();  // the LDS rows and the scratch are the next tile's
+        __syncthreads();  // the LDS rows, the exchange and the scratch are the next tile's
     }
     flag_nan(ctl, nanf);
     block_maxima(part, rs);
