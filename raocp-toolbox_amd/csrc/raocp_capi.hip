@@ -2891,7 +2891,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             if (c->cp5) {
                 if (cp3_tasks(c->cp5_tk, {{c->cp3_mL, m}, {0, c->cp3_mL}}, 0, 0, 1, c->cp3_mL) < 0)
                     return bail(fail(RAOCP_ERR_ARG, "k_cp5 task list exceeds its parent-range slots"));
-                c->cp5_gl = raocp::cp5_leaf_grid(m, n);
+                c->cp5_gl = raocp::cp5_leaf_grid(m, n, c->f32);
                 // k_cp5_fams (profiles/r05/cp_time_fams*.log: config 4 100.7 -> 90.9 us, config 5
                 // 335.3 -> 334.8 us, config 3 60.9 -> 57.4 us with the compacted slot sums)
                 c->cp5_fams = true;

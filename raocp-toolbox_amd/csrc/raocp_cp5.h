@@ -13,8 +13,9 @@ bool cp5_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbo
 // the two kernels as rocprofv3 names them, "leaf x1 + fam x1"; fs: the family launch is
 // k_cp5_fams (a workgroup of C waves per tile), else k_cp5_fam (a wave per tile)
 const char* cp5_name(bool f32, int nx, int nu, int C, bool fs);
-// grids of the two launches for n leaves in [l0, l1) and the family task list tk
-int cp5_leaf_grid(int l0, int l1);
+// grids of the two launches for the leaves [l0, l1) (f32: the context's type; the leaf
+// launch's form depends on it) and the family task list tk
+int cp5_leaf_grid(int l0, int l1, bool f32);
 int cp5_fam_grid(const Cp3Tasks& tk, bool fs);
 // rows of residual partials the two launches write (one per workgroup; the family launch's
 // rows after the leaf launch's gl)

@@ -379,26 +379,62 @@ __global__ void __launch_bounds__(256, LPF ? 1 : 2) k_cp5_leaf(Dev p, Ctl* ctl, 
             *elw(eo, p.E12 + l) = ep12;
         }
         if (live && h == 1) *elw(eo, p.E13 + l) = ep13;
-        T eA[RX][4], eW[RX][4], eC[RX][4];
-        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-            T ep = T(0), x2 = T(0);
-            if (tok<NX>(rt, e)) rs.fin(cur.d11[rt][e], v11[rt][e], so.first(v11[rt][e]), lb[rt][e], ep, x2);
-            eA[rt][e] = ep;
-            eW[rt][e] = cur.d11[rt][e] - ep;
-            eC[rt][e] = x2;
+        if constexpr (LPF) {
+            T eA[RX][4], eW[RX][4], eC[RX][4];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                T ep = T(0), x2 = T(0);
+                if (tok<NX>(rt, e)) rs.fin(cur.d11[rt][e], v11[rt][e], so.first(v11[rt][e]), lb[rt][e], ep, x2);
+                eA[rt][e] = ep;
+                eW[rt][e] = cur.d11[rt][e] - ep;
+                eC[rt][e] = x2;
+            }
+            st_rows_o<T, NX>(eo, p.E11 + m + ((live ? l : m) - m) * NX, live, eA);
+            // L^T of the leaf rows: sqrtPf' (eta+, d - eta+, xi2) onto the box terms
+            mmt(wp.fresh(), eA, gA);
+            mmt(wp.fresh(), eW, gW);
+            mmt(wp.fresh(), eC, gC);
+            T ox[RX][4];
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                ox[rt][e] = cur.lz[rt][e] - alpha * gA[rt][e];
+                if (tok<NX>(rt, e)) rs.account(cur.lp[rt][e], cur.lz[rt][e], gW[rt][e], gC[rt][e]);
+            }
+            st_rows_o<T, NX>(out, p.X0 + (live ? l : 0) * NX, live, ox);
+            cur = nxt;
+        } else {
+            // two waves per SIMD: one L^T stream at a time, each stream's entries recomputed
+            // from (d11, v11, lb) and the SOC selects (the residual maxima taken in the first
+            // pass), so only one stream's rows are live at a time
+            {
+                T eA[RX][4];
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                    T ep = T(0), x2 = T(0);
+                    if (tok<NX>(rt, e)) rs.fin(cur.d11[rt][e], v11[rt][e], so.first(v11[rt][e]), lb[rt][e], ep, x2);
+                    eA[rt][e] = ep;
+                }
+                st_rows_o<T, NX>(eo, p.E11 + m + ((live ? l : m) - m) * NX, live, eA);
+                mmt(wp.fresh(), eA, gA);
+                T ox[RX][4];
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                    ox[rt][e] = cur.lz[rt][e] - alpha * gA[rt][e];
+                st_rows_o<T, NX>(out, p.X0 + (live ? l : 0) * NX, live, ox);
+            }
+            {
+                T eW[RX][4];
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                    eW[rt][e] = tok<NX>(rt, e) ? cur.d11[rt][e] - alpha * (v11[rt][e] - so.first(v11[rt][e])) : T(0);
+                mmt(wp.fresh(), eW, gW);
+            }
+            {
+                T eC[RX][4];
+                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                    const T ep = alpha * (v11[rt][e] - so.first(v11[rt][e]));
+                    eC[rt][e] = tok<NX>(rt, e) ? (cur.d11[rt][e] - ep) * ra + lb[rt][e] : T(0);
+                }
+                mmt(wp.fresh(), eC, gC);
+            }
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) rs.account(cur.lp[rt][e], cur.lz[rt][e], gW[rt][e], gC[rt][e]);
         }
-        st_rows_o<T, NX>(eo, p.E11 + m + ((live ? l : m) - m) * NX, live, eA);
-        // L^T of the leaf rows: sqrtPf' (eta+, d - eta+, xi2) onto the box terms
-        mmt(wp.fresh(), eA, gA);
-        mmt(wp.fresh(), eW, gW);
-        mmt(wp.fresh(), eC, gC);
-        T ox[RX][4];
-        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-            ox[rt][e] = cur.lz[rt][e] - alpha * gA[rt][e];
-            if (tok<NX>(rt, e)) rs.account(cur.lp[rt][e], cur.lz[rt][e], gW[rt][e], gC[rt][e]);
-        }
-        st_rows_o<T, NX>(out, p.X0 + (live ? l : 0) * NX, live, ox);
-        if (LPF) cur = nxt;
     }
     flag_nan(ctl, nanf);
     block_maxima(part, rs);
@@ -1603,12 +1639,15 @@ int resident_grid(long tasks, int per) {
 
 // k_cp5_leaf's form (RAOCP_CP5_LPF): 1 = one wave per SIMD with the next tile's operands in
 // flight (register double buffering), 0 = two waves per SIMD, a tile's operands at its start
-bool leaf_pf() {
+// and one L^T stream at a time. Default: 0 in fp64 (config 3 56.3 -> 53.2 us, config 4
+// 91.3 -> 89.7 us for the CP iteration), 1 in fp32 (config 5 327.8 vs 333.0 us;
+// profiles/r05/cp_time_lpf.log)
+bool leaf_pf(bool f32) {
     static const int v = [] {
         const char* e = getenv("RAOCP_CP5_LPF");
-        return e ? atoi(e) : 1;
+        return e ? atoi(e) : -1;
     }();
-    return v != 0;
+    return v < 0 ? f32 : v != 0;
 }
 
 template <class T, int NX, int NU, int C>
@@ -1620,7 +1659,7 @@ void launch_t(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, int l0, int
         const char* e = getenv("RAOCP_CP5_FPF");
         return e ? atoi(e) != 0 : false;
     }();
-    const bool lpf = leaf_pf();
+    const bool lpf = leaf_pf(sizeof(T) == 4);
     if (fs) {
         if (lpf) {
             if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
@@ -1670,9 +1709,9 @@ const char* cp5_name(bool f32, int nx, int nu, int C, bool fs) {
 }
 // persistent grids (every workgroup resident, one wave per SIMD): a wave's tiles stream behind
 // each other; at most one workgroup per CU
-int cp5_leaf_grid(int l0, int l1) {
+int cp5_leaf_grid(int l0, int l1, bool f32) {
     const long tasks = (long)(std::max(l1 - l0, 0) + 15) / 16 + (l0 + 63) / 64;
-    return (leaf_pf() ? 1 : 2) * resident_grid(tasks, 2);  // two workgroups per CU without the prefetch
+    return (leaf_pf(f32) ? 1 : 2) * resident_grid(tasks, 2);  // two workgroups per CU without the prefetch
 }
 // rows of residual partials of the two launches (one per workgroup)
 int cp5_rows(int gl, int gf, bool fs, int C) {

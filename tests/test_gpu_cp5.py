@@ -222,3 +222,25 @@ def test_cp5_slot_parallel_family_matches_wave_family(case):
     assert trace_rel_err(ra[1], rb[1]) <= tol and trace_rel_err(ra[2], rb[2]) <= tol
     assert rel_err(ra[3], rb[3]) <= tol and rel_err(ra[4], rb[4]) <= tol
     print(f"{case}: bit-identical {all(np.array_equal(u, v) for u, v in zip(ra, rb))}")
+
+
+@pytest.mark.parametrize("case", ["q20", "t32", "c4", "q64"])
+def test_cp5_leaf_forms_agree(case):
+    """k_cp5_leaf's two forms (RAOCP_CP5_LPF: 1 = one wave per SIMD with the next tile's
+    operands in registers, 0 = two waves per SIMD with one L^T stream at a time, its entries
+    recomputed; fp64 default 0, fp32 default 1) differ in FMA contraction only: 1e-12 on the
+    traces and the iterate (fp32: 1e-5)."""
+    r = _recipe(case)
+    tree, prob = build_problem(r)
+    dt = "float32" if case == "q64" else None
+    mk = (lambda: core.Cache(prob, dtype=dt)) if dt else (lambda: core.Cache(prob))
+    a = _with_env({"RAOCP_CP5_LPF": "1"}, mk)
+    b = _with_env({"RAOCP_CP5_LPF": "0"}, mk)
+    alpha = 0.999 / a.native.step_size(rtol=1e-7 if dt else 1e-14)
+    K = 14 if case == "c4" else 30
+    ra = _run(a, r["x0"], K, alpha)
+    rb = _run(b, r["x0"], K, alpha)
+    tol = 1e-5 if dt else 1e-12
+    assert ra[0] == rb[0] == 1
+    assert trace_rel_err(ra[1], rb[1]) <= tol and trace_rel_err(ra[2], rb[2]) <= tol
+    assert rel_err(ra[3], rb[3]) <= tol and rel_err(ra[4], rb[4]) <= tol
