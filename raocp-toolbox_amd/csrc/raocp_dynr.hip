@@ -117,30 +117,15 @@ struct Dma {
 // second context's stream) can break; a workgroup that is never scheduled turns into the
 // bounded wait's RAOCP_ERR_STATE, not a hang
 //
-// The wait itself is one wave's: its lanes poll the last granule of each of the rows rows
-// (sleeping between rounds) while the other waves sit at the barrier; then every lane reads
-// its granules (normally all there) and re-polls only the missing ones.
-__device__ __forceinline__ bool poll_gran(const unsigned long long* src, int n, int rows, unsigned tag, ldsu* dst,
+// Every lane polls its own granules from the start and keeps the ones that carry the tag, so
+// the payload is read once, as soon as it is there (round 4 had one wave wait for the last
+// granule of each row first and then every lane read its granules: one more dependent round
+// trip per hand-off, 1.0 us more per projection at config 2, profiles/r05/dr_poll.log).
+__device__ __forceinline__ bool poll_gran(const unsigned long long* src, int n, unsigned tag, ldsu* dst,
                                           long long timeout, unsigned* sync, int& s_ok) {
-    const int tid = threadIdx.x, bs = blockDim.x, G = n / rows;
+    const int tid = threadIdx.x, bs = blockDim.x;
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     bool bad = false;
-    if (tid < 64) {
-        for (int r0 = 0; r0 < rows && !bad; r0 += 64) {
-            const int r = r0 + tid;
-            for (;;) {
-                const bool ok = r >= rows || (unsigned)(ld_gran(src + (size_t)r * G + G - 1) >> 32) == tag;
-                if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
-                // another workgroup's timeout (the error word): this wait cannot complete either
-                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout || ld_u32(sync + 1) != 0u) {
-                    bad = true;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(4);
-            }
-        }
-    }
-    __syncthreads();
     unsigned got = 0;
     for (;;) {
         unsigned long long v[kDrMaxGran];
@@ -160,7 +145,8 @@ __device__ __forceinline__ bool poll_gran(const unsigned long long* src, int n, 
                 }
             }
         }
-        if (all || bad) break;
+        if (all) break;
+        // another workgroup's timeout (the error word): this wait cannot complete either
         if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > timeout || ld_u32(sync + 1) != 0u) {
             bad = true;
             break;
@@ -191,6 +177,12 @@ __device__ __forceinline__ void stamp(const DrPlan& pl, Stamps& s) {
         if (s.n == 0) s.c0 = __builtin_amdgcn_s_memtime();
         s.ts[s.n++] = __builtin_amdgcn_s_memrealtime();
     }
+}
+// every workgroup (diagnostics, tools/dr_skew.py): slots 1024 + 3 b + {0 start, 1 backward
+// sweep done, 2 end}
+__device__ __forceinline__ void wg_stamp(const DrPlan& pl, int q) {
+    if (kDiag && pl.stamps && threadIdx.x == 0)
+        pl.stamps[1024 + 3 * blockIdx.x + q] = __builtin_amdgcn_s_memrealtime();
 }
 // slots [32 k, 32 k + 30): the stamps; 32 k + 30: the end; 32 k + 31: cycles from the first
 // stamp to the end
@@ -392,7 +384,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     // ---- 2. the child subtrees' q rows
     if (!deepest) {
         const DrTier& ct = pl.t[k + 1];
-        if (!poll_gran(pl.gq + (size_t)(ct.w0 + o * NB) * G, NB * G, NB, tag, (ldsu*)XL, pl.timeout, pl.sync, s_ok)) {
+        if (!poll_gran(pl.gq + (size_t)(ct.w0 + o * NB) * G, NB * G, tag, (ldsu*)XL, pl.timeout, pl.sync, s_ok)) {
             dma_wait();
             return;
         }
@@ -417,6 +409,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     });
     lds_sync();
     stamp(pl, stp);
+    wg_stamp(pl, 1);
     // ---- 4./5. the root's q row up, its x row down (below the top the forward tables load
     // during that wait; the top issued them as its backward sweep freed the slots)
     if (top && !(kDiag && (pl.fault & 4))) TF::issue(SL, pl.fimg + (size_t)(s0 + L - 1) * TFN);
@@ -427,7 +420,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
                 constexpr int f = fc.value;
                 TF::issue(SL + (L - 1 - f) * SLOT, pl.fimg + (size_t)(s0 + f) * TFN);
             });
-        if (!poll_gran(pl.gx + (size_t)(tt.w0 + o) * G, G, 1, tag, (ldsu*)XD, pl.timeout, pl.sync, s_ok)) {
+        if (!poll_gran(pl.gx + (size_t)(tt.w0 + o) * G, G, tag, (ldsu*)XD, pl.timeout, pl.sync, s_ok)) {
             dma_wait();
             return;
         }
@@ -500,6 +493,7 @@ k_dr(DrPlan pl, Bufs bf, int zsel, const Ctl* ctl, ChkArg ck) {
     const unsigned tag = (unsigned)sw + 1u;
     const int done = ctl ? ctl->done : 0;
     stamp(pl, stp);
+    wg_stamp(pl, 0);
     if (err) return;
     int k, o;
     role(pl, k, o);
@@ -514,6 +508,7 @@ k_dr(DrPlan pl, Bufs bf, int zsel, const Ctl* ctl, ChkArg ck) {
     });
     stamp(pl, stp);
     stamp_flush(pl, stp, k, o);
+    wg_stamp(pl, 2);
 }
 
 template <int NX, int NU, int C, int LMAX>
