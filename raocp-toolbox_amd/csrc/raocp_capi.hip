@@ -458,7 +458,11 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
     const int thr = lmax > 64 * 1024 ? 512 : 256, wpb = thr / 64;
     // (1,024-lane workgroups for the wide stages when the tables allow one workgroup per CU
     // measured slower at config 5: 215.3 vs 190.9 us per projection, profiles/r03_v3)
-    const int thr_w = thr, wpb_w = thr_w / 64;
+    // the wide stages (a wave per tile, looping) in 256-lane workgroups: at config 5 (one
+    // workgroup per CU by LDS) 4 waves of 4 tiles each beat 8 waves of 2 (projection 197.1 ->
+    // 191.9 us); at least 2 tiles per wave measured slower at configs 4 and 5 (fewer waves in
+    // flight: 113.6 -> 123.1, 197.1 -> 217.9 us; profiles/r05/dy3_geometry.log)
+    const int thr_w = 256, wpb_w = thr_w / 64;
     const int per_cu = std::max<int>(1, std::min<int>(2048 / thr_w, (int)(160 * 1024 / lmax)));
     const int cap = 256 * per_cu;  // one round of resident workgroups; waves loop over tiles
     auto kb = raocp::k_dy3_back<T, NX, NU>;
