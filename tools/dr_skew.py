@@ -34,5 +34,8 @@ for rep in range(reps):
                       for i, q in enumerate(("start", "bwd", "end")))
         print(f"rep {rep} {name:4s}: {d}", flush=True)
     print(f"rep {rep} bwd done of deep 0..15: " + " ".join(f"{x:5d}" for x in w[0:16, 1]), flush=True)
+    # by XCD (block b on XCD b mod 8 under the round-robin dispatch): median start and backward done of the deep tier
+    print(f"rep {rep} deep by b mod 8 (median start / bwd): " + "  ".join(
+        f"{x}: {int(np.median(w[x:256:8, 0]))}/{int(np.median(w[x:256:8, 1]))}" for x in range(8)), flush=True)
     print(f"rep {rep} bwd done of deep by 16s (max): " +
           " ".join(f"{x:5d}" for x in w[0:256, 1].reshape(16, 16).max(axis=1)), flush=True)
