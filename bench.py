@@ -92,11 +92,14 @@ def kernel_bytes(cache, w=8):
     output written once, tables excluded. The CP iteration after the dynamics sweep:
     the fused k_cp3 reads p, z+, d and writes eta+ and the next half step (3|P| + 2|D|);
     the two-launch k_cpd* + k_cpp* also write and re-read xi2 and re-read p, z+, d
-    (5|P| + 6|D|). The dynamics projection reads and writes x, u."""
+    (5|P| + 6|D|). The dynamics projection reads and writes x, u. The one
+    launch of both (k_drc) reads the half step's x, u and writes the projected x+, u+, then
+    runs the CP iteration with x+, u+ from LDS: 3|P| + 2|D| + (n nx + m nu)."""
     P, D = active_sizes(cache)
     pk = cache.packed
+    xu = pk.n * pk.nx + pk.m * pk.nu
     return {"cp_fused": w * (3 * P + 2 * D), "cp_two": w * (5 * P + 6 * D),
-            "dynamics": w * 2 * (pk.n * pk.nx + pk.m * pk.nu), "L": w * (P + D)}
+            "dynamics": w * 2 * xu, "dyn_cp": w * (3 * P + 2 * D + xu), "L": w * (P + D)}
 
 
 def pmc_traffic(kernel):
@@ -369,16 +372,22 @@ def iteration_kernels(nat, cache, w, reps, dev_ms_per_step):
     k_cpd* + k_cpp*); kernel names from the library's own selection (raocp_kernel_info).
     The roofline names the part with the larger device time per iteration."""
     kb = kernel_bytes(cache, w)
-    name_cp, name_dyn = nat.kernel_info(10), nat.kernel_info(9)
+    name_cp, name_dyn, name_one = nat.kernel_info(10), nat.kernel_info(9), nat.kernel_info(11)
     fused = name_cp.startswith(("k_cp3", "k_cp4", "k_cp5", "k_cp6"))
     t_cp = 1e3 * nat.op_bench(10, reps)
     t_dyn = 1e3 * nat.op_bench(9, max(1, reps // 4))
-    kernels = {"cp": dict(_rate(kb["cp_fused" if fused else "cp_two"], t_cp), kernel=name_cp, in_cp_iteration=True),
-               "dynamics": dict(_rate(kb["dynamics"], t_dyn), kernel=name_dyn, in_cp_iteration=True)}
+    # with a one-launch iteration (k_drc) the loop runs neither standalone part: they are
+    # reported beside it (the RAOCP_DRC=0 loop's kernels), the roofline is the one launch's
+    kernels = {"cp": dict(_rate(kb["cp_fused" if fused else "cp_two"], t_cp), kernel=name_cp,
+                          in_cp_iteration=not name_one),
+               "dynamics": dict(_rate(kb["dynamics"], t_dyn), kernel=name_dyn, in_cp_iteration=not name_one)}
+    if name_one:
+        t_one = 1e3 * nat.op_bench(11, reps)
+        kernels["dynamics_cp"] = dict(_rate(kb["dyn_cp"], t_one), kernel=name_one, in_cp_iteration=True)
     dev_us = 1e3 * dev_ms_per_step
     for k in kernels.values():
-        k["share_of_step"] = k["us_per_launch"] / dev_us if dev_us > 0 else None
-    dom = max(kernels, key=lambda k: kernels[k]["us_per_launch"])
+        k["share_of_step"] = k["us_per_launch"] / dev_us if dev_us > 0 and k["in_cp_iteration"] else None
+    dom = max((k for k in kernels if kernels[k]["in_cp_iteration"]), key=lambda k: kernels[k]["us_per_launch"])
     traffic, src = pmc_traffic(kernels[dom]["kernel"])
     roofline = {"bound": "hbm", "kernel": kernels[dom]["kernel"], "part": dom, "achieved": kernels[dom]["achieved"],
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": kernels[dom]["frac"], "traffic": traffic,

@@ -130,7 +130,10 @@ int raocp_set_initial_state(raocp_ctx* ctx, const double* x0);
 int raocp_reset_iterate(raocp_ctx* ctx);
 /* Name of the kernel the context's default selection launches for `op` (raocp_op_bench
  * numbering: 0 L, 1 L^T, 2 dual CP kernel, 6 primal CP kernel, 9 dynamics projection,
- * 10 fused CP iteration), as rocprofv3 reports it; written NUL-terminated to buf. */
+ * 10 fused CP iteration, 11 the CP loop's one launch of dynamics projection + CP iteration
+ * (k_drc; "" when the loop runs 9 and 10 as separate launches)), as rocprofv3 reports it;
+ * op 12: the forms of the k_cp5 launches ("leaf_pf=. fams=. fam_pf=.", "" when k_cp5 does not
+ * run); written NUL-terminated to buf. */
 int raocp_kernel_info(raocp_ctx* ctx, int op, char* buf, int cap);
 
 /* prox of f on the current primal (Cache.proximal_of_f, cache.py:248-257) and its steps */

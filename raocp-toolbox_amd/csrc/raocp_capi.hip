@@ -75,6 +75,8 @@ struct raocp_ctx {
     int cp6_grid = 0;
     raocp::Cp3Tasks cp5_tk{};    // k_cp5_fam's / k_cp6's task list (every parent, leaf parents first)
     int cp5_gl = 0, cp5_gf = 0;  // grids of the two launches
+    bool cp5_lpf = false;        // k_cp5_leaf's form (RAOCP_CP5_LPF, raocp_cp5.h)
+    bool cp5_fpf = false;        // k_cp5_fam with the next tile in registers (RAOCP_CP5_FPF; spills, diagnostics)
     int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
     int cp3_split = 0;           // leaves as tasks of their own (small trees: more waves, shorter chains)
@@ -148,6 +150,13 @@ struct raocp_ctx {
     raocp::DrPlan drp{};
     int dr_block = 512;
     size_t dr_lds = 0;
+    // k_drc (raocp_dynr.hip): k_dr with each subtree's CP families fused behind its forward
+    // sweep, one launch per CP iteration (config 2: binary, 20 / 8, fp64, tiers of 4 levels, the
+    // k_cp6 box patterns); RAOCP_DRC=0 keeps k_dr + k_cp6. Its residual rows alternate between two
+    // sets of cp_rows rows (the extra workgroup tests the previous iteration beside the next)
+    bool drc = false;
+    raocp::DrcArg drca{};
+    size_t drc_lds = 0;
     size_t dr_gran = 0;  // granules of each hand-off buffer
     double* x0 = nullptr;
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
@@ -1012,7 +1021,8 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
     // error-path test (tests/test_gpu_dynr.py): RAOCP_DR_FAULT=1 makes the deepest tier's first
     // subtree skip its publish, so its parent's wait times out and the call fails; the
     // timing-only bits (no DMA / arithmetic / write-out) exist in diagnostic builds only
-    if (const char* e = getenv("RAOCP_DR_FAULT")) p.fault = atoi(e) & (raocp::kDiag ? ~0 : 1);
+    // (the timing bits pass where the sweep's unit is a diagnostic build: VAR_UNIT=dynr variants)
+    if (const char* e = getenv("RAOCP_DR_FAULT")) p.fault = atoi(e) & ((raocp::kDiag || raocp::dr_diag_build()) ? ~0 : 1);
     int rc;
     const double *bi = nullptr, *fi = nullptr;
     unsigned long long *gq = nullptr, *gx = nullptr;
@@ -1041,6 +1051,69 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
         fprintf(stderr, "; %d lanes, LDS %zu B, occupancy %d\n", c->dr_block, c->dr_lds,
                 raocp::dr_occupancy(nx, nu, C, lmax, c->dr_lds));
     }
+    return RAOCP_OK;
+}
+
+// k_drc (raocp_dynr.hip): where k_dr and k_cp6 both run and every tier of the plan has 4 levels
+// (binary trees, 20 / 8, fp64, every node boxed or none), the fused launch replaces the pair;
+// RAOCP_DRC=0 keeps them. Its weight image is k_cp3's [sqrtQ | sqrtR | sqrtPf] followed by the
+// one box table of each kind [lo_nl | hi_nl | lo_l | hi_l] (zeros when unboxed); its residual rows
+// are two sets of one row per sweep workgroup (drc_part).
+int drc_setup(raocp_ctx* c) {
+    c->drc = false;
+    if (!c->dr || !c->cp6 || c->f32 || c->sh_S > 0 || !raocp::drc_supported(c->nx, c->nu, c->reg_C)) return RAOCP_OK;
+    if (const char* e = getenv("RAOCP_DRC"))
+        if (!atoi(e)) return RAOCP_OK;
+    const raocp::DrPlan& p = c->drp;
+    for (int k = 0; k < p.T; ++k)
+        if (p.t[k].L != 4) return RAOCP_OK;
+    const int bx = c->box_mode;
+    if (bx != 5 && bx != 10) return RAOCP_OK;
+    const size_t lds = raocp::drc_lds(c->nx, c->nu, 2);
+    int n_cus = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cus <= 0)
+        n_cus = 256;
+    const int occ = raocp::drc_occupancy(lds);
+    if (occ < 1 || (long)p.nblk + 1 > (long)occ * n_cus) return RAOCP_OK;  // the grid must be resident
+    const int nx = c->nx, nu = c->nu, R = nx + nu;
+    const size_t nimg = raocp::kDrcWa + raocp::kDrcWb;
+    double* img = nullptr;
+    int rc;
+    if ((rc = c->alloc(&img, nimg))) return rc;
+    HIPCHK(hipMemset(img, 0, nimg * sizeof(double)));
+    HIPCHK(hipMemcpy(img, c->cp3img, (size_t)(raocp::kDrcWa + 640) * sizeof(double), hipMemcpyDeviceToDevice));
+    if ((bx & 3) == 1) {
+        double* bx0 = img + raocp::kDrcWa + 640;
+        HIPCHK(hipMemcpy(bx0, c->dev.blo_nl, R * sizeof(double), hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(bx0 + R, c->dev.bhi_nl, R * sizeof(double), hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(bx0 + 2 * R, c->dev.blo_l, nx * sizeof(double), hipMemcpyDeviceToDevice));
+        HIPCHK(hipMemcpy(bx0 + 2 * R + nx, c->dev.bhi_l, nx * sizeof(double), hipMemcpyDeviceToDevice));
+    }
+    const int rows = p.nblk;
+    if (2 * rows > c->red_rows) {
+        c->red_rows = 2 * rows;
+        if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return rc;
+        HIPCHK(hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)));
+    }
+    c->cp_rows = rows;
+    raocp::DrcArg& a = c->drca;
+    const raocp::Dev& D = c->dev;
+    a = raocp::DrcArg{};
+    a.m = c->m;
+    a.Y0 = D.Y0;
+    a.T0 = D.T0;
+    a.S0 = D.S0;
+    a.E1 = D.E1; a.E2 = D.E2; a.E3 = D.E3; a.E4 = D.E4; a.E5 = D.E5; a.E6 = D.E6; a.E7 = D.E7;
+    a.E11 = D.E11; a.E12 = D.E12; a.E13 = D.E13; a.E14 = D.E14;
+    a.cond = D.cond;
+    a.alpha_r = D.alpha_r;
+    a.blo_nl = D.blo_nl; a.bhi_nl = D.bhi_nl; a.blo_l = D.blo_l; a.bhi_l = D.bhi_l;
+    a.img = img;
+    a.ctl = c->ctl;
+    a.box = (bx & 3) == 1 ? 1 : 2;
+    c->drc_lds = lds;
+    c->drc = true;
     return RAOCP_OK;
 }
 
@@ -1224,7 +1297,7 @@ void launch_cp3(raocp_ctx* c, int part = 0) {
     }
     if (c->cp5 && c->sh_S == 0) {
         raocp::cp5_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->m, c->n, c->cp5_gl, c->cp5_tk,
-                          c->cp5_gf, c->cp3img, c->cp5_fams, c->stream);
+                          c->cp5_gf, c->cp3img, c->cp5_fams, c->cp5_lpf, c->cp5_fpf, c->stream);
         return;
     }
     if (c->cp4 && c->sh_S == 0) {
@@ -1390,6 +1463,19 @@ int enqueue_shard_tail(raocp_ctx* c) {
 }
 
 // returns the first failure of an RCCL call (launch errors surface at the next sync)
+// k_drc's residual rows of iteration parity q, and the ctl->flags bit of its NaN-in-box flag
+double* drc_part(raocp_ctx* c, int q) { return c->redpart + (size_t)(q & 1) * c->cp_rows * 6; }
+int drc_nanbit(int q) { return 2 << (q & 1); }
+// the fused launch of iteration `it` (k = it mod 2 within a batch that starts at k = 0 mod 6)
+void launch_drc(raocp_ctx* c, int it, bool with_check) {
+    raocp::DrcArg a = c->drca;
+    a.part = drc_part(c, it);
+    a.nanbit = drc_nanbit(it);
+    raocp::DrPlan p = c->drp;
+    if (c->dev.stamps) p.stamps = c->dev.stamps;
+    const raocp::ChkArg ck{c->ctl, c->hist, drc_part(c, it - 1), c->cp_rows, with_check ? 1 : 0, drc_nanbit(it - 1)};
+    raocp::drc_launch(p, a, c->drc_lds, c->bufs, c->ctl, ck, c->stream);
+}
 int enqueue_cp_iteration(raocp_ctx* c, int it) {
     const raocp::Bufs keep = c->bufs;
     c->bufs = rotated(c, it);
@@ -1399,6 +1485,13 @@ int enqueue_cp_iteration(raocp_ctx* c, int it) {
         return rc;
     }
     const bool defer = defer_check(c);
+    if (c->drc && c->sh_S == 0) {
+        launch_drc(c, it, defer && it > 0);
+        c->bufs = keep;
+        if (!defer)
+            raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, drc_part(c, it), c->cp_rows, drc_nanbit(it));
+        return RAOCP_OK;
+    }
     const raocp::ChkArg ck{c->ctl, c->hist, c->redpart, c->cp_rows, 1};
     launch_dynamics(c, c->bufs, 1, c->ctl, 0, defer && it > 0 ? &ck : nullptr);
     if (c->cp3) {
@@ -1408,7 +1501,7 @@ int enqueue_cp_iteration(raocp_ctx* c, int it) {
         launch_cpp(c);
     }
     c->bufs = keep;
-    if (!defer) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
+    if (!defer) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0);
     return RAOCP_OK;
 }
 // the kernel the default selection launches for op (raocp_op_bench numbering: 0 L, 1 L^T,
@@ -1473,6 +1566,12 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             for (const auto& t : terms) s += (s.empty() ? "" : " + ") + t.first + " x" + std::to_string(t.second);
             return s;
         }
+        case 11:  // the CP loop's fused launch (dynamics projection + CP iteration), if any
+            return c->drc && c->sh_S == 0 ? raocp::drc_name() : "";
+        case 12:  // the forms of the k_cp5 launches, when they run ("" otherwise)
+            if (!(c->cp5 && c->sh_S == 0)) return "";
+            return std::string("leaf_pf=") + (c->cp5_lpf ? "1" : "0") + " fams=" + (c->cp5_fams ? "1" : "0") +
+                   " fam_pf=" + (c->cp5_fpf ? "1" : "0");
         case 10:
             if (c->cp6 && c->sh_S == 0) return raocp::cp6_name();
             if (c->cp5 && c->sh_S == 0) return raocp::cp5_name(c->f32, c->nx, c->nu, c->unif_C, c->cp5_fams);
@@ -1483,9 +1582,14 @@ std::string kernel_name(const raocp_ctx* c, int op) {
     }
 }
 
-// the end of a batch: the deferred test of its last iteration
-void enqueue_batch_tail(raocp_ctx* c) {
-    if (defer_check(c)) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
+// the end of a batch of `iters` iterations: the deferred test of its last iteration
+void enqueue_batch_tail(raocp_ctx* c, int iters) {
+    if (!defer_check(c)) return;
+    if (c->drc && c->sh_S == 0)
+        raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, drc_part(c, iters - 1), c->cp_rows,
+                                                       drc_nanbit(iters - 1));
+    else
+        raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0);
 }
 
 
@@ -1576,7 +1680,7 @@ int ensure_graph(raocp_ctx* c, int iters) {
     HIPCHK(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
     int rc_enq = RAOCP_OK;
     for (int it = 0; it < iters && rc_enq == RAOCP_OK; ++it) rc_enq = enqueue_cp_iteration(c, it);
-    if (rc_enq == RAOCP_OK) enqueue_batch_tail(c);
+    if (rc_enq == RAOCP_OK) enqueue_batch_tail(c, iters);
     hipError_t e = hipStreamEndCapture(c->stream, &g);
     if (rc_enq != RAOCP_OK) {
         if (g) (void)hipGraphDestroy(g);
@@ -1611,7 +1715,7 @@ int launch_batch(raocp_ctx* c, int iters) {
             const int rc = enqueue_cp_iteration(c, it);
             if (rc) return rc;
         }
-        enqueue_batch_tail(c);
+        enqueue_batch_tail(c, iters);
         HIPCHK(hipGetLastError());
         return RAOCP_OK;
     }
@@ -2895,7 +2999,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             if (c->cp5) {
                 if (cp3_tasks(c->cp5_tk, {{c->cp3_mL, m}, {0, c->cp3_mL}}, 0, 0, 1, c->cp3_mL) < 0)
                     return bail(fail(RAOCP_ERR_ARG, "k_cp5 task list exceeds its parent-range slots"));
-                c->cp5_gl = raocp::cp5_leaf_grid(m, n, c->f32);
+                // the leaf launch's form is read here, per context (a later context with another
+                // RAOCP_CP5_LPF gets its own)
+                c->cp5_lpf = raocp::cp5_leaf_pf_default(c->f32);
+                if (const char* e = getenv("RAOCP_CP5_LPF")) c->cp5_lpf = atoi(e) != 0;
+                if (const char* e = getenv("RAOCP_CP5_FPF")) c->cp5_fpf = atoi(e) != 0;
+                c->cp5_gl = raocp::cp5_leaf_grid(m, n, c->cp5_lpf);
                 // k_cp5_fams (profiles/r05/cp_time_fams*.log: config 4 100.7 -> 90.9 us, config 5
                 // 335.3 -> 334.8 us, config 3 60.9 -> 57.4 us with the compacted slot sums)
                 c->cp5_fams = true;
@@ -2913,6 +3022,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             }
         }
     }
+    if ((rc = drc_setup(c))) return bail(rc);
     c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics (diagnostic builds only)
     if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = raocp::kDiag ? atoi(e) : 0;
     if (const char* e = getenv("RAOCP_DEFER_CHECK")) c->no_defer_check = atoi(e) == 0;
@@ -3017,7 +3127,7 @@ int raocp_kernel_info(raocp_ctx* c, int op, char* buf, int cap) {
     DevGuard dg_(c);
     if (!c || !buf || cap < 1) return fail(RAOCP_ERR_ARG, "bad argument");
     const std::string s = kernel_name(c, op);
-    if (s.empty()) return fail(RAOCP_ERR_ARG, "unknown op " + std::to_string(op));
+    if (s.empty() && op != 11 && op != 12) return fail(RAOCP_ERR_ARG, "unknown op " + std::to_string(op));
     snprintf(buf, (size_t)cap, "%s", s.c_str());
     return RAOCP_OK;
 }
@@ -3355,9 +3465,15 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
 // `cap` raw 100 MHz timestamps.
 int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
     DevGuard dg_(c);
-    if (!raocp::kDiag) return fail(RAOCP_ERR_ARG, "in-kernel stamps need a diagnostic build (make DIAG=1)");
+    // the regular-tree sweeps' stamps need only their own unit built with them (VAR_UNIT=dynr)
+    if (!raocp::kDiag && !(c && c->dr && raocp::dr_diag_build()))
+        return fail(RAOCP_ERR_ARG, "in-kernel stamps need a diagnostic build (make DIAG=1)");
     if (c && c->f32) return fail(RAOCP_ERR_ARG, "not available on an fp32 context (the CP loop and L / L^T are)");
     if (!c || !out || cap <= 0) return fail(RAOCP_ERR_ARG, "bad argument");
+    // k_dr / k_drc stamp 4 slots per workgroup from slot 1024 (raocp_dynr.hip wg_stamp) and
+    // k_drc's CP waves 128 slots from 3072
+    if (c->dr && (size_t)cap < std::max(c->drc ? (size_t)3072 + 128 : (size_t)0, 1024 + 4 * ((size_t)c->drp.nblk + 1)))
+        return fail(RAOCP_ERR_ARG, "stamp buffer too small for the regular-tree sweep's workgroup stamps");
     // the tiered sweep stamps 64 slots per launch (2 per tier + the top)
     if (c->cut > 0 && (size_t)cap < 64 * (2 * c->tiers.size() + 1))
         return fail(RAOCP_ERR_ARG, "stamp buffer too small: 64 slots per dynamics launch");
@@ -3380,6 +3496,15 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
         int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
         if (rc2) return rc2;
         launch_cp3(c);
+    } else if (which && which[0] == 'f') {  // the fused dynamics + CP launch (k_drc) on a valid control block
+        if (!c->drc) return fail(RAOCP_ERR_ARG, "no fused dynamics + CP launch on this context");
+        std::vector<double> x0(c->nx, 0.0);
+        int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
+        if (rc2) return rc2;
+        const raocp::Bufs keep = c->bufs;
+        c->bufs = rotated(c, 0);
+        launch_drc(c, 0, false);
+        c->bufs = keep;
     } else if (which && which[0] == 'l') {  // k_ell on the staging buffers
         launch_ell(c, c->tmpP, c->tmpD);
     } else if (which && which[0] == 't') {  // k_ell_t
@@ -3658,7 +3783,8 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
                     launch_cpp(c);
                 }
                 break;
-            default: raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows);
+            case 11: launch_drc(c, 0, false); break;  // the fused dynamics + CP launch (k_drc)
+            default: raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0);
         }
     };
     for (int i = 0; i < 3; ++i) run();  // warm-up

@@ -42,6 +42,12 @@ struct ChkArg {
     const double* part;
     int rows;
     int on;
+    // 0, or the ctl->flags bit that the iteration being tested raised for a NaN in a box: a CP
+    // kernel that may run beside the test of the iteration before it (k_drc: the next
+    // iteration's CP step is in the launch whose extra workgroup runs this test) raises bit
+    // 2 << (k % 2) instead of bit 0, and the test of iteration k moves it to bit 0 (the flag
+    // the host reports) only for its own k
+    int nanbit;
 };
 
 // explicit address spaces: loads through these types are ds_read / global_load, never flat
@@ -158,6 +164,7 @@ __device__ __forceinline__ void cp_check_wave(const ChkArg& ck) {
     const int k = ctl->k;
     for (int q = 0; q < 6; ++q) ck.hist[(size_t)k * 6 + q] = m[q];
     const double err = nmax(nmax(m[0], m[1]), m[2]);
+    if (ctl->flags & ck.nanbit) ctl->flags |= 1;
     if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
         ctl->done = 1;
         ctl->final_k = k;

@@ -42,7 +42,9 @@ struct DrPlan {
     int fault;                // error-path test: bit 0 the deepest tier's subtree 0 never publishes
                               // (the wait times out, the call fails with RAOCP_ERR_STATE); timing
                               // only, diagnostic builds (kDiag) only: bit 2 no table DMAs, bit 3 no
-                              // write-out, bit 4 no level arithmetic, bit 5 no row DMAs
+                              // write-out, bit 4 no level arithmetic, bit 5 no row DMAs; k_drc: bit 6
+                              // no CP step, bit 7 no CP operand gather, bit 9 the CP step alone (no
+                              // sweep, no hand-offs: the epoch does not advance)
 };
 
 // split-k lanes per backward output row: one per child slot, a power of two
@@ -78,5 +80,44 @@ void dr_launch(const DrPlan& pl, int nx, int nu, size_t lds, Bufs bf, int zsel, 
                hipStream_t s);
 // kernel name for raocp_kernel_info
 const char* dr_name(int nx, int nu);
+
+// ---- k_drc: the sweep with the CP iteration of each subtree's families fused behind its forward
+// sweep (one launch per CP iteration, config 2: fp64, nx = 20, nu = 8, C = 2, every tier of L = 4
+// levels). Kernel argument beside the plan: the CP operands' offsets and tables.
+struct DrcArg {
+    int m;                    // nonleaf nodes (the first leaf)
+    int Y0, T0, S0;           // primal offsets of y, tau, s (x, u: DrPlan::X0 / U0)
+    int E1, E2, E3, E4, E5, E6, E7, E11, E12, E13, E14;  // dual offsets (Dev)
+    const double* cond;       // conditional probabilities, child j at [j]
+    const double* alpha_r;    // AVaR alpha per nonleaf node
+    const double* blo_nl;     // the one box table of the nonleaf nodes [x | u] (box == 1)
+    const double* bhi_nl;
+    const double* blo_l;      // the one box table of the leaves (box == 1)
+    const double* bhi_l;
+    const double* img;        // [sqrtQ | sqrtR | sqrtPf] MFMA fragments (k_cp3_image)
+    Ctl* ctl;
+    double* part;             // this iteration's residual maxima: one row of 6 per sweep workgroup
+    int nanbit;               // the ctl->flags bit of this iteration's NaN-in-box flag (ChkArg::nanbit)
+    int box;                  // 1: every node boxed by one table per kind; 2: no boxes
+};
+// doubles of the CP operand region of a workgroup (raocp_dynr.hip Cpa)
+constexpr int kDrcCpa = 3712;
+// the weight image (DrcArg::img): [sqrtQ 640 | sqrtR 128] (kDrcWa doubles), then [sqrtPf 640 |
+// lo_nl 28 | hi_nl 28 | lo_l 20 | hi_l 20] (kDrcWb)
+constexpr int kDrcWa = 768, kDrcWb = 736;
+// nx, nu, C, fp64 compiled for the fused form (the plan must have L = 4 in every tier)
+bool drc_supported(int nx, int nu, int C);
+// LDS bytes of a k_drc workgroup (tiers of 4 levels)
+size_t drc_lds(int nx, int nu, int C);
+// workgroups of k_drc (512 lanes) resident per CU at lds bytes
+int drc_occupancy(size_t lds);
+// one launch: the projection of z1 = pick3(bf, 1) in place, then the CP iteration of every family
+// (p = bf.z0, eta = bf.e0 -> eta+ = bf.e1, the next half step -> bf.z2); ck: the previous
+// iteration's stopping test (an extra workgroup)
+void drc_launch(const DrPlan& pl, const DrcArg& a, size_t lds, Bufs bf, const Ctl* ctl, ChkArg ck, hipStream_t s);
+const char* drc_name();
+// this translation unit compiled with the in-kernel stamps (make DIAG=1, or a VAR_UNIT=dynr
+// variant build with -DRAOCP_DIAG, tools/build_var.sh)
+bool dr_diag_build();
 
 }  // namespace raocp

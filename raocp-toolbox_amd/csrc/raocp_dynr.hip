@@ -43,6 +43,7 @@
 // and the granules, raocp_capi.hip).
 
 #include "raocp_dynr.h"
+#include "raocp_cpops.h"
 
 namespace raocp {
 namespace {
@@ -56,7 +57,6 @@ __device__ __forceinline__ d2v ld2(const ldsd* p) { return *(const lds2*)p; }
 
 // LDS barrier that does not wait for this wave's global memory operations
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-__device__ __forceinline__ void dma_wait() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 
 // {sync[0], sync[1]} by a scalar load (lgkmcnt, outside the vmcnt queue of the counted
@@ -178,11 +178,12 @@ __device__ __forceinline__ void stamp(const DrPlan& pl, Stamps& s) {
         s.ts[s.n++] = __builtin_amdgcn_s_memrealtime();
     }
 }
-// every workgroup (diagnostics, tools/dr_skew.py): slots 1024 + 3 b + {0 start, 1 backward
-// sweep done, 2 end}
+// every workgroup (diagnostics, tools/dr_skew.py): slots 1024 + 4 b + {0 start, 1 backward
+// sweep done, 2 end, 3 forward sweep done (k_drc: the CP step's start)}; the host checks the
+// buffer holds them (raocp_debug_dyn_stamps)
 __device__ __forceinline__ void wg_stamp(const DrPlan& pl, int q) {
     if (kDiag && pl.stamps && threadIdx.x == 0)
-        pl.stamps[1024 + 3 * blockIdx.x + q] = __builtin_amdgcn_s_memrealtime();
+        pl.stamps[1024 + 4 * blockIdx.x + q] = __builtin_amdgcn_s_memrealtime();
 }
 // slots [32 k, 32 k + 30): the stamps; 32 k + 30: the end; 32 k + 31: cycles from the first
 // stamp to the end
@@ -343,10 +344,681 @@ __device__ __forceinline__ void wait_vm_c() {
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// one tier's subtree o (L nonleaf levels): steps 1-7 of the header
-template <int NX, int NU, int C, int BS, int UMAX, int L>
+// ================================ k_drc: the fused CP step ================================
+// A workgroup of the sweep owns the CP families whose parent is one of its subtree's nonleaf
+// nodes (solver.py:27-95 with cache.py:248-393): the family of node i reads the projection only
+// at i (x+_i, u+_i: eta3 / eta4 of a child are sqrtQ / sqrtR of the PARENT's rows,
+// operators.py:19-53), and a leaf's rows only its own x+. So right behind its forward sweep, with
+// x+ and u+ still in LDS, a workgroup runs the CP iteration of its 15 families (one 16-lane MFMA
+// tile, lane lo = subtree-local BFS index, lo = 15 dead) and, in the deepest tier, of its 16
+// leaves (lane lo = leaf), with k_cp6's entry arithmetic (raocp_cp5.hip) split over the waves:
+//   wave 0, 1    child slot k: the parent's L products, the child block SOC (eta3..eta6), the
+//                slot's (eta+, d - eta+, xi2) rows to LDS, tau_j; a nonleaf child's s_j from its
+//                eta2 (recomputed, k_cp6's arithmetic)
+//   wave 2       phase 1: eta1, eta2 of the parent, y_i of the half step, s_0
+//   wave 3       (deepest) the leaf tile: eta11..eta14 with the leaf SOC and box, x_l of the half
+//                step by the eta+ stream, s_l; the (d - eta+) and xi2 rows to LDS
+//   -- barrier --
+//   wave 0       L^T of the eta+ stream (Gamma' eta7 + slot sums in slot order): x_i, u_i
+//   wave 1       the (d - eta+) and xi2 streams and the residual terms of x_i, u_i
+//   wave 2       the AVaR kernel projection of the family (cache.py:290-317)
+//   wave 4       (deepest) the leaves' (d - eta+) and xi2 streams and their residual terms
+// Every operand that does not depend on the projection is in LDS before the forward sweep ends:
+// gathered by 4-B LDS-DMA (Cpa) while the workgroup waits for its root's x row (the top: behind
+// its forward sweep, off the critical path); the MFMA weight fragments and box tables land in the
+// table slots the forward levels free (slot 3 after level 0, slot 2 after level 1).
+//
+// Global index of the subtree-local node lc (C = 2): (R0 << level(lc)) + lc, R0 the root.
+__device__ __forceinline__ int lev2(int lc) { return 31 - __builtin_clz((unsigned)lc + 1u); }
+__device__ __forceinline__ int gnode(int R0, int lc) { return (R0 << lev2(lc)) + lc; }
+
+// the CP operand region (doubles): rows of the 15 families lo (row 15 zero), their 30 children
+// c = 2 lo + 1 + k (row c - 1; rows 30, 31 zero), the deepest tier's 16 leaves q
+struct Cpa {
+    static constexpr int PX = 0;      // [16][20] x of p (the previous z+) at the parents
+    static constexpr int PU = 320;    // [16][8]  u of p
+    static constexpr int D3 = 448;    // [32][20] eta3 of the children
+    static constexpr int D4 = 1088;   // [32][8]  eta4
+    static constexpr int SC = 1344;   // [32][16] eta5, eta6, tau of z+ / p; a nonleaf child's s of z+ / p,
+                                      //          eta2, cond of its children, y of z+ / p (entries 0, 1, 2C)
+    static constexpr int PS = 1856;   // [16][24] y of z+ / p (5 + 5), eta1 (5), s of z+ / p, eta2,
+                                      //          cond of the children (2), AVaR alpha
+    static constexpr int D7 = 2240;   // [16][28] eta7 (boxed nonleaf nodes)
+    static constexpr int LP = 2688;   // [16][20] x of p at the leaves (deepest tier)
+    static constexpr int D11 = 3008;  // [16][20] eta11
+    static constexpr int D14 = 3328;  // [16][20] eta14 (boxed leaves)
+    static constexpr int LS = 3648;   // [16][4]  eta12, eta13, s of z+ / p
+    static constexpr int N = 3712;
+    // after barrier A2 (k_drc cp_phase): the families' box seeds of the (d - eta+) and xi2 streams
+    // over the dead eta3 / eta4 rows ([16][28] each), the xi2 stream's L^T over the child scalars
+    static constexpr int SDW = D3, SDC = D3 + 448;
+};
+static_assert(Cpa::N == kDrcCpa, "CP operand region");
+// scratch in the table slots once the forward sweep is done (doubles from the first slot; slot
+// s at s * 1344): the weight image in slots 2 and 3 as the forward levels free them; slots 0-1
+// first hold the L products that waves exchange (qa, qb, lb, ua, ub), then (after barrier A2)
+// the child slots' stream rows [slot k][stream q][x 320 | u 128]; the leaves' (d - eta+) and xi2
+// rows, the kernel-projection scratch and the residual maxima in the slots' tails
+struct Cps {
+    static constexpr int WA = kDrcWa;  // doubles of the first image part ([sqrtQ | sqrtR])
+    static constexpr int WB = kDrcWb;  // the second ([sqrtPf | lo_nl | hi_nl | lo_l | hi_l])
+    static constexpr int SLOT = 1344;
+    static constexpr int QA = 0, QB = 512, LB = 1024, UA = 1536, UB = 1792;  // products (row-layout v4 x 64 lanes)
+    static constexpr int SB = 0, SX = 320, SS = 448;                          // stream rows (compacted)
+    static constexpr int WP = 2 * SLOT, BX = 2 * SLOT + 640, LEW = 2 * SLOT + 736, KPS = 2 * SLOT + 1056;
+    static constexpr int WQ = 3 * SLOT, WR = 3 * SLOT + 640, LEC = 3 * SLOT + 768, RED = 3 * SLOT + 1088;
+};
+static_assert(Cps::UB + 256 <= 2 * Cps::SLOT && 6 * Cps::SS <= 2 * Cps::SLOT, "slots 0-1");
+static_assert(Cps::KPS + 272 <= 3 * Cps::SLOT && Cps::RED + 96 <= 4 * Cps::SLOT, "slot tails");
+
+// 4-B LDS-DMA gather of n doubles into dst: element e from src(e) (a global address)
+template <class F>
+__device__ __forceinline__ void gather(ldsd* dst, int n, F src) {
+    typedef const __attribute__((address_space(1))) unsigned gcu;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int c0 = wave * 64; c0 < 2 * n; c0 += nw * 64) {
+        const int f = c0 + lane;
+        if (f < 2 * n) __builtin_amdgcn_global_load_lds((gcu*)src(f >> 1) + (f & 1), (ldsu*)dst + c0, 4, 0, 0);
+    }
+}
+
+template <int NX, int NU, int BXN>
+__device__ __forceinline__ void cpa_gather(const DrcArg& a, const DrPlan& pl, const Bufs& bf, int R0, bool deepest,
+                                           ldsd* A) {
+    const double* pz = bf.z0;  // p
+    const double* zp = bf.z1;  // z+ (y, tau, s: not written by this launch)
+    const double* dd = bf.e0;  // eta
+    const double* zpg = pl.zpage;
+    gather(A + Cpa::PX, 16 * NX, [=](int e) {
+        const int r = e / NX;
+        return r < 15 ? pz + pl.X0 + (size_t)gnode(R0, r) * NX + (e - r * NX) : zpg;
+    });
+    gather(A + Cpa::PU, 16 * NU, [=](int e) {
+        const int r = e / NU;
+        return r < 15 ? pz + pl.U0 + (size_t)gnode(R0, r) * NU + (e - r * NU) : zpg;
+    });
+    gather(A + Cpa::D3, 32 * NX, [=](int e) {
+        const int r = e / NX;
+        return r < 30 ? dd + a.E3 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NX + (e - r * NX) : zpg;
+    });
+    gather(A + Cpa::D4, 32 * NU, [=](int e) {
+        const int r = e / NU;
+        return r < 30 ? dd + a.E4 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NU + (e - r * NU) : zpg;
+    });
+    gather(A + Cpa::SC, 32 * 16, [=](int e) {
+        const int r = e >> 4, q = e & 15;
+        if (r >= 30) return zpg;
+        const int j = gnode(R0, r + 1);
+        switch (q) {
+            case 0: return dd + a.E5 + j;
+            case 1: return dd + a.E6 + j;
+            case 2: return zp + a.T0 + j;
+            case 3: return pz + a.T0 + j;
+            default: break;
+        }
+        if ((deepest && r + 1 >= 15) || q == 15) return zpg;  // a leaf child: no eta2
+        switch (q) {
+            case 4: return zp + a.S0 + j;
+            case 5: return pz + a.S0 + j;
+            case 6: return dd + a.E2 + j;
+            case 7: return a.cond + 1 + 2 * j;
+            case 8: return a.cond + 2 + 2 * j;
+            case 9: return zp + a.Y0 + 5 * j;
+            case 10: return zp + a.Y0 + 5 * j + 1;
+            case 11: return zp + a.Y0 + 5 * j + 4;
+            case 12: return pz + a.Y0 + 5 * j;
+            case 13: return pz + a.Y0 + 5 * j + 1;
+            default: return pz + a.Y0 + 5 * j + 4;
+        }
+    });
+    gather(A + Cpa::PS, 16 * 24, [=](int e) {
+        const int r = e / 24, q = e - r * 24;
+        if (r >= 15 || q >= 21) return zpg;
+        const int g = gnode(R0, r);
+        if (q < 5) return zp + a.Y0 + 5 * g + q;
+        if (q < 10) return pz + a.Y0 + 5 * g + (q - 5);
+        if (q < 15) return dd + a.E1 + 5 * g + (q - 10);
+        switch (q) {
+            case 15: return zp + a.S0 + g;
+            case 16: return pz + a.S0 + g;
+            case 17: return dd + a.E2 + g;
+            case 18: return a.cond + 1 + 2 * g;
+            case 19: return a.cond + 2 + 2 * g;
+            default: return a.alpha_r + g;
+        }
+    });
+    if (BXN == 1)
+        gather(A + Cpa::D7, 16 * (NX + NU), [=](int e) {
+            const int r = e / (NX + NU);
+            return r < 15 ? dd + a.E7 + (size_t)gnode(R0, r) * (NX + NU) + (e - r * (NX + NU)) : zpg;
+        });
+    if (deepest) {
+        const int l0 = 16 * R0 + 15;  // the first leaf of the subtree
+        gather(A + Cpa::LP, 16 * NX, [=](int e) { return pz + pl.X0 + (size_t)l0 * NX + e; });
+        gather(A + Cpa::D11, 16 * NX, [=](int e) { return dd + a.E11 + a.m + (size_t)(l0 - a.m) * NX + e; });
+        if (a.box == 1)
+            gather(A + Cpa::D14, 16 * NX, [=](int e) { return dd + a.E14 + a.m + (size_t)(l0 - a.m) * NX + e; });
+        gather(A + Cpa::LS, 64, [=](int e) {
+            const int l = l0 + (e >> 2);
+            switch (e & 3) {
+                case 0: return dd + a.E12 + l;
+                case 1: return dd + a.E13 + l;
+                case 2: return zp + a.S0 + l;
+                default: return pz + a.S0 + l;
+            }
+        });
+    }
+}
+
+// an R-row node vector from an LDS row in the tile's row layout (raocp_tile.h ld_rows), zero
+// when !live (row must be a valid LDS row either way)
+template <int R>
+__device__ __forceinline__ void ld_lr(const ldsd* row, bool live, double (&a)[(R + 15) / 16][4]) {
+    constexpr int KC = R / 4;
+    const ldsd* b = row + KC * ((threadIdx.x & 63) >> 4);
+    _Pragma("unroll") for (int rt = 0; rt < (R + 15) / 16; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+        double w = 0.0;
+        if (tok<R>(rt, e)) w = b[4 * rt + e];
+        a[rt][e] = live ? w : 0.0;
+    }
+}
+
+// slot (rt, e) of a lane's R-row vector: its row index KC h + 4 rt + e (tok<R>(rt, e)), and its
+// place in a compacted LDS image (lds_putc: lane's KC values at base + lane KC)
+template <int R>
+__device__ __forceinline__ int row_of(int rt, int e) {
+    return (R / 4) * ((threadIdx.x & 63) >> 4) + 4 * rt + e;
+}
+template <int R>
+__device__ __forceinline__ int cpos(int rt, int e) {
+    return (threadIdx.x & 63) * (R / 4) + 4 * rt + e;
+}
+
+template <int NX, int NU, int BXN, int BXL>
+__device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double alpha_in, int X0, int U0, int R0,
+                                         bool deepest, const ldsd* XD, const ldsd* XL, const ldsd* U, ldsd* A,
+                                         ldsd* SL, unsigned long long* dstamps, int nblk) {
+    typedef double T;
+    typedef MF<T>::v4 v4;
+    constexpr int C = 2, RX = (NX + 15) / 16, RU = (NU + 15) / 16, G = 2 * C + 1, NQ = (G + 3) / 4;
+    constexpr int SXD = NX + NU, SS = Cps::SS, SX = Cps::SX;
+    static_assert(NX == 20 && NU == 8, "the scratch layout (Cps) is sized for nx = 20, nu = 8");
+    typedef WL<T, NX, NX> WQ;
+    typedef WL<T, NU, NU> WR;
+    typedef __attribute__((address_space(3))) KpScratch<T> lkps;
+    const int tid = threadIdx.x, lane = tid & 63, lo = lane & 15, h = lane >> 4, wv = tid >> 6;
+    // diagnostics: per-wave stamps of the first (deepest) and the last (top) workgroup at
+    // 3072 + {0, 64} + 8 wave + {0 start, 1 first role done, 2 second role done, 3 third role
+    // done, 4 end}
+    auto dstamp = [&](int q) {
+        if (kDiag && dstamps && lane == 0 && (blockIdx.x == 0 || (int)blockIdx.x == nblk - 1))
+            dstamps[3072 + ((int)blockIdx.x == 0 ? 0 : 64) + 8 * wv + q] = __builtin_amdgcn_s_memrealtime();
+    };
+    dstamp(0);
+    const WQ wq{SL + Cps::WQ};
+    const WR wr{SL + Cps::WR};
+    const WQ wp{SL + Cps::WP};
+    const ldsd* BX = SL + Cps::BX;  // [lo_nl | hi_nl | lo_l | hi_l]
+    lkps& ks = *(lkps*)(SL + Cps::KPS);
+    glbp<T> out = (glbp<T>)bf.z2;  // next half step
+    glbp<T> eo = (glbp<T>)bf.e1;   // eta+
+    const int m = a.m;
+    Resid<T> rs;
+    rs.alpha = alpha_in;
+    rs.ra = T(1) / rs.alpha;
+    const T alpha = rs.alpha, ra = rs.ra;
+    bool nanf = false;  // a NaN reached a box (Rectangle._constrain raises)
+    const bool live = lo < 15;
+    const int lq = live ? lo : 0;
+    const int i = gnode(R0, lq), yo = G * i;  // this lane's parent (global)
+    const int l = 16 * R0 + 15 + lo;           // this lane's leaf (deepest tier)
+    // ============ Ia: the L products, one MFMA chain per wave (waves w, w + 4 share a SIMD)
+    v4 pk[RX];  // wave 0: qa = sqrtQ (2 x+ - p); wave 1: qb = sqrtQ (x+ - p); wave 2: la; wave 3: lb
+    if (wv < 2 || (wv < 4 && deepest)) {
+        T b[RX][4];
+        {
+            T z[RX][4], pp[RX][4];
+            if (wv < 2) {
+                ld_lr<NX>(XD + lq * SXD, live, z);
+                ld_lr<NX>(A + Cpa::PX + lq * NX, live, pp);
+            } else {
+                ld_lr<NX>(XL + lo * NX, true, z);
+                ld_lr<NX>(A + Cpa::LP + lo * NX, true, pp);
+            }
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                b[rt][e] = (wv & 1) ? z[rt][e] - pp[rt][e] : T(2) * z[rt][e] - pp[rt][e];
+        }
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) pk[rt] = v4{0, 0, 0, 0};
+        if (wv < 2) mmt(wq.fresh(), b, pk);
+        else mmt(wp.fresh(), b, pk);
+        if (wv != 2) {  // qa, qb, lb to LDS (la stays in wave 2's registers)
+            ldsd* dst = SL + (wv == 0 ? Cps::QA : (wv == 1 ? Cps::QB : Cps::LB));
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                dst[(rt * 64 + lane) * 4 + e] = pk[rt][e];
+        }
+    } else if (wv == 4) {
+        T c1[RU][4], c2[RU][4];
+        {
+            T uz[RU][4], up[RU][4];
+            ld_lr<NU>(U + lq * NU, live, uz);
+            ld_lr<NU>(A + Cpa::PU + lq * NU, live, up);
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                c1[rt][e] = T(2) * uz[rt][e] - up[rt][e];
+                c2[rt][e] = uz[rt][e] - up[rt][e];
+            }
+        }
+        v4 ua[RU], ub[RU];
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) ua[rt] = ub[rt] = v4{0, 0, 0, 0};
+        mmt(wr.fresh(), c1, ua);
+        mmt(wr.fresh(), c2, ub);
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+            SL[Cps::UA + (rt * 64 + lane) * 4 + e] = ua[rt][e];
+            SL[Cps::UB + (rt * 64 + lane) * 4 + e] = ub[rt][e];
+        }
+    } else if (wv == 5) {
+        // ================= phase 1: the parent's eta2, eta1 (AVaR cone), y_i, s_0
+        const ldsd* ps = A + Cpa::PS + lq * 24;
+        T cp[C], zyk[C], pyk[C];
+        _Pragma("unroll") for (int q = 0; q < C; ++q) {
+            cp[q] = live ? ps[18 + q] : T(0);
+            zyk[q] = live ? ps[q] : T(0);
+            pyk[q] = live ? ps[5 + q] : T(0);
+        }
+        const T zyc = live ? ps[2 * C] : T(0), pyc = live ? ps[5 + 2 * C] : T(0);
+        const T zs = live ? ps[15] : T(0), pps = live ? ps[16] : T(0), d2 = live ? ps[17] : T(0);
+        T qz[NQ], qp[NQ], qd[NQ];
+        _Pragma("unroll") for (int t = 0; t < NQ; ++t) {
+            const int q = h + 4 * t;
+            const bool ok = live && q < G;
+            const int qq = q < G ? q : 0;
+            qz[t] = ok ? ps[qq] : T(0);
+            qp[t] = ok ? ps[5 + qq] : T(0);
+            qd[t] = ok ? ps[10 + qq] : T(0);
+        }
+        T bya = T(0), byb = T(0);
+        _Pragma("unroll") for (int q = 0; q < C; ++q) {
+            bya = fma(cp[q], T(2) * zyk[q] - pyk[q], bya);
+            byb = fma(cp[q], zyk[q] - pyk[q], byb);
+        }
+        bya += T(2) * zyc - pyc;
+        byb += zyc - pyc;
+        T e2A, e2C;
+        {
+            const T av = (T(2) * zs - pps) - bya, bb = (zs - pps) - byb;
+            const T v = (d2 + alpha * av) * ra;
+            T x2;
+            rs.fin(d2, v, fmax(v, T(0)), bb, e2A, x2);
+            e2C = x2;
+            if (live && h == 0) *elw(eo, a.E2 + i) = e2A;
+        }
+        const T e2W = d2 - e2A;
+        if (live && i == 0 && h == 0) {
+            // root s_0: L^T -> eta2_0, then the relaxation prox s_0 -= alpha (cache.py:253-257)
+            *elw(out, a.S0) = (zs - alpha * e2A) - alpha;
+            rs.account(pps, zs, e2W, e2C);
+        }
+        _Pragma("unroll") for (int t = 0; t < NQ; ++t) {
+            const int q = h + 4 * t;
+            if (!live || q >= G) break;
+            const T zy = qz[t], py = qp[t], dv = qd[t];
+            const T v = (dv + alpha * (T(2) * zy - py)) * ra;
+            T ep, x2;
+            rs.fin(dv, v, q < 2 * C ? fmax(v, T(0)) : v, zy - py, ep, x2);
+            *elw(eo, a.E1 + yo + q) = ep;
+            T bq = T(1);
+            if (q < C) {
+                _Pragma("unroll") for (int kk = 0; kk < C; ++kk) if (kk == q) bq = cp[kk];
+            } else if (q < 2 * C) {
+                bq = T(0);
+            }
+            ks.y[lo][q] = zy - alpha * (ep - bq * e2A);
+            rs.account(py, zy, (dv - ep) - bq * e2W, x2 - bq * e2C);
+        }
+    } else if (wv == 6) {
+        // ================= s_j of the nonleaf children (k = h < C): its eta2 recomputed (its own
+        // family's phase 1, k_cp6's arithmetic)
+        const int k = h, cl = 2 * lq + 1 + (h & 1);
+        if (live && h < C && !(deepest && cl >= 15)) {
+            const ldsd* sc = A + Cpa::SC + (cl - 1) * 16;
+            const T csz = sc[4], csp = sc[5], cdj = sc[6];
+            const T ccp[C] = {sc[7], sc[8]}, czy[C + 1] = {sc[9], sc[10], sc[11]}, cpy[C + 1] = {sc[12], sc[13], sc[14]};
+            T ba = T(0), bb2 = T(0);
+            _Pragma("unroll") for (int q = 0; q < C; ++q) {
+                ba = fma(ccp[q], T(2) * czy[q] - cpy[q], ba);
+                bb2 = fma(ccp[q], czy[q] - cpy[q], bb2);
+            }
+            ba += T(2) * czy[C] - cpy[C];
+            bb2 += czy[C] - cpy[C];
+            const T av = (T(2) * csz - csp) - ba, bb = (csz - csp) - bb2;
+            const T v = (cdj + alpha * av) * ra;
+            const T ep = alpha * (v - fmax(v, T(0)));
+            const T x2 = (cdj - ep) * ra + bb;
+            ks.s[lo][k] = csz - alpha * ep;
+            rs.account(csp, csz, cdj - ep, x2);
+        }
+    }
+    dstamp(1);
+    lds_sync();  // A: the products in LDS
+    // ============ Ib: the SOC of each child block (wave k: slot k) and of the leaves (wave 2);
+    // every operand read into registers before barrier A2, after which the stream rows overwrite
+    // the products' LDS
+    if (wv < 2) {
+        const int k = wv, cl = 2 * lq + 1 + k, j = gnode(R0, cl);
+        v4 qa[RX], qb[RX], ua[RU], ub[RU];
+        {
+            const ldsd* o = SL + (k == 0 ? Cps::QB : Cps::QA);
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) {
+                v4 w;
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) w[e] = o[(rt * 64 + lane) * 4 + e];
+                if (k == 0) {
+                    qa[rt] = pk[rt];
+                    qb[rt] = w;
+                } else {
+                    qa[rt] = w;
+                    qb[rt] = pk[rt];
+                }
+            }
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                ua[rt][e] = SL[Cps::UA + (rt * 64 + lane) * 4 + e];
+                ub[rt][e] = SL[Cps::UB + (rt * 64 + lane) * 4 + e];
+            }
+        }
+        T d3[RX][4], d4[RU][4];
+        ld_lr<NX>(A + Cpa::D3 + (cl - 1) * NX, live, d3);
+        ld_lr<NU>(A + Cpa::D4 + (cl - 1) * NU, live, d4);
+        const ldsd* sc = A + Cpa::SC + (cl - 1) * 16;
+        const T d5 = live ? sc[0] : T(0), d6 = live ? sc[1] : T(0), tz = live ? sc[2] : T(0), tp = live ? sc[3] : T(0);
+        lds_sync();  // A2
+        // ---------------- the child block SOC (cache.py:321-372)
+        T v3[RX][4], v4_[RU][4];
+        T ss = T(0);
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+            v3[rt][e] = (d3[rt][e] + alpha * qa[rt][e]) * ra;
+            if (tok<NX>(rt, e)) ss += v3[rt][e] * v3[rt][e];
+        }
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+            v4_[rt][e] = (d4[rt][e] + alpha * ua[rt][e]) * ra;
+            if (tok<NU>(rt, e)) ss += v4_[rt][e] * v4_[rt][e];
+        }
+        ss = sum_h(ss);
+        const T a5 = T(0.5) * (T(2) * tz - tp), b5 = T(0.5) * (tz - tp);
+        const T v5 = (d5 + alpha * a5) * ra + T(-0.5);
+        const T v6 = (d6 + alpha * a5) * ra + T(0.5);
+        ss += v5 * v5;
+        const Soc<T> so(sqrt(ss), v6);
+        // each entry's (eta+, d - eta+, xi2) straight to the slot's stream rows and eta+ to the dual
+        ldsd* sk = SL + Cps::SB + k * 3 * SS;
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+            if (!tok<NX>(rt, e)) continue;
+            T ep, x2;
+            rs.fin(d3[rt][e], v3[rt][e], so.first(v3[rt][e]), qb[rt][e], ep, x2);
+            const int q = cpos<NX>(rt, e);
+            sk[q] = ep;
+            sk[SS + q] = d3[rt][e] - ep;
+            sk[2 * SS + q] = x2;
+            if (live) *elw(eo, a.E3 + 1 + (j - 1) * NX + row_of<NX>(rt, e)) = ep;
+        }
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+            if (!tok<NU>(rt, e)) continue;
+            T ep, x2;
+            rs.fin(d4[rt][e], v4_[rt][e], so.first(v4_[rt][e]), ub[rt][e], ep, x2);
+            const int q = SX + cpos<NU>(rt, e);
+            sk[q] = ep;
+            sk[SS + q] = d4[rt][e] - ep;
+            sk[2 * SS + q] = x2;
+            if (live) *elw(eo, a.E4 + 1 + (j - 1) * NU + row_of<NU>(rt, e)) = ep;
+        }
+        T ep5, x25, ep6, x26;
+        rs.fin(d5, v5, so.first(v5), b5, ep5, x25);
+        rs.fin(d6, v6, so.last(v6), b5, ep6, x26);
+        if (live && h == 0) {
+            *elw(eo, a.E5 + j) = ep5;
+            ks.tau[lo][k] = tz - alpha * (T(0.5) * (ep5 + ep6));
+            rs.account(tp, tz, T(0.5) * ((d5 - ep5) + (d6 - ep6)), T(0.5) * (x25 + x26));
+        }
+        if (live && h == 1) *elw(eo, a.E6 + j) = ep6;
+    } else if (wv == 2 && deepest) {
+        // ================= the leaf tile (lane lo = leaf lo of the subtree; k_cp6's leaf waves)
+        v4 lb[RX];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+            lb[rt][e] = SL[Cps::LB + (rt * 64 + lane) * 4 + e];
+        T d11[RX][4];
+        ld_lr<NX>(A + Cpa::D11 + lo * NX, true, d11);
+        const ldsd* ls = A + Cpa::LS + lo * 4;
+        const T d12 = ls[0], d13 = ls[1], sz = ls[2], sp = ls[3];
+        lds_sync();  // A2
+        T v11[RX][4];
+        T ss = T(0);
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+            v11[rt][e] = (d11[rt][e] + alpha * pk[rt][e]) * ra;
+            if (tok<NX>(rt, e)) ss += v11[rt][e] * v11[rt][e];
+        }
+        ss = sum_h(ss);
+        const T a5 = T(0.5) * (T(2) * sz - sp), b5 = T(0.5) * (sz - sp);
+        const T v12 = (d12 + alpha * a5) * ra + T(-0.5);
+        const T v13 = (d13 + alpha * a5) * ra + T(0.5);
+        ss += v12 * v12;
+        const Soc<T> so(sqrt(ss), v13);
+        T ep12, x212, ep13, x213;
+        rs.fin(d12, v12, so.first(v12), b5, ep12, x212);
+        rs.fin(d13, v13, so.last(v13), b5, ep13, x213);
+        if (h == 0) {
+            ks.s[7 + (lo >> 1)][lo & 1] = sz - alpha * (T(0.5) * (ep12 + ep13));
+            rs.account(sp, sz, T(0.5) * ((d12 - ep12) + (d13 - ep13)), T(0.5) * (x212 + x213));
+            *elw(eo, a.E12 + l) = ep12;
+        }
+        if (h == 1) *elw(eo, a.E13 + l) = ep13;
+        T eA[RX][4];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+            T ep = T(0), x2 = T(0);
+            if (tok<NX>(rt, e)) {
+                rs.fin(d11[rt][e], v11[rt][e], so.first(v11[rt][e]), lb[rt][e], ep, x2);
+                const int q = cpos<NX>(rt, e);
+                SL[Cps::LEW + q] = d11[rt][e] - ep;
+                SL[Cps::LEC + q] = x2;
+                *elw(eo, a.E11 + m + (l - m) * NX + row_of<NX>(rt, e)) = ep;
+            }
+            eA[rt][e] = ep;
+        }
+        // the eta+ stream (after barrier B, the same wave): sqrtPf' eta11+ onto the box term
+        lds_sync();  // B
+        dstamp(2);
+        v4 gA[RX];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) gA[rt] = v4{0, 0, 0, 0};
+        if (BXL == 1) {
+            // eta14 = x_l (box, cache.py:374-393) seeds the eta+ stream's L^T accumulator
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) {
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                    if (!tok<NX>(rt, e)) continue;
+                    const int r = row_of<NX>(rt, e);
+                    const T lzv = XL[lo * NX + r], lpv = A[Cpa::LP + lo * NX + r], d14 = A[Cpa::D14 + lo * NX + r];
+                    const T v = (d14 + alpha * (T(2) * lzv - lpv)) * ra;
+                    T ep, x2;
+                    rs.fin(d14, v, box_sel(v, BX[2 * (NX + NU) + r], BX[2 * (NX + NU) + NX + r], nanf), lzv - lpv, ep, x2);
+                    gA[rt][e] = ep;
+                    *elw(eo, a.E14 + m + (l - m) * NX + r) = ep;
+                }
+                __builtin_amdgcn_sched_barrier(0);  // a row block at a time: bounded live operands
+            }
+        }
+        mmt(wp.fresh(), eA, gA);
+        const ldsd* xl = XL;
+        asm volatile("" : "+v"(xl));  // x+_l read again: not kept live across the SOC
+        T lz[RX][4], ox[RX][4];
+        ld_lr<NX>(xl + lo * NX, true, lz);
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+            ox[rt][e] = lz[rt][e] - alpha * gA[rt][e];
+        st_rows_o<T, NX>(out, X0 + l * NX, true, ox);
+    }
+    if (!(wv < 2 || (wv == 2 && deepest))) lds_sync();  // A2
+    if (BXN == 1 && wv == 7) {
+        // ================= the box rows of the families (Rectangle on eta7 = [x_i | u_i],
+        // cache.py:374-393): eta7+ to the dual, and per entry the three streams' seeds
+        // (eta7+ over eta7 in place, d - eta7+ and xi2 over the dead eta3 / eta4 rows)
+        // lane group h takes the entries r = r0 + h, r0 = 0, 4, .., 24
+        _Pragma("unroll") for (int r0 = 0; r0 < NX + NU; r0 += 4) {
+            const int r = r0 + h;
+            const T zv = live ? (r < NX ? XD[lq * SXD + r] : U[lq * NU + r - NX]) : T(0);
+            const T pv = live ? (r < NX ? A[Cpa::PX + lq * NX + r] : A[Cpa::PU + lq * NU + r - NX]) : T(0);
+            const int o = lq * (NX + NU) + r;
+            const T d7 = live ? A[Cpa::D7 + o] : T(0);
+            const T lv = live ? BX[r] : T(0), hv = live ? BX[(NX + NU) + r] : T(0);  // dead lanes: zero terms
+            const T v = (d7 + alpha * (T(2) * zv - pv)) * ra;
+            T ep, x2;
+            rs.fin(d7, v, box_sel(v, lv, hv, nanf), zv - pv, ep, x2);
+            if (live) {
+                *elw(eo, a.E7 + i * (NX + NU) + r) = ep;
+                A[Cpa::D7 + o] = ep;
+                A[Cpa::SDW + o] = d7 - ep;
+                A[Cpa::SDC + o] = x2;
+            }
+        }
+    }
+    if (!(wv == 2 && deepest)) {
+        dstamp(2);
+        lds_sync();  // B: the stream rows, tau, s, y of the half step are in LDS
+    }
+    // ============ II: the L^T streams (operators.py:73-94), one MFMA chain per wave
+    if (wv == 0 || wv == 1 || wv == 3) {
+        // families: wave 0 the eta+ stream onto Gamma' eta7 (box) -> x_i, u_i of the half step;
+        // wave 1 the (d - eta+) stream, wave 3 the xi2 stream (to LDS for wave 1's residual terms)
+        const int q = wv == 0 ? 0 : (wv == 1 ? 1 : 2);
+        v4 g[RX], hh[RU];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) g[rt] = v4{0, 0, 0, 0};
+        _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) hh[rt] = v4{0, 0, 0, 0};
+        if (BXN == 1) {
+            // the box terms of the stream (wave 7's seeds: eta7+, d - eta7+ or xi2 per entry of
+            // [x | u]) seed the accumulator
+            const ldsd* sd = A + (q == 0 ? Cpa::D7 : (q == 1 ? Cpa::SDW : Cpa::SDC)) + lq * (NX + NU);
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) g[rt][e] = live ? sd[row_of<NX>(rt, e)] : T(0);
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NU>(rt, e)) hh[rt][e] = live ? sd[NX + row_of<NU>(rt, e)] : T(0);
+        }
+        {
+            // the slots' rows of stream q summed per parent in slot order
+            const ldsd* sb = SL + Cps::SB;
+            T sx[RX][4], su[RU][4], ax[RX][4], au[RU][4];
+            lds_getc<T, NX>(sb + q * SS, sx);
+            lds_getc<T, NU>(sb + q * SS + SX, su);
+            lds_getc<T, NX>(sb + (3 + q) * SS, ax);
+            lds_getc<T, NU>(sb + (3 + q) * SS + SX, au);
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) sx[rt][e] += ax[rt][e];
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) su[rt][e] += au[rt][e];
+            mmt(wq.fresh(), sx, g);
+            mmt(wr.fresh(), su, hh);
+        }
+        if (wv == 0) {
+            T xz[RX][4], uz[RU][4], ox[RX][4], ou[RU][4];
+            ld_lr<NX>(XD + lq * SXD, live, xz);
+            ld_lr<NU>(U + lq * NU, live, uz);
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                ox[rt][e] = xz[rt][e] - alpha * g[rt][e];
+            st_rows_o<T, NX>(out, X0 + i * NX, live, ox);
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                ou[rt][e] = uz[rt][e] - alpha * hh[rt][e];
+            st_rows_o<T, NU>(out, U0 + i * NU, live, ou);
+            dstamp(3);
+            lds_sync();  // C
+        } else if (wv == 3) {
+            // xi2 stream to LDS, compacted (the child scalars are dead after barrier A2)
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) A[Cpa::SC + cpos<NX>(rt, e)] = g[rt][e];
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NU>(rt, e)) A[Cpa::SC + SX + cpos<NU>(rt, e)] = hh[rt][e];
+            dstamp(3);
+            lds_sync();  // C
+        } else {
+            dstamp(3);
+            lds_sync();  // C
+            // ============ III: the residual terms of x_i, u_i from both streams
+            T xz[RX][4], xp[RX][4], uz[RU][4], up[RU][4];
+            ld_lr<NX>(XD + lq * SXD, live, xz);
+            ld_lr<NX>(A + Cpa::PX + lq * NX, live, xp);
+            ld_lr<NU>(U + lq * NU, live, uz);
+            ld_lr<NU>(A + Cpa::PU + lq * NU, live, up);
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) rs.account(xp[rt][e], xz[rt][e], g[rt][e], A[Cpa::SC + cpos<NX>(rt, e)]);
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NU>(rt, e)) rs.account(up[rt][e], uz[rt][e], hh[rt][e], A[Cpa::SC + SX + cpos<NU>(rt, e)]);
+        }
+    } else if ((wv == 4 || wv == 5) && deepest) {
+        // leaves: wave 4 the (d - eta+) stream, wave 5 the xi2 stream (to LDS for wave 4's terms)
+        v4 g[RX];
+        _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) g[rt] = v4{0, 0, 0, 0};
+        if (BXL == 1) {
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) {
+                _Pragma("unroll") for (int e = 0; e < 4; ++e) {
+                    if (!tok<NX>(rt, e)) continue;
+                    const int r = row_of<NX>(rt, e);
+                    const T lzv = XL[lo * NX + r], lpv = A[Cpa::LP + lo * NX + r], d14 = A[Cpa::D14 + lo * NX + r];
+                    const T v = (d14 + alpha * (T(2) * lzv - lpv)) * ra;
+                    T ep, x2;
+                    rs.fin(d14, v, box_sel(v, BX[2 * (NX + NU) + r], BX[2 * (NX + NU) + NX + r], nanf), lzv - lpv, ep, x2);
+                    g[rt][e] = wv == 4 ? d14 - ep : x2;
+                }
+                __builtin_amdgcn_sched_barrier(0);  // a row block at a time: bounded live operands
+            }
+        }
+        {
+            T ew[RX][4];
+            lds_getc<T, NX>(SL + (wv == 4 ? Cps::LEW : Cps::LEC), ew);
+            mmt(wp.fresh(), ew, g);
+        }
+        if (wv == 5) {
+            // compacted; the eta11 operand rows are dead after barrier A2
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) A[Cpa::D11 + cpos<NX>(rt, e)] = g[rt][e];
+            dstamp(3);
+            lds_sync();  // C
+        } else {
+            dstamp(3);
+            lds_sync();  // C
+            T lz[RX][4], lp[RX][4];
+            ld_lr<NX>(XL + lo * NX, true, lz);
+            ld_lr<NX>(A + Cpa::LP + lo * NX, true, lp);
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) rs.account(lp[rt][e], lz[rt][e], g[rt][e], A[Cpa::D11 + cpos<NX>(rt, e)]);
+        }
+    } else if (wv == 6 && live) {
+        // ================= the AVaR kernel projection of the family (cache.py:290-317)
+        const T al = A[Cpa::PS + lq * 24 + 20];
+        const T y2c = ks.y[lo][2 * C];
+        T rk[C], sr = T(0);
+        _Pragma("unroll") for (int k = 0; k < C; ++k) {
+            rk[k] = al * ks.y[lo][k] - ks.y[lo][C + k] + y2c - ks.tau[lo][k] - ks.s[lo][k];
+            sr += rk[k];
+        }
+        const T aa = al * al + T(3);
+        T sw = T(0);
+        _Pragma("unroll") for (int k = 0; k < C; ++k) {
+            const T w = (rk[k] - sr / (aa + (T)C)) / aa;
+            sw += w;
+            if (k == h) {
+                const int j = 1 + C * i + k;
+                *elw(out, a.Y0 + yo + k) = ks.y[lo][k] - al * w;
+                *elw(out, a.Y0 + yo + C + k) = ks.y[lo][C + k] + w;
+                *elw(out, a.T0 + j) = ks.tau[lo][k] + w;
+                *elw(out, a.S0 + j) = ks.s[lo][k] + w;
+            }
+        }
+        if (h == 0) *elw(out, a.Y0 + yo + 2 * C) = y2c - sw;
+    }
+    if (!(wv == 0 || wv == 1 || wv == 3 || ((wv == 4 || wv == 5) && deepest))) {
+        dstamp(3);
+        lds_sync();  // C
+    }
+    flag_nan(a.ctl, nanf, a.nanbit);
+    block_maxima_at(a.part, blockIdx.x, rs, SL + Cps::RED);
+    dstamp(4);
+}
+
+// one tier's subtree o (L nonleaf levels): steps 1-7 of the header. BX > 0 (k_drc): the CP
+// iteration of the subtree's families follows (cp_phase; BX = 1 every node boxed, 2 none)
+template <int NX, int NU, int C, int BS, int UMAX, int L, int BX = 0>
 __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* z, unsigned tag, bool work,
-                                          Stamps& stp, int& s_ok, ldsd* sm) {
+                                          Stamps& stp, int& s_ok, ldsd* sm, const DrcArg* ca = nullptr,
+                                          const Bufs* bfp = nullptr, double alpha = 0.0) {
     constexpr int SXD = NX + NU, TBN = dr_tb_n(NX, NU, C), TFN = dr_tf_n(NX, NU, C), SLOT = dr_slot_n(NX, NU, C);
     constexpr int G = 2 * NX, NW = BS / 64;
     constexpr int NB = cpow(C, L), NNL = (NB - 1) / (C - 1);
@@ -362,6 +1034,23 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     ldsd* XL = XD + NNL * SXD;
     ldsd* U = XL + NB * NX;
     ldsd* X0B = U + NNL * NU;
+    constexpr bool CPF = BX > 0;
+    static_assert(!CPF || (C == 2 && L == 4), "k_drc: binary trees, tiers of 4 levels");
+    ldsd* CPA = X0B + NX;  // k_drc: the CP operand region (Cpa)
+    const int R0 = pl.sbase[s0] + o;  // the subtree's root
+    const bool gat = !(kDiag && (pl.fault & 128));  // timing probes (diagnostic builds)
+    if constexpr (CPF)
+        if (kDiag && (pl.fault & 512)) {  // the CP step alone
+            if (work) {
+                cpa_gather<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, CPA);
+                TableDma<Cps::WA, BS / 64>::issue(SL + 3 * SLOT, ca->img);
+                TableDma<Cps::WB, BS / 64>::issue(SL + 2 * SLOT, ca->img + Cps::WA);
+                dma_wait();
+                lds_sync();
+                cp_phase<NX, NU, BX, BX>(*ca, *bfp, alpha, pl.X0, pl.U0, R0, deepest, XD, XL, U, CPA, SL, nullptr, pl.nblk);
+            }
+            return;
+        }
     // first node of each level of this subtree (level L: the boundary)
     int gl[L + 1];
     static_for<0, L + 1>([&](auto lc) { gl[lc.value] = pl.sbase[s0 + lc.value] + o * cpow(C, lc.value); });
@@ -381,7 +1070,10 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
             constexpr int l = L - 1 - ic.value;
             TB::issue(SL + l * SLOT, pl.bimg + (size_t)(s0 + l) * TBN);
         });
-    // ---- 2. the child subtrees' q rows
+    // ---- 2. the child subtrees' q rows (k_drc: above the deepest tier the CP operands land
+    // during this wait)
+    if constexpr (CPF)
+        if (work && gat && (!deepest || top)) cpa_gather<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, CPA);
     if (!deepest) {
         const DrTier& ct = pl.t[k + 1];
         if (!poll_gran(pl.gq + (size_t)(ct.w0 + o * NB) * G, NB * G, tag, (ldsu*)XL, pl.timeout, pl.sync, s_ok)) {
@@ -415,6 +1107,10 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     if (top && !(kDiag && (pl.fault & 4))) TF::issue(SL, pl.fimg + (size_t)(s0 + L - 1) * TFN);
     if (!top) {
         if (!((pl.fault & 1) && deepest && o == 0)) publish(pl.gq + (size_t)(tt.w0 + o) * G, G, tag, (const ldsu*)XD);
+        // k_drc: the deepest tier's CP operands land during the wait below (older than the
+        // forward tables, so the forward levels' counted waits are unchanged)
+        if constexpr (CPF)
+            if (work && gat && deepest) cpa_gather<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, CPA);  // (not the top)
         if (!(kDiag && (pl.fault & 4)))
             static_for<0, L>([&](auto fc) {
                 constexpr int f = fc.value;
@@ -428,12 +1124,19 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     } else if (tid < NX) {
         XD[tid] = X0B[tid];  // x_0 = x0bar (cache.py:282)
     }
-    // ---- 6. forward sweep: level f waits for its table only (the younger ones stay in flight)
+    // ---- 6. forward sweep: level f waits for its table only (the younger ones stay in flight).
+    // k_drc: the CP weight image lands in the slots levels 0 and 1 free (issued behind their
+    // barriers, so level f >= 2 also lets those younger DMAs stay in flight)
+    typedef TableDma<Cps::WA, NW> WAD;
+    typedef TableDma<Cps::WB, NW> WBD;
     static_for<0, L>([&](auto fc) {
         constexpr int f = fc.value, cnt = cpow(C, f), off = (cnt - 1) / (C - 1);
-        wait_vm_c<(L - 1 - f) * TF::IPW>();
+        constexpr int XW = CPF ? (f >= 2 ? WAD::IPW : 0) + (f >= 3 ? WBD::IPW : 0) : 0;
+        wait_vm_c<(L - 1 - f) * TF::IPW + XW>();
         lds_sync();
         stamp(pl, stp);
+        if constexpr (CPF && f == 1) WAD::issue(SL + 3 * SLOT, ca->img);
+        if constexpr (CPF && f == 2) WBD::issue(SL + 2 * SLOT, ca->img + Cps::WA);
         if (work && !(kDiag && (pl.fault & 16))) {
             const bool last = f == L - 1;
             fwd_level<NX, NU, C, BS, UMAX, cnt>(SL + (L - 1 - f) * SLOT, XD + off * SXD, last ? XL : XD + (off + cnt) * SXD,
@@ -444,6 +1147,10 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     stamp(pl, stp);
     // ---- 7. the boundary x rows to the child subtrees, then x and u to the iterate
     if (!deepest) publish(pl.gx + (size_t)(pl.t[k + 1].w0 + o * NB) * G, NB * G, tag, (const ldsu*)XL);
+    if constexpr (CPF) {
+        dma_wait();
+        lds_sync();  // operands, weights and boxes in LDS for every wave
+    }
     if (work && !(kDiag && (pl.fault & 8))) {
         static_for<0, L + 1>([&](auto lc) {
             constexpr int l = lc.value, cnt = cpow(C, l), off = (cnt - 1) / (C - 1);
@@ -463,6 +1170,12 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
             glb2* dst = (glb2*)(z + pl.U0 + (size_t)gl[l] * NU);
             for (int e = tid; e < cnt * (NU / 2); e += BS) dst[e] = ld2(U + off * NU + 2 * e);
         });
+    }
+    if constexpr (CPF) {
+        wg_stamp(pl, 3);
+        if (work && !(kDiag && (pl.fault & 64)))
+            cp_phase<NX, NU, BX, BX>(*ca, *bfp, alpha, pl.X0, pl.U0, R0, deepest, XD, XL, U, CPA, SL,
+                                     kDiag ? pl.stamps : nullptr, pl.nblk);
     }
     if (top && tid == 0) st_u32(pl.sync, tag);  // every workgroup has read the epoch
 }
@@ -506,6 +1219,43 @@ k_dr(DrPlan pl, Bufs bf, int zsel, const Ctl* ctl, ChkArg ck) {
         if (L == lc.value)
             tier_body<NX, NU, C, BS, (LMAX <= 4 ? 1 : (C == 2 ? 4 : 2)), lc.value>(pl, k, o, z, tag, done == 0, stp, s_ok, sm);
     });
+    stamp(pl, stp);
+    stamp_flush(pl, stp, k, o);
+    wg_stamp(pl, 2);
+}
+
+// k_drc: k_dr's sweep with each subtree's CP families behind its forward sweep (every tier of 4
+// levels, binary trees at nx / nu = 20 / 8; the host checks the plan). One launch per CP
+// iteration; the extra workgroup runs the previous iteration's stopping test (its residual rows
+// are the other of the two alternating row sets, ck.part).
+template <int NX, int NU, int C, int BX>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
+k_drc(DrPlan pl, DrcArg ca, Bufs bf, ChkArg ck) {
+    extern __shared__ __attribute__((aligned(16))) double smem_[];
+    __shared__ Stamps stp;
+    __shared__ int s_ok;
+    const int tid = threadIdx.x;
+    if (ck.on && (int)blockIdx.x == pl.nblk) {  // the previous CP iteration's stopping test
+        if (tid < 64) cp_check_wave(ck);
+        return;
+    }
+    if (tid == 0) {
+        stp.n = 0;
+        s_ok = 1;
+    }
+    const unsigned long long sw = sload_pair(pl.sync);
+    const unsigned err = (unsigned)(sw >> 32);
+    const unsigned tag = (unsigned)sw + 1u;
+    const int done = ca.ctl->done;
+    const double alpha = ca.ctl->alpha;  // the CP step size, read at the start (not on the CP path)
+    stamp(pl, stp);
+    wg_stamp(pl, 0);
+    if (err) return;
+    int k, o;
+    role(pl, k, o);
+    glbd* z = pick3(bf, 1);
+    if (pl.t[k].L == 4)
+        tier_body<NX, NU, C, 512, 1, 4, BX>(pl, k, o, z, tag, done == 0, stp, s_ok, (ldsd*)smem_, &ca, &bf, alpha);
     stamp(pl, stp);
     stamp_flush(pl, stp, k, o);
     wg_stamp(pl, 2);
@@ -563,5 +1313,32 @@ void dr_launch(const DrPlan& pl, int nx, int nu, size_t lds, Bufs bf, int zsel, 
     }
 }
 const char* dr_name(int nx, int nu) { return nx == 20 && nu == 8 ? "k_dr<20, 8>" : "k_dr"; }
+
+bool drc_supported(int nx, int nu, int C) { return nx == 20 && nu == 8 && C == 2; }
+size_t drc_lds(int nx, int nu, int C) { return dr_lds(nx, nu, C, 4) + 8 * (size_t)kDrcCpa; }
+int drc_occupancy(size_t lds) {
+    int nb = 0;
+    const void* kf = (const void*)k_drc<20, 8, 2, 1>;
+    (void)hipFuncSetAttribute(kf, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kf, 512, lds) != hipSuccess) return 0;
+    int nb2 = 0;
+    const void* kf2 = (const void*)k_drc<20, 8, 2, 2>;
+    (void)hipFuncSetAttribute(kf2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, kf2, 512, lds) != hipSuccess) return 0;
+    return nb < nb2 ? nb : nb2;
+}
+void drc_launch(const DrPlan& pl, const DrcArg& a, size_t lds, Bufs bf, const Ctl* ctl, ChkArg ck, hipStream_t s) {
+    (void)ctl;
+    const int grid = pl.nblk + (ck.on ? 1 : 0);
+    if (a.box == 1) {
+        (void)hipFuncSetAttribute((const void*)k_drc<20, 8, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        k_drc<20, 8, 2, 1><<<grid, 512, lds, s>>>(pl, a, bf, ck);
+    } else {
+        (void)hipFuncSetAttribute((const void*)k_drc<20, 8, 2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        k_drc<20, 8, 2, 2><<<grid, 512, lds, s>>>(pl, a, bf, ck);
+    }
+}
+const char* drc_name() { return "k_drc<20, 8, 2>"; }
+bool dr_diag_build() { return kDiag; }
 
 }  // namespace raocp

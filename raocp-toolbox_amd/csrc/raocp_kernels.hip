@@ -796,8 +796,9 @@ __global__ void k_zero_idx(double* __restrict__ x, const int* __restrict__ idx, 
 }
 
 // end of iteration: record residuals, stopping test (solver.py:137-161)
+// nanbit: as ChkArg::nanbit (0: the CP kernels raise bit 0 themselves)
 __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, const double* __restrict__ part,
-                                                      int rows) {
+                                                      int rows, int nanbit) {
     __shared__ double s_m[6][kBlock];
     if (ctl->done) return;
     double m[6] = {0, 0, 0, 0, 0, 0};
@@ -814,6 +815,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, con
     const int k = ctl->k;
     for (int q = 0; q < 6; ++q) hist[(size_t)k * 6 + q] = s_m[q][0];
     const double err = nmax(nmax(s_m[0][0], s_m[1][0]), s_m[2][0]);  // NaN: not converged
+    if (ctl->flags & nanbit) ctl->flags |= 1;
     if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
         ctl->done = 1;
         ctl->final_k = k;

@@ -236,6 +236,9 @@ def test_cp5_leaf_forms_agree(case):
     mk = (lambda: core.Cache(prob, dtype=dt)) if dt else (lambda: core.Cache(prob))
     a = _with_env({"RAOCP_CP5_LPF": "1"}, mk)
     b = _with_env({"RAOCP_CP5_LPF": "0"}, mk)
+    # each context reads the switch at its creation (not once per process)
+    assert a.native.kernel_info(12).startswith("leaf_pf=1")
+    assert b.native.kernel_info(12).startswith("leaf_pf=0")
     alpha = 0.999 / a.native.step_size(rtol=1e-7 if dt else 1e-14)
     K = 14 if case == "c4" else 30
     ra = _run(a, r["x0"], K, alpha)

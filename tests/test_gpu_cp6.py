@@ -25,6 +25,13 @@ from helpers import rel_err, trace_rel_err
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _pair_loop(monkeypatch):
+    """These tests pin k_cp6 itself in the CP loop: RAOCP_DRC=0 keeps the pair k_dr + k_cp6
+    where the fused launch k_drc would replace it (config 2; tests/test_gpu_drc.py)."""
+    monkeypatch.setenv("RAOCP_DRC", "0")
+
+
 def _with_env(env, fn):
     old = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})

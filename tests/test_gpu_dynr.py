@@ -100,13 +100,16 @@ def test_dr_invalid_cut_list_is_rejected():
         _with_env({"RAOCP_DR_CUTS": "2"}, lambda: core.Cache(prob))
 
 
-def test_dr_cp_loop_matches_tiers_and_oracle():
+@pytest.mark.parametrize("drc", ["1", "0"])
+def test_dr_cp_loop_matches_tiers_and_oracle(drc):
     """30 CP iterations (a full 24-iteration graph batch plus a remainder; the deferred
-    stopping test rides on k_dr), tol = 0."""
+    stopping test rides on k_dr), tol = 0; the loop's launch k_drc (k_dr with the CP families
+    fused) and the pair k_dr + k_cp6 (RAOCP_DRC=0)."""
     from oracle.raocp_oracle import OracleProblem
     r = recipe_config(2)
     tree, prob = build_problem(r)
-    dr = core.Cache(prob)
+    dr = _with_env({"RAOCP_DRC": drc}, lambda: core.Cache(prob))
+    assert dr.native.kernel_info(11) == ("k_drc<20, 8, 2>" if drc == "1" else "")
     tiers = _with_env(TIERS, lambda: core.Cache(prob))
     assert dr.native.kernel_info(9).startswith("k_dr<")
     alpha = 0.999 / dr.native.step_size()
@@ -122,14 +125,15 @@ def test_dr_cp_loop_matches_tiers_and_oracle():
     assert trace_rel_err(e1, err_o) <= 1e-8 and rel_err(z1, z_o) <= 1e-10
 
 
+@pytest.mark.parametrize("drc", ["1", "0"])
 @pytest.mark.parametrize("iters,stop", [(1, None), (24, None), (30, None), (60, True)])
-def test_dr_deferred_stopping_test_matches_eager(iters, stop):
-    """The deferred stopping test (an extra workgroup of k_dr) against k_cp_check after
-    every iteration (RAOCP_DEFER_CHECK=0): bit for bit, early stops included."""
+def test_dr_deferred_stopping_test_matches_eager(iters, stop, drc):
+    """The deferred stopping test (an extra workgroup of k_dr / k_drc) against k_cp_check
+    after every iteration (RAOCP_DEFER_CHECK=0): bit for bit, early stops included."""
     r = recipe_config(2)
     tree, prob = build_problem(r)
-    dfr = core.Cache(prob)
-    eag = _with_env({"RAOCP_DEFER_CHECK": "0"}, lambda: core.Cache(prob))
+    dfr = _with_env({"RAOCP_DRC": drc}, lambda: core.Cache(prob))
+    eag = _with_env({"RAOCP_DEFER_CHECK": "0", "RAOCP_DRC": drc}, lambda: core.Cache(prob))
     assert dfr.native.kernel_info(9).startswith("k_dr<")
     alpha = 0.999 / dfr.native.step_size()
     tol = 0.0
@@ -178,3 +182,21 @@ def test_dr_forced_timeout_is_reported_quickly():
     # a healthy context on the same device is unaffected
     good = core.Cache(prob)
     assert rel_err(_project(good, r, zz), _project(_with_env(TIERS, lambda: core.Cache(prob)), r, zz)) <= 1e-13
+
+
+def test_drc_forced_timeout_in_the_cp_loop_is_reported():
+    """RAOCP_DR_FAULT=1 in the fused CP loop (k_drc): the hand-off wait times out, every later
+    launch of the batch leaves at its start (the error word), and cp_run raises within a
+    fraction of a second per batch; a healthy context afterwards runs normally."""
+    r = recipe_config(2)
+    tree, prob = build_problem(r)
+    bad = _with_env({"RAOCP_DR_FAULT": "1", "RAOCP_FUSE_TIMEOUT_MS": "5"}, lambda: core.Cache(prob))
+    assert bad.native.kernel_info(11) == "k_drc<20, 8, 2>"
+    alpha = 0.999 / bad.native.step_size()
+    t0 = time.perf_counter()
+    with pytest.raises(Exception, match="timed out"):
+        bad.native.cp_run(r["x0"], 10, 0.0, alpha)
+    assert time.perf_counter() - t0 < 1.0
+    good = core.Cache(prob)
+    st, err, _ = good.native.cp_run(r["x0"], 10, 0.0, alpha)
+    assert st == 1 and err.shape == (11, 3) and np.all(np.isfinite(err))

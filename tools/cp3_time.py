@@ -19,12 +19,14 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
     reps = {2: 400, 3: 100, 4: 100, 5: 20}[cfg]
     t10 = nat.op_bench(10, reps)
     t9 = nat.op_bench(9, max(1, reps // 2))
+    t11 = nat.op_bench(11, reps) if nat.kernel_info(11) else 0.0  # the fused launch (k_drc)
     alpha = 0.999 / nat.step_size(rtol=1e-7 if cfg == 5 else 1e-14)
     K = {2: 480, 3: 120, 4: 120, 5: 24}[cfg]
     ms = nat.cp_bench(r["x0"], K, alpha)
     var = ",".join(f"{k[6:]}={v}" for k, v in sorted(os.environ.items()) if k.startswith("RAOCP_")) or "default"
     print(f"config {cfg} {var:12s} {nat.kernel_info(10):40s} {nat.kernel_info(9)[:34]:34s} "
-          f"cp {1e3 * t10:8.1f} us  dyn {1e3 * t9:8.1f} us  loop {1e3 * ms / K:8.1f} us/it", flush=True)
+          f"cp {1e3 * t10:8.1f} us  dyn {1e3 * t9:8.1f} us  fused {1e3 * t11:8.1f} us  loop {1e3 * ms / K:8.1f} us/it",
+          flush=True)
     sys.exit(0)
 cfgs = sys.argv[1:] or ["2", "4", "5"]
 for cfg in cfgs:

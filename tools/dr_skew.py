@@ -25,7 +25,7 @@ for rep in range(reps):
     st = cache.native.debug_dyn_stamps(4096).astype(np.int64)
     if rep < reps - 3:
         continue
-    w = st[1024:1024 + 3 * 273].reshape(273, 3)
+    w = st[1024:1024 + 4 * 273].reshape(273, 4)[:, :3]
     t0 = w[w > 0].min()
     w = (w - t0) * 10
     for name, b0, n in tiers:
