@@ -7,7 +7,6 @@
 #include "raocp_dynr.h"
 #include "raocp_cp4.h"
 #include "raocp_cp5.h"
-#include "raocp_dyn4.h"
 #include "../../include/raocp_hip.h"
 
 #include <dlfcn.h>
@@ -99,10 +98,6 @@ struct raocp_ctx {
     std::vector<raocp::Dy3Stage> d3own;  // a shard's stages (owned parent ranges below its cut)
     int d3ts = 0;  // the top stages k_dy3_top_back / k_dy3_top_fwd run in one workgroup (0: none)
     size_t d3nb = 0, d3nf = 0;  // doubles per stage image (backward, forward)
-    bool dy4 = false;           // the same sweep in ONE launch of dataflow tile tasks (raocp_dyn4.hip;
-                                // opt-in RAOCP_DY4=1)
-    raocp::Dy4Plan dy4p{};
-    size_t dy4_lds = 0;
     int wsz = 8;                 // bytes per scalar of the iterate
     hipStream_t stream = nullptr;
     Dev dev{};
@@ -162,6 +157,7 @@ struct raocp_ctx {
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
     Ctl* ctl = nullptr;
     Ctl* h_ctl = nullptr;        // pinned host mirror
+    unsigned* h_err = nullptr;   // pinned host copy of a hand-off sweep's error word (raocp_cp_bench)
     double* hist = nullptr;
     size_t hist_rows = 0;
     double* cur_z = nullptr;     // the Cache's current primal / dual
@@ -729,13 +725,6 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
                          ck ? *ck : raocp::ChkArg{nullptr, nullptr, nullptr, 0, 0}, c->stream);
         return;
     }
-    if (c->dy4 && c->sh_S == 0 && part == 0) {  // the one-launch dataflow sweep (raocp_dyn4.hip)
-        double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
-        raocp::dy4_launch(c->dy4p, c->f32, c->nx, c->nu, c->dev, ctl,
-                          ck ? *ck : raocp::ChkArg{nullptr, nullptr, nullptr, 0, 0}, z, c->Q2, c->Dd2, c->x0,
-                          c->dy4_lds, c->stream);
-        return;
-    }
     if (c->dyn3) {
         double* z = zsel % 3 == 0 ? bf.z0 : (zsel % 3 == 1 ? bf.z1 : bf.z2);
         launch_dyn3(c, z, ctl, ck, part);
@@ -750,21 +739,15 @@ void launch_dynamics(raocp_ctx* c, raocp::Bufs bf, int zsel, const Ctl* ctl, int
     dispatch(c->nx, c->nu, DynOp{}, c, bf, zsel, ctl, part, ck);
 }
 
+// the device word a hand-off sweep sets when a wait times out (nullptr: no such sweep)
+const unsigned* err_word(const raocp_ctx* c) {
+    if (c->dr && c->sh_S == 0) return c->drp.sync + 1;
+    if (c->dyn_split && c->fuse_sync) return (const unsigned*)c->fuse_sync + 1;
+    return nullptr;
+}
 // the fused sweep's error word (a hand-off wait timed out, raocp_dynf.hip): checked after
 // every synchronised run that may have launched it; the context is unusable afterwards
 int fuse_err(raocp_ctx* c) {
-    if (c->dy4 && c->sh_S == 0) {
-        unsigned e = 0;
-        HIPCHK(hipMemcpy(&e, c->dy4p.sync + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
-        if (e) {
-            int nfl = c->dy4p.ftop + 1;
-            HIPCHK(hipMemset(c->dy4p.sync, 0, 4 * sizeof(unsigned)));
-            HIPCHK(hipMemset(c->dy4p.flags, 0, (size_t)nfl * sizeof(unsigned)));
-            return fail(RAOCP_ERR_STATE, "dynamics sweep: a tile task's wait timed out (k_dy4); "
-                                         "RAOCP_DY4=0 selects the per-stage launches");
-        }
-        return RAOCP_OK;
-    }
     if (c->dr && c->sh_S == 0) {
         unsigned e = 0;
         HIPCHK(hipMemcpy(&e, c->drp.sync + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
@@ -785,99 +768,6 @@ int fuse_err(raocp_ctx* c) {
     if (e) HIPCHK(hipMemset(c->fuse_sync, 0, c->fuse_words * sizeof(unsigned)));  // clean protocol state
     if (e) return fail(RAOCP_ERR_STATE, "dynamics sweep: a workgroup hand-off timed out (k_dyn_up / k_dyn_down); "
                                         "RAOCP_DYN_SPLIT=0 selects the tier launches");
-    return RAOCP_OK;
-}
-
-// ---- the one-launch dataflow sweep (raocp_dyn4.hip) ------------------------------------------
-// The plan over k_dy3's stages and images (c->d3st, c->d3img_b / f): the top stages are the
-// leading stages of at most two tiles (one workgroup runs them back to back); every other
-// stage's tiles are tasks of the launch (4 per task on wide stages). With RAOCP_DY4=1, when
-// the grid (occupancy x CUs, one workgroup kept for the stopping test) is resident;
-// RAOCP_DY4_TS=t forces the top stages [0, t).
-int dy4_setup(raocp_ctx* c) {
-    const int C = c->unif_branch, N = (int)c->d3st.size();
-    if (N < 2 || N > raocp::kDy4MaxStages || !raocp::dy4_supported(c->f32, c->nx, c->nu, C)) return RAOCP_OK;
-    // opt-in (RAOCP_DY4=1): measured slower than the per-stage launches at configs 4 / 5
-    // (profiles/r05/cp_time_dy4.log: 145-170 vs 113 us, 336-341 vs 195 us)
-    const char* on = getenv("RAOCP_DY4");
-    if (!on || !atoi(on)) return RAOCP_OK;
-    raocp::Dy4Plan& p = c->dy4p;
-    memset(&p, 0, sizeof(p));
-    p.N = N;
-    p.C = C;
-    for (int t = 0; t < N; ++t) {
-        p.i0[t] = c->d3st[t].i0;
-        p.nt[t] = (c->d3st[t].i1 - c->d3st[t].i0 + 15) / 16;
-    }
-    p.i0[N] = c->d3st[N - 1].i1;
-    int ts = 0;
-    while (ts < N - 1 && p.nt[ts] <= 2) ++ts;
-    ts = std::max(ts, 1);
-    if (const char* e = getenv("RAOCP_DY4_TS")) ts = std::min(std::max(atoi(e), 1), N - 1);
-    p.ts = ts;
-    // stages of at least `wide` tiles run tasks of 4 tiles, a wave per tile (the slot sums in
-    // the MFMA registers); the others a tile per task, a wave per slot (RAOCP_DY4_WIDE)
-    int wide = 64;
-    if (const char* e = getenv("RAOCP_DY4_WIDE")) wide = std::max(1, atoi(e));
-    for (int t = 0; t < N; ++t) {
-        p.wide[t] = t >= ts && p.nt[t] >= wide;
-        p.nk[t] = p.wide[t] ? (p.nt[t] + 3) / 4 : p.nt[t];
-    }
-    int task = 0;
-    for (int t = N - 1; t >= ts; --t) {
-        p.tb[t] = task;
-        task += p.nk[t];
-    }
-    p.ttop = task++;
-    for (int t = ts; t < N; ++t) {
-        p.tf[t] = task;
-        task += p.nk[t];
-    }
-    p.ntask = task;
-    int fl = 0;
-    for (int t = ts; t < N; ++t) {
-        p.fb[t] = fl;
-        fl += p.nt[t];
-    }
-    for (int t = ts; t < N; ++t) {
-        p.ff[t] = fl;
-        fl += p.nt[t];
-    }
-    p.ftop = fl++;
-    p.same_kinds = 1;
-    for (int t = 1; t < N; ++t)
-        for (int k = 0; k < C; ++k) p.same_kinds &= c->d3st[t].kind[k] == c->d3st[0].kind[k];
-    p.bimg = c->d3img_b;
-    p.fimg = c->d3img_f;
-    p.bstride = (int)c->d3nb;
-    p.fstride = (int)c->d3nf;
-    p.X0 = c->dev.X0;
-    p.U0 = c->dev.U0;
-    const size_t lds = raocp::dy4_lds(c->f32, c->nx, c->nu, C);
-    const int occ = lds <= 160 * 1024 ? raocp::dy4_occupancy(c->f32, c->nx, c->nu, C, lds) : 0;
-    int dev = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        cus <= 0)
-        cus = 256;
-    if (occ < 1) return RAOCP_OK;
-    p.nwg = std::max(1, std::min(p.ntask, occ * cus - 1));  // resident, with room for the stopping test
-    if (const char* e = getenv("RAOCP_DY4_GRID")) p.nwg = std::max(1, std::min(p.nwg, atoi(e)));
-    int rc;
-    unsigned *fw = nullptr, *sy = nullptr;
-    if ((rc = c->alloc(&fw, (size_t)fl)) || (rc = c->alloc(&sy, 4))) return rc;
-    HIPCHK(hipMemset(fw, 0, (size_t)fl * sizeof(unsigned)));
-    HIPCHK(hipMemset(sy, 0, 4 * sizeof(unsigned)));
-    p.flags = fw;
-    p.sync = sy;
-    long long ms = 1000;  // a wait normally lasts microseconds
-    if (const char* e = getenv("RAOCP_FUSE_TIMEOUT_MS")) ms = std::max(1, atoi(e));
-    p.timeout = ms * 100000LL;  // 100 MHz ticks
-    if (const char* e = getenv("RAOCP_DY4_FAULT")) p.fault = atoi(e) & 1;
-    c->dy4 = true;
-    c->dy4_lds = lds;
-    if (getenv("RAOCP_DYN_VERBOSE"))
-        fprintf(stderr, "[raocp] dataflow sweep: %d stages, top [0,%d), %d tasks on %d workgroups (occupancy %d), LDS %zu B\n",
-                N, ts, p.ntask, p.nwg, occ, lds);
     return RAOCP_OK;
 }
 
@@ -1542,8 +1432,6 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             auto b = [](bool v) { return std::string(v ? "true" : "false"); };
             if (c->dr && c->sh_S == 0) {
                 return std::string(raocp::dr_name(c->nx, c->nu)) + " x1";
-            } else if (c->dy4 && c->sh_S == 0) {
-                return raocp::dy4_name(c->f32, c->nx, c->nu);
             } else if (c->dyn3) {  // a backward and a forward launch per nonleaf stage below the top
                 const int ts = c->sh_S == 0 ? c->d3ts : 0;
                 for (int t = ts; t < c->N; ++t) add("k_dy3_back<" + T + ", " + nn + ">");
@@ -2289,7 +2177,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         }
         if (c->dyn3) {
             if ((rc = c->alloc(&c->Q2, (size_t)n * nx)) || (rc = c->alloc(&c->Dd2, (size_t)m * nu)) ||
-                (rc = dyn3_images(c)) || (rc = dy4_setup(c)))
+                (rc = dyn3_images(c)))
                 return bail(rc);
             c->dyn32 = c->f32;
         }
@@ -2856,6 +2744,7 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         (rc = c->alloc(&c->tmpD, c->D)) || (rc = c->alloc(&c->part, 1024)) || (rc = c->alloc(&c->scal, 8)))
         return bail(rc);
     if (hipHostMalloc((void**)&c->h_ctl, sizeof(Ctl), 0) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "hipHostMalloc"));
+    if (hipHostMalloc((void**)&c->h_err, 4 * sizeof(unsigned), 0) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "hipHostMalloc"));
     {
         double* zp = nullptr;
         if ((rc = c->alloc(&zp, 16))) return bail(rc);
@@ -3042,6 +2931,7 @@ void raocp_ctx_destroy(raocp_ctx* c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
+    if (c->h_err) (void)hipHostFree(c->h_err);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -3450,10 +3340,15 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     if (rem && (rc = launch_batch(c, rem))) return rc;
     if (c->comm && (rc = enqueue_shard_tail(c))) return rc;
     HIPCHK(hipEventRecord(e1, c->stream));
-    HIPCHK(hipEventSynchronize(e1));
+    // the control block and the hand-off sweep's error word come back behind the last
+    // iteration on the same stream: one synchronisation for the timed call
+    HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+    const unsigned* ew = err_word(c);
+    if (ew) HIPCHK(hipMemcpyAsync(c->h_err, ew, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
-    HIPCHK(hipMemcpy(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost));
-    if (int fe = fuse_err(c)) return fe;  // a timed-out hand-off skipped its arithmetic
+    if (ew && *c->h_err)
+        if (int fe = fuse_err(c)) return fe;  // a timed-out hand-off skipped its arithmetic
     if (c->h_ctl->final_k != iters - 1) return fail(RAOCP_ERR_STATE, "bench did not run the requested iterations");
     c->cur_z = c->Z[iters % 3];
     c->cur_e = c->E[iters % 2];

@@ -411,102 +411,113 @@ struct Cps {
 static_assert(Cps::UB + 256 <= 2 * Cps::SLOT && 6 * Cps::SS <= 2 * Cps::SLOT, "slots 0-1");
 static_assert(Cps::KPS + 272 <= 3 * Cps::SLOT && Cps::RED + 96 <= 4 * Cps::SLOT, "slot tails");
 
-// 4-B LDS-DMA gather of n doubles into dst: element e from src(e) (a global address)
-template <class F>
-__device__ __forceinline__ void gather(ldsd* dst, int n, F src) {
-    typedef const __attribute__((address_space(1))) unsigned gcu;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    for (int c0 = wave * 64; c0 < 2 * n; c0 += nw * 64) {
-        const int f = c0 + lane;
-        if (f < 2 * n) __builtin_amdgcn_global_load_lds((gcu*)src(f >> 1) + (f & 1), (ldsu*)dst + c0, 4, 0, 0);
-    }
-}
-
+// The CP operands through registers: every lane loads up to four pairs of the region (pair f =
+// doubles 2 f, 2 f + 1 of Cpa, f = tid + 512 s) with 8-byte loads at valid addresses (zeros from
+// the zero page where a row is dead), before the wait they hide behind; once they have landed,
+// the pairs go to LDS with 16-B stores (cpa_commit). 16 VGPRs across the wait, 8 load
+// instructions per lane, no per-dword DMA.
+constexpr int kCpaPairs = Cpa::N / 2;
+constexpr int kCpaSlots = (kCpaPairs + 511) / 512;
+struct CpaStage {
+    d2v v[kCpaSlots];
+};
 template <int NX, int NU, int BXN>
-__device__ __forceinline__ void cpa_gather(const DrcArg& a, const DrPlan& pl, const Bufs& bf, int R0, bool deepest,
-                                           ldsd* A) {
+__device__ __forceinline__ void cpa_issue(const DrcArg& a, const DrPlan& pl, const Bufs& bf, int R0, bool deepest,
+                                          CpaStage& st) {
     const double* pz = bf.z0;  // p
     const double* zp = bf.z1;  // z+ (y, tau, s: not written by this launch)
     const double* dd = bf.e0;  // eta
     const double* zpg = pl.zpage;
-    gather(A + Cpa::PX, 16 * NX, [=](int e) {
-        const int r = e / NX;
-        return r < 15 ? pz + pl.X0 + (size_t)gnode(R0, r) * NX + (e - r * NX) : zpg;
-    });
-    gather(A + Cpa::PU, 16 * NU, [=](int e) {
-        const int r = e / NU;
-        return r < 15 ? pz + pl.U0 + (size_t)gnode(R0, r) * NU + (e - r * NU) : zpg;
-    });
-    gather(A + Cpa::D3, 32 * NX, [=](int e) {
-        const int r = e / NX;
-        return r < 30 ? dd + a.E3 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NX + (e - r * NX) : zpg;
-    });
-    gather(A + Cpa::D4, 32 * NU, [=](int e) {
-        const int r = e / NU;
-        return r < 30 ? dd + a.E4 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NU + (e - r * NU) : zpg;
-    });
-    gather(A + Cpa::SC, 32 * 16, [=](int e) {
-        const int r = e >> 4, q = e & 15;
-        if (r >= 30) return zpg;
-        const int j = gnode(R0, r + 1);
-        switch (q) {
-            case 0: return dd + a.E5 + j;
-            case 1: return dd + a.E6 + j;
-            case 2: return zp + a.T0 + j;
-            case 3: return pz + a.T0 + j;
-            default: break;
-        }
-        if ((deepest && r + 1 >= 15) || q == 15) return zpg;  // a leaf child: no eta2
-        switch (q) {
-            case 4: return zp + a.S0 + j;
-            case 5: return pz + a.S0 + j;
-            case 6: return dd + a.E2 + j;
-            case 7: return a.cond + 1 + 2 * j;
-            case 8: return a.cond + 2 + 2 * j;
-            case 9: return zp + a.Y0 + 5 * j;
-            case 10: return zp + a.Y0 + 5 * j + 1;
-            case 11: return zp + a.Y0 + 5 * j + 4;
-            case 12: return pz + a.Y0 + 5 * j;
-            case 13: return pz + a.Y0 + 5 * j + 1;
-            default: return pz + a.Y0 + 5 * j + 4;
-        }
-    });
-    gather(A + Cpa::PS, 16 * 24, [=](int e) {
-        const int r = e / 24, q = e - r * 24;
-        if (r >= 15 || q >= 21) return zpg;
-        const int g = gnode(R0, r);
-        if (q < 5) return zp + a.Y0 + 5 * g + q;
-        if (q < 10) return pz + a.Y0 + 5 * g + (q - 5);
-        if (q < 15) return dd + a.E1 + 5 * g + (q - 10);
-        switch (q) {
-            case 15: return zp + a.S0 + g;
-            case 16: return pz + a.S0 + g;
-            case 17: return dd + a.E2 + g;
-            case 18: return a.cond + 1 + 2 * g;
-            case 19: return a.cond + 2 + 2 * g;
-            default: return a.alpha_r + g;
-        }
-    });
-    if (BXN == 1)
-        gather(A + Cpa::D7, 16 * (NX + NU), [=](int e) {
-            const int r = e / (NX + NU);
-            return r < 15 ? dd + a.E7 + (size_t)gnode(R0, r) * (NX + NU) + (e - r * (NX + NU)) : zpg;
-        });
-    if (deepest) {
-        const int l0 = 16 * R0 + 15;  // the first leaf of the subtree
-        gather(A + Cpa::LP, 16 * NX, [=](int e) { return pz + pl.X0 + (size_t)l0 * NX + e; });
-        gather(A + Cpa::D11, 16 * NX, [=](int e) { return dd + a.E11 + a.m + (size_t)(l0 - a.m) * NX + e; });
-        if (a.box == 1)
-            gather(A + Cpa::D14, 16 * NX, [=](int e) { return dd + a.E14 + a.m + (size_t)(l0 - a.m) * NX + e; });
-        gather(A + Cpa::LS, 64, [=](int e) {
-            const int l = l0 + (e >> 2);
-            switch (e & 3) {
-                case 0: return dd + a.E12 + l;
-                case 1: return dd + a.E13 + l;
-                case 2: return zp + a.S0 + l;
-                default: return pz + a.S0 + l;
+    const int l0 = 16 * R0 + 15;  // the first leaf of the subtree (deepest tier)
+    _Pragma("unroll") for (int sl = 0; sl < kCpaSlots; ++sl) {
+        const int f = threadIdx.x + 512 * sl, e = 2 * f;
+        const double* s0 = zpg;
+        const double* s1 = zpg;
+        bool pair = true;  // the two doubles are adjacent in global memory (s1 = s0 + 1)
+        if (e < Cpa::PU) {
+            const int r = e / NX;
+            if (r < 15) s0 = pz + pl.X0 + (size_t)gnode(R0, r) * NX + (e - r * NX);
+        } else if (e < Cpa::D3) {
+            const int q = e - Cpa::PU, r = q / NU;
+            if (r < 15) s0 = pz + pl.U0 + (size_t)gnode(R0, r) * NU + (q - r * NU);
+        } else if (e < Cpa::D4) {
+            const int q = e - Cpa::D3, r = q / NX;
+            if (r < 30) s0 = dd + a.E3 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NX + (q - r * NX);
+        } else if (e < Cpa::SC) {
+            const int q = e - Cpa::D4, r = q / NU;
+            if (r < 30) s0 = dd + a.E4 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NU + (q - r * NU);
+        } else if (e < Cpa::PS) {
+            // child scalars (Cpa::SC): eta5, eta6 | tau z+, p | a nonleaf child's s z+, p | eta2,
+            // cond k=0 | cond k=1, y0 z+ | y1 z+, y4 z+ | y0 p, y1 p | y4 p, -
+            pair = false;
+            const int q = e - Cpa::SC, r = q >> 4, c = q & 15;
+            if (r < 30) {
+                const int j = gnode(R0, r + 1);
+                const bool nl = !(deepest && r + 1 >= 15);
+                switch (c) {
+                    case 0: s0 = dd + a.E5 + j; s1 = dd + a.E6 + j; break;
+                    case 2: s0 = zp + a.T0 + j; s1 = pz + a.T0 + j; break;
+                    case 4: if (nl) { s0 = zp + a.S0 + j; s1 = pz + a.S0 + j; } break;
+                    case 6: if (nl) { s0 = dd + a.E2 + j; s1 = a.cond + 1 + 2 * j; } break;
+                    case 8: if (nl) { s0 = a.cond + 2 + 2 * j; s1 = zp + a.Y0 + 5 * j; } break;
+                    case 10: if (nl) { s0 = zp + a.Y0 + 5 * j + 1; s1 = zp + a.Y0 + 5 * j + 4; } break;
+                    case 12: if (nl) { s0 = pz + a.Y0 + 5 * j; s1 = pz + a.Y0 + 5 * j + 1; } break;
+                    default: if (nl) s0 = pz + a.Y0 + 5 * j + 4; break;
+                }
             }
-        });
+        } else if (e < Cpa::D7) {
+            // parent scalars (Cpa::PS): y z+ (5), y p (5), eta1 (5), s z+, s p, eta2, cond (2), alpha, -
+            pair = false;
+            const int q = e - Cpa::PS, r = q / 24, c = q - r * 24;
+            if (r < 15) {
+                const int g = gnode(R0, r);
+                auto src = [&](int cc) -> const double* {
+                    if (cc < 5) return zp + a.Y0 + 5 * g + cc;
+                    if (cc < 10) return pz + a.Y0 + 5 * g + (cc - 5);
+                    if (cc < 15) return dd + a.E1 + 5 * g + (cc - 10);
+                    switch (cc) {
+                        case 15: return zp + a.S0 + g;
+                        case 16: return pz + a.S0 + g;
+                        case 17: return dd + a.E2 + g;
+                        case 18: return a.cond + 1 + 2 * g;
+                        case 19: return a.cond + 2 + 2 * g;
+                        case 20: return a.alpha_r + g;
+                        default: return zpg;
+                    }
+                };
+                s0 = src(c);
+                s1 = src(c + 1);
+            }
+        } else if (e < Cpa::LP) {
+            const int q = e - Cpa::D7, r = q / (NX + NU);
+            if (BXN == 1 && r < 15) s0 = dd + a.E7 + (size_t)gnode(R0, r) * (NX + NU) + (q - r * (NX + NU));
+        } else if (e < Cpa::D11) {
+            if (deepest) s0 = pz + pl.X0 + (size_t)l0 * NX + (e - Cpa::LP);
+        } else if (e < Cpa::D14) {
+            if (deepest) s0 = dd + a.E11 + a.m + (size_t)(l0 - a.m) * NX + (e - Cpa::D11);
+        } else if (e < Cpa::LS) {
+            if (deepest && a.box == 1) s0 = dd + a.E14 + a.m + (size_t)(l0 - a.m) * NX + (e - Cpa::D14);
+        } else if (e < Cpa::N) {
+            pair = false;
+            const int q = e - Cpa::LS, ll = l0 + (q >> 2);
+            if (deepest) {
+                if ((q & 3) == 0) {
+                    s0 = dd + a.E12 + ll;
+                    s1 = dd + a.E13 + ll;
+                } else {
+                    s0 = zp + a.S0 + ll;
+                    s1 = pz + a.S0 + ll;
+                }
+            }
+        }
+        if (pair) s1 = s0 == zpg ? zpg : s0 + 1;
+        st.v[sl] = d2v{*(const glbd*)s0, *(const glbd*)s1};
+    }
+}
+__device__ __forceinline__ void cpa_commit(ldsd* A, const CpaStage& st) {
+    _Pragma("unroll") for (int sl = 0; sl < kCpaSlots; ++sl) {
+        const int f = threadIdx.x + 512 * sl;
+        if (f < kCpaPairs) *(lds2*)(A + 2 * f) = st.v[sl];
     }
 }
 
@@ -534,10 +545,15 @@ __device__ __forceinline__ int cpos(int rt, int e) {
     return (threadIdx.x & 63) * (R / 4) + 4 * rt + e;
 }
 
+// a store of the CP step (stv false: timing probes of diagnostic builds skip them)
+__device__ __forceinline__ void gput(bool stv, glbp<double> b, unsigned o, double v) {
+    if (stv) *elw(b, o) = v;
+}
+
 template <int NX, int NU, int BXN, int BXL>
 __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double alpha_in, int X0, int U0, int R0,
                                          bool deepest, const ldsd* XD, const ldsd* XL, const ldsd* U, ldsd* A,
-                                         ldsd* SL, unsigned long long* dstamps, int nblk) {
+                                         ldsd* SL, unsigned long long* dstamps, int nblk, bool stv = true) {
     typedef double T;
     typedef MF<T>::v4 v4;
     constexpr int C = 2, RX = (NX + 15) / 16, RU = (NU + 15) / 16, G = 2 * C + 1, NQ = (G + 3) / 4;
@@ -649,12 +665,12 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             T x2;
             rs.fin(d2, v, fmax(v, T(0)), bb, e2A, x2);
             e2C = x2;
-            if (live && h == 0) *elw(eo, a.E2 + i) = e2A;
+            if (live && h == 0) gput(stv, eo, a.E2 + i, e2A);
         }
         const T e2W = d2 - e2A;
         if (live && i == 0 && h == 0) {
             // root s_0: L^T -> eta2_0, then the relaxation prox s_0 -= alpha (cache.py:253-257)
-            *elw(out, a.S0) = (zs - alpha * e2A) - alpha;
+            gput(stv, out, a.S0, (zs - alpha * e2A) - alpha);
             rs.account(pps, zs, e2W, e2C);
         }
         _Pragma("unroll") for (int t = 0; t < NQ; ++t) {
@@ -664,7 +680,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             const T v = (dv + alpha * (T(2) * zy - py)) * ra;
             T ep, x2;
             rs.fin(dv, v, q < 2 * C ? fmax(v, T(0)) : v, zy - py, ep, x2);
-            *elw(eo, a.E1 + yo + q) = ep;
+            gput(stv, eo, a.E1 + yo + q, ep);
             T bq = T(1);
             if (q < C) {
                 _Pragma("unroll") for (int kk = 0; kk < C; ++kk) if (kk == q) bq = cp[kk];
@@ -756,7 +772,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             sk[q] = ep;
             sk[SS + q] = d3[rt][e] - ep;
             sk[2 * SS + q] = x2;
-            if (live) *elw(eo, a.E3 + 1 + (j - 1) * NX + row_of<NX>(rt, e)) = ep;
+            if (live) gput(stv, eo, a.E3 + 1 + (j - 1) * NX + row_of<NX>(rt, e), ep);
         }
         _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
             if (!tok<NU>(rt, e)) continue;
@@ -766,17 +782,17 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             sk[q] = ep;
             sk[SS + q] = d4[rt][e] - ep;
             sk[2 * SS + q] = x2;
-            if (live) *elw(eo, a.E4 + 1 + (j - 1) * NU + row_of<NU>(rt, e)) = ep;
+            if (live) gput(stv, eo, a.E4 + 1 + (j - 1) * NU + row_of<NU>(rt, e), ep);
         }
         T ep5, x25, ep6, x26;
         rs.fin(d5, v5, so.first(v5), b5, ep5, x25);
         rs.fin(d6, v6, so.last(v6), b5, ep6, x26);
         if (live && h == 0) {
-            *elw(eo, a.E5 + j) = ep5;
+            gput(stv, eo, a.E5 + j, ep5);
             ks.tau[lo][k] = tz - alpha * (T(0.5) * (ep5 + ep6));
             rs.account(tp, tz, T(0.5) * ((d5 - ep5) + (d6 - ep6)), T(0.5) * (x25 + x26));
         }
-        if (live && h == 1) *elw(eo, a.E6 + j) = ep6;
+        if (live && h == 1) gput(stv, eo, a.E6 + j, ep6);
     } else if (wv == 2 && deepest) {
         // ================= the leaf tile (lane lo = leaf lo of the subtree; k_cp6's leaf waves)
         v4 lb[RX];
@@ -805,9 +821,9 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         if (h == 0) {
             ks.s[7 + (lo >> 1)][lo & 1] = sz - alpha * (T(0.5) * (ep12 + ep13));
             rs.account(sp, sz, T(0.5) * ((d12 - ep12) + (d13 - ep13)), T(0.5) * (x212 + x213));
-            *elw(eo, a.E12 + l) = ep12;
+            gput(stv, eo, a.E12 + l, ep12);
         }
-        if (h == 1) *elw(eo, a.E13 + l) = ep13;
+        if (h == 1) gput(stv, eo, a.E13 + l, ep13);
         T eA[RX][4];
         _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
             T ep = T(0), x2 = T(0);
@@ -816,7 +832,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
                 const int q = cpos<NX>(rt, e);
                 SL[Cps::LEW + q] = d11[rt][e] - ep;
                 SL[Cps::LEC + q] = x2;
-                *elw(eo, a.E11 + m + (l - m) * NX + row_of<NX>(rt, e)) = ep;
+                gput(stv, eo, a.E11 + m + (l - m) * NX + row_of<NX>(rt, e), ep);
             }
             eA[rt][e] = ep;
         }
@@ -836,7 +852,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
                     T ep, x2;
                     rs.fin(d14, v, box_sel(v, BX[2 * (NX + NU) + r], BX[2 * (NX + NU) + NX + r], nanf), lzv - lpv, ep, x2);
                     gA[rt][e] = ep;
-                    *elw(eo, a.E14 + m + (l - m) * NX + r) = ep;
+                    gput(stv, eo, a.E14 + m + (l - m) * NX + r, ep);
                 }
                 __builtin_amdgcn_sched_barrier(0);  // a row block at a time: bounded live operands
             }
@@ -848,7 +864,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         ld_lr<NX>(xl + lo * NX, true, lz);
         _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
             ox[rt][e] = lz[rt][e] - alpha * gA[rt][e];
-        st_rows_o<T, NX>(out, X0 + l * NX, true, ox);
+        if (stv) st_rows_o<T, NX>(out, X0 + l * NX, true, ox);
     }
     if (!(wv < 2 || (wv == 2 && deepest))) lds_sync();  // A2
     if (BXN == 1 && wv == 7) {
@@ -867,7 +883,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             T ep, x2;
             rs.fin(d7, v, box_sel(v, lv, hv, nanf), zv - pv, ep, x2);
             if (live) {
-                *elw(eo, a.E7 + i * (NX + NU) + r) = ep;
+                gput(stv, eo, a.E7 + i * (NX + NU) + r, ep);
                 A[Cpa::D7 + o] = ep;
                 A[Cpa::SDW + o] = d7 - ep;
                 A[Cpa::SDC + o] = x2;
@@ -914,10 +930,10 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             ld_lr<NU>(U + lq * NU, live, uz);
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                 ox[rt][e] = xz[rt][e] - alpha * g[rt][e];
-            st_rows_o<T, NX>(out, X0 + i * NX, live, ox);
+            if (stv) st_rows_o<T, NX>(out, X0 + i * NX, live, ox);
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                 ou[rt][e] = uz[rt][e] - alpha * hh[rt][e];
-            st_rows_o<T, NU>(out, U0 + i * NU, live, ou);
+            if (stv) st_rows_o<T, NU>(out, U0 + i * NU, live, ou);
             dstamp(3);
             lds_sync();  // C
         } else if (wv == 3) {
@@ -996,13 +1012,13 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             sw += w;
             if (k == h) {
                 const int j = 1 + C * i + k;
-                *elw(out, a.Y0 + yo + k) = ks.y[lo][k] - al * w;
-                *elw(out, a.Y0 + yo + C + k) = ks.y[lo][C + k] + w;
-                *elw(out, a.T0 + j) = ks.tau[lo][k] + w;
-                *elw(out, a.S0 + j) = ks.s[lo][k] + w;
+                gput(stv, out, a.Y0 + yo + k, ks.y[lo][k] - al * w);
+                gput(stv, out, a.Y0 + yo + C + k, ks.y[lo][C + k] + w);
+                gput(stv, out, a.T0 + j, ks.tau[lo][k] + w);
+                gput(stv, out, a.S0 + j, ks.s[lo][k] + w);
             }
         }
-        if (h == 0) *elw(out, a.Y0 + yo + 2 * C) = y2c - sw;
+        if (h == 0) gput(stv, out, a.Y0 + yo + 2 * C, y2c - sw);
     }
     if (!(wv == 0 || wv == 1 || wv == 3 || ((wv == 4 || wv == 5) && deepest))) {
         dstamp(3);
@@ -1042,12 +1058,16 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     if constexpr (CPF)
         if (kDiag && (pl.fault & 512)) {  // the CP step alone
             if (work) {
-                cpa_gather<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, CPA);
+                CpaStage cs;
+                if (gat) cpa_issue<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, cs);
                 TableDma<Cps::WA, BS / 64>::issue(SL + 3 * SLOT, ca->img);
                 TableDma<Cps::WB, BS / 64>::issue(SL + 2 * SLOT, ca->img + Cps::WA);
                 dma_wait();
+                if (gat) cpa_commit(CPA, cs);
                 lds_sync();
-                cp_phase<NX, NU, BX, BX>(*ca, *bfp, alpha, pl.X0, pl.U0, R0, deepest, XD, XL, U, CPA, SL, nullptr, pl.nblk);
+                if (!(pl.fault & 64))
+                    cp_phase<NX, NU, BX, BX>(*ca, *bfp, alpha, pl.X0, pl.U0, R0, deepest, XD, XL, U, CPA, SL, nullptr, pl.nblk,
+                                         !(pl.fault & 1024));
             }
             return;
         }
@@ -1070,10 +1090,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
             constexpr int l = L - 1 - ic.value;
             TB::issue(SL + l * SLOT, pl.bimg + (size_t)(s0 + l) * TBN);
         });
-    // ---- 2. the child subtrees' q rows (k_drc: above the deepest tier the CP operands land
-    // during this wait)
-    if constexpr (CPF)
-        if (work && gat && (!deepest || top)) cpa_gather<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, CPA);
+    // ---- 2. the child subtrees' q rows
     if (!deepest) {
         const DrTier& ct = pl.t[k + 1];
         if (!poll_gran(pl.gq + (size_t)(ct.w0 + o * NB) * G, NB * G, tag, (ldsu*)XL, pl.timeout, pl.sync, s_ok)) {
@@ -1107,15 +1124,21 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     if (top && !(kDiag && (pl.fault & 4))) TF::issue(SL, pl.fimg + (size_t)(s0 + L - 1) * TFN);
     if (!top) {
         if (!((pl.fault & 1) && deepest && o == 0)) publish(pl.gq + (size_t)(tt.w0 + o) * G, G, tag, (const ldsu*)XD);
-        // k_drc: the deepest tier's CP operands land during the wait below (older than the
-        // forward tables, so the forward levels' counted waits are unchanged)
+        // k_drc: the CP operands are loaded (older than the forward tables) and go to LDS once
+        // they have landed, still inside the wait below
+        CpaStage cs;
         if constexpr (CPF)
-            if (work && gat && deepest) cpa_gather<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, CPA);  // (not the top)
+            if (work && gat) cpa_issue<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, cs);
         if (!(kDiag && (pl.fault & 4)))
             static_for<0, L>([&](auto fc) {
                 constexpr int f = fc.value;
                 TF::issue(SL + (L - 1 - f) * SLOT, pl.fimg + (size_t)(s0 + f) * TFN);
             });
+        if constexpr (CPF)
+            if (work && gat) {
+                wait_vm_c<L * TF::IPW>();  // the operands have landed (the forward tables stay in flight)
+                cpa_commit(CPA, cs);
+            }
         if (!poll_gran(pl.gx + (size_t)(tt.w0 + o) * G, G, tag, (ldsu*)XD, pl.timeout, pl.sync, s_ok)) {
             dma_wait();
             return;
@@ -1148,6 +1171,12 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     // ---- 7. the boundary x rows to the child subtrees, then x and u to the iterate
     if (!deepest) publish(pl.gx + (size_t)(pl.t[k + 1].w0 + o * NB) * G, NB * G, tag, (const ldsu*)XL);
     if constexpr (CPF) {
+        if (work && gat && top) {  // the top has no wait to hide its operands behind
+            CpaStage ct;
+            cpa_issue<NX, NU, BX>(*ca, pl, *bfp, R0, deepest, ct);
+            dma_wait();
+            cpa_commit(CPA, ct);
+        }
         dma_wait();
         lds_sync();  // operands, weights and boxes in LDS for every wave
     }
@@ -1175,7 +1204,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
         wg_stamp(pl, 3);
         if (work && !(kDiag && (pl.fault & 64)))
             cp_phase<NX, NU, BX, BX>(*ca, *bfp, alpha, pl.X0, pl.U0, R0, deepest, XD, XL, U, CPA, SL,
-                                     kDiag ? pl.stamps : nullptr, pl.nblk);
+                                     kDiag ? pl.stamps : nullptr, pl.nblk, !(kDiag && (pl.fault & 1024)));
     }
     if (top && tid == 0) st_u32(pl.sync, tag);  // every workgroup has read the epoch
 }

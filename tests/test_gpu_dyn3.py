@@ -22,13 +22,6 @@ from helpers import rel_err, trace_rel_err
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True)
-def _per_stage_launches(monkeypatch):
-    # the one-launch dataflow form of the same sweep (k_dy4, opt-in): tests/test_gpu_dyn4.py;
-    # here the per-stage launches
-    monkeypatch.setenv("RAOCP_DY4", "0")
-
-
 def _with_env(env, fn):
     old = {k: os.environ.get(k) for k in env}
     os.environ.update({k: str(v) for k, v in env.items()})

@@ -43,7 +43,7 @@ def _kern_cache(prob, kern, dtype=None):
     # runs (k_cp3: a shard's task list; the unsharded defaults at config 2 / configs 4, 5 are
     # k_cp6 / k_cp5, the same arithmetic with a different FMA contraction, test_gpu_cp6.py,
     # test_gpu_cp5.py)
-    env = {"RAOCP_DR": "0", "RAOCP_DY4": "0", "RAOCP_CP4": "0", "RAOCP_CP5": "0", "RAOCP_CP6": "0"}
+    env = {"RAOCP_DR": "0", "RAOCP_CP4": "0", "RAOCP_CP5": "0", "RAOCP_CP6": "0"}
     if kern == "two":
         env["RAOCP_CP3"] = "0"
     old = {k: os.environ.get(k) for k in env}

@@ -10,7 +10,6 @@
 #   cp4         tests/test_gpu_cp4.py (k_cp4 against k_cp3 and the oracle)
 #   cp5         tests/test_gpu_cp5.py (k_cp5 against k_cp3 and the oracle)
 #   cp6         tests/test_gpu_cp6.py (k_cp6 against k_cp4, k_cp3 and the oracle)
-#   dyn4        tests/test_gpu_dyn4.py (the one-launch dataflow dynamics sweep k_dy4)
 #   cptests     the CP-kernel test files (cp3, cp4, cp5, fp32)
 #   dyntests    the dynamics test files (dynr, dyn_split, dyn3, variants)
 #   tests       the whole -m gpu suite
@@ -63,11 +62,9 @@ for step in "$@"; do
           tail -3 $out/pytest_cp5.log ;;
     cp6) timeout -k 10 500 $PYT tests/test_gpu_cp6.py > $out/pytest_cp6.log 2>&1 || fail $step $out/pytest_cp6.log
           tail -3 $out/pytest_cp6.log ;;
-    dyn4) timeout -k 10 500 $PYT tests/test_gpu_dyn4.py > $out/pytest_dyn4.log 2>&1 || fail $step $out/pytest_dyn4.log
-          tail -3 $out/pytest_dyn4.log ;;
     cptests) timeout -k 10 900 $PYT tests/test_gpu_cp3.py tests/test_gpu_cp4.py tests/test_gpu_cp5.py tests/test_gpu_cp6.py tests/test_gpu_fp32.py > $out/pytest_cp.log 2>&1 || fail $step $out/pytest_cp.log
           tail -3 $out/pytest_cp.log ;;
-    dyntests) timeout -k 10 900 $PYT tests/test_gpu_dynr.py tests/test_gpu_dyn_split.py tests/test_gpu_dyn3.py tests/test_gpu_dyn4.py tests/test_gpu_variants.py > $out/pytest_dyn.log 2>&1 || fail $step $out/pytest_dyn.log
+    dyntests) timeout -k 10 900 $PYT tests/test_gpu_dynr.py tests/test_gpu_dyn_split.py tests/test_gpu_dyn3.py tests/test_gpu_variants.py > $out/pytest_dyn.log 2>&1 || fail $step $out/pytest_dyn.log
           tail -3 $out/pytest_dyn.log ;;
     rest) timeout -k 10 900 $PYT ${REST_TESTS:-tests/test_gpu_variants.py} > $out/pytest_rest.log 2>&1 || fail $step $out/pytest_rest.log
           tail -3 $out/pytest_rest.log ;;
