@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <random>
 #include <string>
 #include <vector>
@@ -67,15 +68,12 @@ struct raocp_ctx {
                                  // task per wave at four waves per workgroup 18.5 vs 16.7 us at one)
     bool cp5 = false;            // ... as a leaf launch and a family launch (raocp_cp5.hip: configs 3, 4, 5;
                                  // RAOCP_CP5=0: off)
-    bool cp5_fams = false;       // the family launch as k_cp5_fams (a workgroup of C waves per tile), else
-                                 // k_cp5_fam (a wave per tile; RAOCP_CP5_FAMS)
     bool cp6 = false;            // ... as one family tile per workgroup of 2 C waves (raocp_cp5.hip k_cp6: config
                                  // 2; RAOCP_CP6=0: k_cp4)
     int cp6_grid = 0;
     raocp::Cp3Tasks cp5_tk{};    // k_cp5_fam's / k_cp6's task list (every parent, leaf parents first)
     int cp5_gl = 0, cp5_gf = 0;  // grids of the two launches
     bool cp5_lpf = false;        // k_cp5_leaf's form (RAOCP_CP5_LPF, raocp_cp5.h)
-    bool cp5_fpf = false;        // k_cp5_fam with the next tile in registers (RAOCP_CP5_FPF; spills, diagnostics)
     int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
     int cp3_split = 0;           // leaves as tasks of their own (small trees: more waves, shorter chains)
@@ -157,7 +155,8 @@ struct raocp_ctx {
     raocp::Bufs bufs{};          // {Z0, Z1, Z2, E0, E1}
     Ctl* ctl = nullptr;
     Ctl* h_ctl = nullptr;        // pinned host mirror
-    unsigned* h_err = nullptr;   // pinned host copy of a hand-off sweep's error word (raocp_cp_bench)
+    raocp::CtlPub* h_pub = nullptr;  // pinned host memory the batch tail's stopping test publishes to
+    raocp::CtlPub* d_pub = nullptr;  // (its device address)
     double* hist = nullptr;
     size_t hist_rows = 0;
     double* cur_z = nullptr;     // the Cache's current primal / dual
@@ -933,14 +932,6 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
     if (const char* e = getenv("RAOCP_FUSE_TIMEOUT_MS")) ms = std::max(1, atoi(e));
     p.timeout = ms * 100000LL;  // 100 MHz ticks
     c->dr = true;
-    if (getenv("RAOCP_DYN_VERBOSE")) {
-        fprintf(stderr, "[raocp] regular sweep: %d tiers,", T);
-        for (int k = 0; k < T; ++k) fprintf(stderr, " [%d,%d) x%d", p.t[k].s0, p.t[k].s0 + p.t[k].L, p.t[k].nsub);
-        int lmax = 0;
-        for (int k = 0; k < T; ++k) lmax = std::max(lmax, p.t[k].L);
-        fprintf(stderr, "; %d lanes, LDS %zu B, occupancy %d\n", c->dr_block, c->dr_lds,
-                raocp::dr_occupancy(nx, nu, C, lmax, c->dr_lds));
-    }
     return RAOCP_OK;
 }
 
@@ -1187,7 +1178,7 @@ void launch_cp3(raocp_ctx* c, int part = 0) {
     }
     if (c->cp5 && c->sh_S == 0) {
         raocp::cp5_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->m, c->n, c->cp5_gl, c->cp5_tk,
-                          c->cp5_gf, c->cp3img, c->cp5_fams, c->cp5_lpf, c->cp5_fpf, c->stream);
+                          c->cp5_gf, c->cp3img, c->cp5_lpf, c->stream);
         return;
     }
     if (c->cp4 && c->sh_S == 0) {
@@ -1379,7 +1370,7 @@ int enqueue_cp_iteration(raocp_ctx* c, int it) {
         launch_drc(c, it, defer && it > 0);
         c->bufs = keep;
         if (!defer)
-            raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, drc_part(c, it), c->cp_rows, drc_nanbit(it));
+            raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, drc_part(c, it), c->cp_rows, drc_nanbit(it), nullptr, nullptr);
         return RAOCP_OK;
     }
     const raocp::ChkArg ck{c->ctl, c->hist, c->redpart, c->cp_rows, 1};
@@ -1391,7 +1382,7 @@ int enqueue_cp_iteration(raocp_ctx* c, int it) {
         launch_cpp(c);
     }
     c->bufs = keep;
-    if (!defer) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0);
+    if (!defer) raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0, nullptr, nullptr);
     return RAOCP_OK;
 }
 // the kernel the default selection launches for op (raocp_op_bench numbering: 0 L, 1 L^T,
@@ -1458,11 +1449,10 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             return c->drc && c->sh_S == 0 ? raocp::drc_name() : "";
         case 12:  // the forms of the k_cp5 launches, when they run ("" otherwise)
             if (!(c->cp5 && c->sh_S == 0)) return "";
-            return std::string("leaf_pf=") + (c->cp5_lpf ? "1" : "0") + " fams=" + (c->cp5_fams ? "1" : "0") +
-                   " fam_pf=" + (c->cp5_fpf ? "1" : "0");
+            return std::string("leaf_pf=") + (c->cp5_lpf ? "1" : "0");
         case 10:
             if (c->cp6 && c->sh_S == 0) return raocp::cp6_name();
-            if (c->cp5 && c->sh_S == 0) return raocp::cp5_name(c->f32, c->nx, c->nu, c->unif_C, c->cp5_fams);
+            if (c->cp5 && c->sh_S == 0) return raocp::cp5_name(c->f32, c->nx);
             if (c->cp4 && c->sh_S == 0) return raocp::cp4_name(c->f32, c->nx, c->nu);
             if (c->cp3) return "k_cp3<" + T + ", " + nn + (c->sh_S > 0 ? ", true> x2" : ", false>");
             return kernel_name(c, 2) + " + " + kernel_name(c, 6);
@@ -1475,9 +1465,9 @@ void enqueue_batch_tail(raocp_ctx* c, int iters) {
     if (!defer_check(c)) return;
     if (c->drc && c->sh_S == 0)
         raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, drc_part(c, iters - 1), c->cp_rows,
-                                                       drc_nanbit(iters - 1));
+                                                       drc_nanbit(iters - 1), c->d_pub, err_word(c));
     else
-        raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0);
+        raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0, c->d_pub, err_word(c));
 }
 
 
@@ -1576,12 +1566,13 @@ int ensure_graph(raocp_ctx* c, int iters) {
         if (!c->comm) return rc_enq;
         // an RCCL shard whose collectives cannot be captured: launch iterations eagerly
         c->eager = true;
-        if (getenv("RAOCP_VERBOSE")) fprintf(stderr, "[raocp] RCCL capture failed (%s): eager launches\n", g_err.c_str());
         return RAOCP_OK;
     }
     if (e == hipSuccess) {
         e = hipGraphInstantiate(&slot, g, nullptr, nullptr, 0);
         (void)hipGraphDestroy(g);
+        // the executable graph's device-side setup now, not inside its first (timed) launch
+        if (e == hipSuccess) e = hipGraphUpload(slot, c->stream);
     }
     if (e != hipSuccess) {
         if (!c->comm) return fail(RAOCP_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
@@ -1589,7 +1580,6 @@ int ensure_graph(raocp_ctx* c, int iters) {
         (void)hipGetLastError();
         slot = nullptr;
         c->eager = true;
-        if (getenv("RAOCP_VERBOSE")) fprintf(stderr, "[raocp] RCCL graph capture failed (%s): eager launches\n", hipGetErrorString(e));
         return RAOCP_OK;
     }
     slot_iters = iters;
@@ -1819,6 +1809,21 @@ int build_cp_blocks(raocp_ctx* c, const std::vector<std::pair<int, int>>& prange
 // Every entry point that takes a context runs on that context's device: the current
 // device is switched for the call and restored afterwards (a process may hold contexts
 // on several devices; allocations and graph captures must land on c->device).
+// The co-resident sweeps (k_dr, k_drc and the split tier sweep k_dyn_up / k_dyn_down) spin on
+// hand-off flags and need every workgroup of their launch resident at once. Two of them from
+// different contexts on one device could each hold part of the CUs and wait for the other
+// (until the hand-off timeout returns RAOCP_ERR_STATE). One active context per device: the entry
+// points that launch them hold a per-device lock for the call (each synchronises its stream
+// before it returns), so threads of one process run such contexts one at a time. Processes
+// sharing a device are not serialised (docs: INTEGRATION.md "one active context per device").
+std::recursive_mutex g_sweep_mu[64];
+struct SweepLock {
+    std::unique_lock<std::recursive_mutex> l;
+    explicit SweepLock(const raocp_ctx* c) {
+        if (c && (c->dr || c->dyn_split)) l = std::unique_lock<std::recursive_mutex>(g_sweep_mu[c->device & 63]);
+    }
+};
+
 struct DevGuard {
     int prev = -1;
     explicit DevGuard(const raocp_ctx* c) {
@@ -2382,11 +2387,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         std::vector<double> f(N + 1, 1e300);
         std::vector<int> nxt(N + 1, N);
         f[N] = 0.0;
-        int forced = -1;
-        if (const char* env = getenv("RAOCP_DYN_CUT")) forced = atoi(env);  // tier depth (diagnostics)
         for (int a = N - 1; a >= 1; --a)
             for (int b = a + 1; b <= N; ++b) {
-                if (forced > 0 && b - a != forced && b != N) continue;
                 if (f[b] >= 1e299) continue;
                 const Tier w = tier(a, b);
                 if (!w.ok) continue;
@@ -2408,7 +2410,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 const size_t tb = top_bytes(s_, mt, fl, fold);
                 if (tb > kLds) continue;
                 any = true;
-                if (forced > 0 && s_ != std::min(forced, N)) continue;
                 const double cost = top_cost + (fl ? 0.0 : 2.0 * s_) - (fold ? s_ : 0) + f[s_];
                 if (cost < best) {
                     best = cost;
@@ -2537,9 +2538,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 int pu = 0, pd = 0;
                 dispatch(nx, nu, SplitOcc{}, c, &pu, &pd);
                 c->dyn_split = pu > 0 && pd > 0 && grid <= (long)n_cus * std::min(pu, pd);
-                if (getenv("RAOCP_DYN_VERBOSE"))
-                    fprintf(stderr, "[raocp] split sweep: %d tiers, %ld workgroups, %d / %d per CU x %d CUs%s\n", fa.K, grid, pu,
-                            pd, n_cus, c->dyn_split ? "" : " (not co-resident: tier launches)");
             }
             if (c->dyn_split) {
                 size_t words = 2;
@@ -2567,14 +2565,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 if (const char* e = getenv("RAOCP_FUSE_TIMEOUT_MS")) ms = std::max(1, atoi(e));
                 fa.timeout = ms * 100000LL;  // 100 MHz ticks
             }
-        }
-        if (getenv("RAOCP_DYN_VERBOSE")) {
-            fprintf(stderr, "[raocp] dynamics plan: top stages [0,%d) lds %zu F%s%s", c->cut, c->lds_top,
-                    c->f_lds_top ? "(lds)" : "(global)", c->fold_top ? " fold" : "");
-            for (const auto& tp : c->tiers)
-                fprintf(stderr, " | tier [%d,%d) x%d lds %zu/%zu F%s%s", tp.s0, tp.s1, tp.nsub, tp.lds_b, tp.lds_f,
-                        tp.fm == 1 ? "(lds)" : (tp.fm == 2 ? "(lds per level)" : "(global)"), tp.fold ? " fold" : "");
-            fprintf(stderr, "\n");
         }
     }
 
@@ -2616,8 +2606,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         // 256 blocks of 16 parents), leaf blocks of ~1/256 of the leaves
         int FB = std::max(1, std::min((m + 255) / 256, kBlock / (nx + nu + cmax + 1))),
             LB = std::max(1, (n - m + 255) / 256);
-        if (const char* e = getenv("RAOCP_CP_FB")) FB = std::max(1, atoi(e));  // parents per family block
-        if (const char* e = getenv("RAOCP_CP_LB")) LB = std::max(1, atoi(e));  // leaves per leaf block
         const std::vector<std::pair<int, int>> allp{{0, m}}, alll{{m, n}};
         while (FB > 1 && cp_need(c, allp, {}, FB, LB) > kCpLds) FB = FB * 3 / 4;
         while (LB > 1 && cp_need(c, {}, alll, FB, LB) > kCpLds) LB = LB * 3 / 4;
@@ -2633,14 +2621,11 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             int W = 4;
             const int lanes = std::max(2 * cmax + 2 + nx + nu, cmax + 1);
             W = std::max(W, (lanes + 63) / 64);
-            if (const char* e = getenv("RAOCP_CP2_W")) W = std::max((lanes + 63) / 64, std::min(4, atoi(e)));
             if (W > 4) return bail(fail(RAOCP_ERR_ARG, "parent rows exceed a 256-lane CP block (branching too large)"));
             const double cavg = (double)(n - 1) / m;
             c->cp2_W = W;
             c->cp2_FB = std::max(1, (int)(16.0 * W / cavg + 1e-9));
             c->cp2_LB = 16 * W;
-            if (const char* e = getenv("RAOCP_CP2_FB")) c->cp2_FB = std::max(1, atoi(e));
-            if (const char* e = getenv("RAOCP_CP2_LB")) c->cp2_LB = std::max(1, atoi(e));
             // within 64 KB of LDS per block (two blocks per CU)
             const long kLds2 = 64 * 1024;
             while (c->cp2_FB > 1 && cp2_need(c, 0, m, c->cp2_FB, true) > kLds2)
@@ -2659,15 +2644,12 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     }
 
     // ---- L / L^T node-range blocks (raocp_ell.hip): nonleaf and leaf ranges split evenly
-    // over B blocks; B from the node count (env RAOCP_ELL_NODES overrides the nodes per
-    // block), raised until every block's LDS stage fits 64 KB
+    // over B blocks; B from the node count (64 nodes per block), raised until every block's LDS stage fits 64 KB
     {
         // measured (round-2 A/B of the block size): 512-thread blocks while the grid is one block per CU,
         // 256-thread blocks of 64 nodes once there are several per CU
         int per = 64;
-        if (const char* e = getenv("RAOCP_ELL_NODES")) per = std::max(1, atoi(e));
         int thr = (n + per - 1) / per > 512 ? 256 : 512;
-        if (const char* e = getenv("RAOCP_ELL_THREADS")) thr = std::min(512, std::max(64, atoi(e) / 64 * 64));
         c->ell_threads = thr;
         const int Bmax = std::max(1, std::max(m, n - m));
         int B = std::max(1, std::min(std::max(256, (n + per - 1) / per), Bmax));
@@ -2711,8 +2693,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                     for (int q = i0; q < i1 && creg; ++q)
                         if (t->nch[q] != creg || t->ch_start[q] != c0 + (q - i0) * creg) creg = 0;
                 }
-                if (const char* e = getenv("RAOCP_ELLT_PARENT_TILES"))
-                    if (e[0] == '0') creg = 0;
                 T[3] = raocp::Rec{uni(pr->i_sq, c0, c1), uni(pr->i_sr, c0, c1), uni(pr->i_sp, l0, l1), creg};
                 const long np = i1 - i0, nc = c1 - c0, nl = l1 - l0, Y = y1 - y0;
                 need_l = std::max(need_l, dbl(np * nx) + dbl(np * nu) + dbl(Y) + dbl(np) + 2 * dbl(nc) + rec(np) +
@@ -2744,7 +2724,10 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         (rc = c->alloc(&c->tmpD, c->D)) || (rc = c->alloc(&c->part, 1024)) || (rc = c->alloc(&c->scal, 8)))
         return bail(rc);
     if (hipHostMalloc((void**)&c->h_ctl, sizeof(Ctl), 0) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "hipHostMalloc"));
-    if (hipHostMalloc((void**)&c->h_err, 4 * sizeof(unsigned), 0) != hipSuccess) return bail(fail(RAOCP_ERR_HIP, "hipHostMalloc"));
+    if (hipHostMalloc((void**)&c->h_pub, sizeof(raocp::CtlPub), hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer((void**)&c->d_pub, c->h_pub, 0) != hipSuccess)
+        return bail(fail(RAOCP_ERR_HIP, "hipHostMalloc"));
+    memset(c->h_pub, 0, sizeof(raocp::CtlPub));
     {
         double* zp = nullptr;
         if ((rc = c->alloc(&zp, 16))) return bail(rc);
@@ -2775,9 +2758,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
     if (const char* e = getenv("RAOCP_EAGER")) c->eager = atoi(e) != 0;
     c->cur_z = c->Z[0];
     c->cur_e = c->E[0];
+    c->dev.dyn_rot = 1;  // the tier kernels rotate the first wave of each staged range
     if ((rc = ensure_hist(c, 1024))) return bail(rc);
-    c->dev.dyn_rot = 1;  // RAOCP_DYN_ROT=0: every staged range starts at wave 0
-    if (const char* e = getenv("RAOCP_DYN_ROT")) c->dev.dyn_rot = atoi(e) != 0;
 
     {
         // L by streaming wave tasks (raocp_ell3.hip): compile-time sizes, and one sqrtQ / sqrtR
@@ -2795,7 +2777,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         // grid sweep (profiles/r02_v2/ab_order.log): config 4 fp64 best at 2,048 blocks (25.3 us
         // vs 26.7 at 4,096), config 5 fp32 at 1,024 (116 vs 137 us at 4,096)
         c->ell3_grid = (int)std::max(1L, std::min((tasks + 3) / 4, c->f32 ? 1024L : 2048L));
-        if (const char* e = getenv("RAOCP_ELL3_GRID")) c->ell3_grid = std::max(1, atoi(e));
         // L^T by streaming wave tasks: additionally one branching factor C <= 4 over all
         // nonleaf nodes (children 1 + C i .., y_i at (2C + 1) i); RAOCP_ELLT3=0 keeps k_ell_t
         int C = m > 0 ? t->nch[0] : 0;
@@ -2826,7 +2807,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         // grid sweep (profiles/r02_v4/ab_grid.log): 1,536 blocks best at config 4 fp64 (24.0 us
         // vs 24.9 at 4,096, 28.0 at 1,024) and config 5 fp32 (109.4 vs 111.1 at 2,048)
         c->ellt3_grid = (int)std::max(1L, std::min((tasks_t + 3) / 4, 1536L));
-        if (const char* e = getenv("RAOCP_ELLT3_GRID")) c->ellt3_grid = std::max(1, atoi(e));
         // the fused CP iteration (raocp_cp3.hip): uniform branching and tables (unif_C), the
         // compile-time sizes; RAOCP_CP3=0 keeps k_cpd* + k_cpp*
         c->cp3 = c->unif_C > 0 && c->ell3 && cp3_sizes(c->f32, nx, nu);
@@ -2843,7 +2823,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                                          c->cp3_split, c->cp3_mL);
             if (tiles < 0) return bail(fail(RAOCP_ERR_ARG, "k_cp3 task list exceeds its parent-range slots"));
             c->cp3_grid = cp3_grid_of(tiles);
-            if (const char* e = getenv("RAOCP_CP3_GRID")) c->cp3_grid = std::max(1, atoi(e));
             if (c->cp3_grid > c->red_rows) {
                 c->red_rows = c->cp3_grid;
                 if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
@@ -2859,7 +2838,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
             if (c->cp4) {  // k_cp4: cp4_wpb waves per workgroup, the same waves over more CUs
                 if (const char* e = getenv("RAOCP_CP4_HELPER")) c->cp4_wpb = atoi(e) ? 2 : 1;
                 c->cp3_grid = (int)std::max(1L, std::min(tiles, 8192L));  // one task per workgroup
-                if (const char* e = getenv("RAOCP_CP4_GRID")) c->cp3_grid = std::max(1, atoi(e));
                 if (c->cp3_grid > c->red_rows) {
                     c->red_rows = c->cp3_grid;
                     if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
@@ -2892,16 +2870,13 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 // RAOCP_CP5_LPF gets its own)
                 c->cp5_lpf = raocp::cp5_leaf_pf_default(c->f32);
                 if (const char* e = getenv("RAOCP_CP5_LPF")) c->cp5_lpf = atoi(e) != 0;
-                if (const char* e = getenv("RAOCP_CP5_FPF")) c->cp5_fpf = atoi(e) != 0;
                 c->cp5_gl = raocp::cp5_leaf_grid(m, n, c->cp5_lpf);
                 // k_cp5_fams (profiles/r05/cp_time_fams*.log: config 4 100.7 -> 90.9 us, config 5
                 // 335.3 -> 334.8 us, config 3 60.9 -> 57.4 us with the compacted slot sums)
-                c->cp5_fams = true;
-                if (const char* e = getenv("RAOCP_CP5_FAMS")) c->cp5_fams = atoi(e) != 0;
-                c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk, c->cp5_fams);
+                c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk);
                 if (const char* e = getenv("RAOCP_CP5_LGRID")) c->cp5_gl = std::max(1, atoi(e));
                 if (const char* e = getenv("RAOCP_CP5_FGRID")) c->cp5_gf = std::max(1, atoi(e));
-                c->cp_rows = raocp::cp5_rows(c->cp5_gl, c->cp5_gf, c->cp5_fams, c->unif_C);
+                c->cp_rows = raocp::cp5_rows(c->cp5_gl, c->cp5_gf);
                 if (c->cp_rows > c->red_rows) {
                     c->red_rows = c->cp_rows;
                     if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return bail(rc);
@@ -2912,8 +2887,6 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
         }
     }
     if ((rc = drc_setup(c))) return bail(rc);
-    c->dev.cp_dbg = 0;    // RAOCP_CP2_DBG: phase-skipping timing diagnostics (diagnostic builds only)
-    if (const char* e = getenv("RAOCP_CP2_DBG")) c->dev.cp_dbg = raocp::kDiag ? atoi(e) : 0;
     if (const char* e = getenv("RAOCP_DEFER_CHECK")) c->no_defer_check = atoi(e) == 0;
     c->drp.zpage = c->dev.zpage;
     c->drp.x0 = c->x0;
@@ -2931,7 +2904,7 @@ void raocp_ctx_destroy(raocp_ctx* c) {
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     for (void* p : c->allocs) (void)hipFree(p);
     if (c->h_ctl) (void)hipHostFree(c->h_ctl);
-    if (c->h_err) (void)hipHostFree(c->h_err);
+    if (c->h_pub) (void)hipHostFree(c->h_pub);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
@@ -3048,6 +3021,7 @@ int raocp_relax_s0(raocp_ctx* c, double alpha) {
 
 int raocp_project_on_dynamics(raocp_ctx* c) {
     DevGuard dg_(c);
+    SweepLock sl_(c);
     if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 context without a dynamics plan");
     if (!c) return fail(RAOCP_ERR_ARG, "null context");
     if (!c->has_x0) return fail(RAOCP_ERR_STATE, "initial state not cached (call cache_initial_state first)");
@@ -3260,6 +3234,7 @@ int raocp_step_size(raocp_ctx* c, double* lambda_max, int max_it, double rtol) {
 int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, double alpha, int* status, int* iters,
                  double* err_hist, double* delta_hist) {
     DevGuard dg_(c);
+    SweepLock sl_(c);
     if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 CP loop unavailable: no fp32 dynamics plan");
     if (!c || !x0) return fail(RAOCP_ERR_ARG, "null argument");
     if (max_iters < 0) return fail(RAOCP_ERR_ARG, "max_iters must be >= 0");
@@ -3270,10 +3245,13 @@ int raocp_cp_run(raocp_ctx* c, const double* x0, int max_iters, double tol, doub
     {
         const int batch = kGraphBatch;
         if ((rc = ensure_graph(c, batch))) return rc;
+        const bool pub = defer_check(c);
         for (;;) {
+            if (pub) c->h_pub->ctl.final_k = -2;
             if ((rc = launch_batch(c, batch))) return rc;
-            HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+            if (!pub) HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
             HIPCHK(hipStreamSynchronize(c->stream));
+            if (pub) *c->h_ctl = c->h_pub->ctl;  // published by the batch's last stopping test
             if (c->h_ctl->done) break;
         }
     }
@@ -3303,6 +3281,21 @@ int raocp_cp_prepare(raocp_ctx* c, const double* x0, int iters, double alpha) {
     if (iters / kGraphBatch && (rc = ensure_graph(c, kGraphBatch))) return rc;
     if (iters % kGraphBatch && (rc = ensure_graph(c, iters % kGraphBatch))) return rc;
     if (x0) {
+        // one dry replay of each graph the run launches, with ctl->done set (every kernel leaves
+        // without arithmetic): the graphs' first-launch cost (measured ~20 us at K = 20 beyond
+        // hipGraphUpload, tools/k_sweep.py) falls here instead of in the timed call
+        if (!c->eager) {
+            HIPCHK(hipStreamSynchronize(c->stream));
+            Ctl h{};
+            h.done = 1;
+            h.final_k = -1;
+            *c->h_ctl = h;
+            HIPCHK(hipMemcpyAsync(c->ctl, c->h_ctl, sizeof(Ctl), hipMemcpyHostToDevice, c->stream));
+            if (iters / kGraphBatch && (rc = launch_batch(c, kGraphBatch))) return rc;
+            if (iters % kGraphBatch && (rc = launch_batch(c, iters % kGraphBatch))) return rc;
+            HIPCHK(hipStreamSynchronize(c->stream));
+            if (int fe = fuse_err(c)) return fe;
+        }
         // the run's initial state: the following raocp_cp_bench(ctx, NULL, iters, ...) starts here
         if ((rc = cp_init(c, x0, iters - 1, 0.0, alpha))) return rc;
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -3313,6 +3306,7 @@ int raocp_cp_prepare(raocp_ctx* c, const double* x0, int iters, double alpha) {
 
 int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, float* ms) {
     DevGuard dg_(c);
+    SweepLock sl_(c);
     if (c && c->f32 && !c->dyn32) return fail(RAOCP_ERR_ARG, "fp32 CP loop unavailable: no fp32 dynamics plan");
     if (!c || iters < 1) return fail(RAOCP_ERR_ARG, "bad argument");
     int rc;
@@ -3332,6 +3326,11 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     }
     hipEvent_t e0 = c->ev0, e1 = c->ev1;
     if (x0) HIPCHK(hipStreamSynchronize(c->stream));
+    // the batch tail's stopping test publishes the control block and the error word to pinned
+    // host memory (k_cp_check pub): no device-to-host copy behind the timed kernels
+    const bool pub = defer_check(c);
+    raocp::CtlPub* hp = c->h_pub;
+    if (pub) hp->ctl.final_k = -2;
     HIPCHK(hipEventRecord(e0, c->stream));
     // exactly `iters` iterations' kernels: whole batches, then the remainder batch (an RCCL
     // shard then runs the last iteration's deferred stopping test)
@@ -3340,14 +3339,16 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
     if (rem && (rc = launch_batch(c, rem))) return rc;
     if (c->comm && (rc = enqueue_shard_tail(c))) return rc;
     HIPCHK(hipEventRecord(e1, c->stream));
-    // the control block and the hand-off sweep's error word come back behind the last
-    // iteration on the same stream: one synchronisation for the timed call
-    HIPCHK(hipMemcpyAsync(c->h_ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
     const unsigned* ew = err_word(c);
-    if (ew) HIPCHK(hipMemcpyAsync(c->h_err, ew, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+    if (!pub) {
+        HIPCHK(hipMemcpyAsync(&hp->ctl, c->ctl, sizeof(Ctl), hipMemcpyDeviceToHost, c->stream));
+        hp->err = 0;
+        if (ew) HIPCHK(hipMemcpyAsync(&hp->err, ew, sizeof(unsigned), hipMemcpyDeviceToHost, c->stream));
+    }
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipEventElapsedTime(ms, e0, e1));
-    if (ew && *c->h_err)
+    *c->h_ctl = hp->ctl;
+    if (ew && hp->err)
         if (int fe = fuse_err(c)) return fe;  // a timed-out hand-off skipped its arithmetic
     if (c->h_ctl->final_k != iters - 1) return fail(RAOCP_ERR_STATE, "bench did not run the requested iterations");
     c->cur_z = c->Z[iters % 3];
@@ -3360,6 +3361,7 @@ int raocp_cp_bench(raocp_ctx* c, const double* x0, int iters, double alpha, floa
 // `cap` raw 100 MHz timestamps.
 int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
     DevGuard dg_(c);
+    SweepLock sl_(c);
     // the regular-tree sweeps' stamps need only their own unit built with them (VAR_UNIT=dynr)
     if (!raocp::kDiag && !(c && c->dr && raocp::dr_diag_build()))
         return fail(RAOCP_ERR_ARG, "in-kernel stamps need a diagnostic build (make DIAG=1)");
@@ -3379,7 +3381,10 @@ int raocp_debug_dyn_stamps(raocp_ctx* c, unsigned long long* out, int cap) {
     Dev saved = c->dev;
     c->dev.stamps = st;
     const raocp::Bufs solo{c->cur_z, c->cur_z, c->cur_z, c->cur_e, c->cur_e};
+    // RAOCP_STAMP_KERNEL: the launch to stamp (its first letter) and, for the CP kernels, the
+    // workgroup / task that records (the number after it, e.g. "c200")
     const char* which = getenv("RAOCP_STAMP_KERNEL");
+    if (which && which[0]) c->dev.cp_dbg = atoi(which + 1);
     if (which && which[0] == 'p') {  // k_cpp on a valid control block (diagnostics)
         std::vector<double> x0(c->nx, 0.0);
         int rc2 = cp_init(c, x0.data(), 1 << 30, 0.0, 0.5);
@@ -3439,7 +3444,6 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
     c->sh_R = nranks;
     c->sh_r = rank;
     c->sh_S = S;
-    if (const char* e = getenv("RAOCP_SHARD_CP3")) c->cp3 = c->cp3 && atoi(e) != 0;
     std::vector<int> slc(2 * nranks);
     int xmax = 0;
     for (int r = 0; r < nranks; ++r) {
@@ -3638,6 +3642,7 @@ int raocp_group_cp_run(raocp_ctx** cs, int R, const double* x0, int max_iters, d
 
 int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
     DevGuard dg_(c);
+    SweepLock sl_(c);
     if (!c || reps < 1 || !ms_per_launch) return fail(RAOCP_ERR_ARG, "bad argument");
     // random inputs (seed 1), resident in HBM
     std::vector<double> hz(c->P), he(c->D);
@@ -3679,7 +3684,7 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
                 }
                 break;
             case 11: launch_drc(c, 0, false); break;  // the fused dynamics + CP launch (k_drc)
-            default: raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0);
+            default: raocp::k_cp_check<<<1, kBlock, 0, c->stream>>>(c->ctl, c->hist, c->redpart, c->cp_rows, 0, nullptr, nullptr);
         }
     };
     for (int i = 0; i < 3; ++i) run();  // warm-up
@@ -3719,6 +3724,7 @@ int raocp_op_bench(raocp_ctx* c, int op, int reps, float* ms_per_launch) {
 // input from HBM (the repeated-buffer op_bench is L3-assisted once a working set fits)
 int raocp_op_bench_rot(raocp_ctx* c, int op, int reps, int nsets, float* ms_per_launch) {
     DevGuard dg_(c);
+    SweepLock sl_(c);
     if (!c || reps < 1 || nsets < 1 || nsets > 16 || !ms_per_launch || (op != 0 && op != 1))
         return fail(RAOCP_ERR_ARG, "bad argument");
     std::vector<double> hz(c->P), he(c->D);

@@ -34,6 +34,15 @@ struct Ctl {
     double tol;
 };
 
+// what a batch's last stopping test publishes to pinned host memory (raocp_capi.hip h_pub):
+// the control block and the hand-off sweeps' error word, read by the host after its stream
+// synchronisation instead of two device-to-host copies
+struct CtlPub {
+    Ctl ctl;
+    unsigned err;
+    unsigned pad[3];
+};
+
 // the stopping test of the previous CP iteration run by an extra workgroup of the next
 // iteration's first dynamics launch (raocp_capi.hip, defer_check): on = 0 disables it
 struct ChkArg {
@@ -112,8 +121,8 @@ struct Dev {
     const int* stage_ptr;  // [N+2] first node id of each stage (BFS numbering)
     int N;                 // last stage
     unsigned long long* stamps;  // diagnostics: s_memrealtime stamps (nullptr = off)
-    int dyn_rot;           // tier kernels rotate the first wave of each staged range (RAOCP_DYN_ROT)
-    int cp_dbg;            // timing diagnostics only (RAOCP_CP2_DBG bits): skip phases of k_cpd2 / k_cpp2
+    int dyn_rot;           // tier kernels rotate the first wave of each staged range (always 1)
+    int cp_dbg;            // diagnostics only: the workgroup / task whose stamps k_cp4 / k_cp5 / k_cp6 record
 };
 
 // The task list of a k_cp3 / k_cp4 launch (host-built, raocp_capi.hip cp3_tasks): tiles of 16

@@ -299,7 +299,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
         lds_sync();
         if (done) return;
         // (1) child tiles: eta3 (nx), eta4 (nu), eta5, eta6 -> one SOC of dim nx + nu + 2
-        const int ntc = (kDiag && (p.cp_dbg & 1)) ? 0 : (C + 15) >> 4;
+        const int ntc = (C + 15) >> 4;
         for (int t = wv; t < ntc; t += nw) {
             const int j0 = 16 * t, ja = j0 + lo;
             const bool la = ja < C;
@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
             }
         }
         // (2) parent rows eta1 (2c+1), eta2, eta7 (nx+nu): lanes over rows
-        if (!(kDiag && (p.cp_dbg & 2))) {
+        {
             const int G = 2 * p.cmax + 2 + nx + nu, per = blockDim.x / G;
             const int gl = tid / G, r = tid - gl * G;
             for (int q0 = 0; q0 < P; q0 += per) {
@@ -448,7 +448,7 @@ __global__ void __launch_bounds__(256) k_cpd2(Dev p, Ctl* __restrict__ ctl, Bufs
         dma_wait();
         lds_sync();
         if (done) return;
-        const int ntl = (kDiag && (p.cp_dbg & 4)) ? 0 : (Lc + 15) >> 4;
+        const int ntl = (Lc + 15) >> 4;
         for (int t = wv; t < ntl; t += nw) {
             const int q0 = 16 * t, qa = q0 + lo;
             const bool la = qa < Lc;
@@ -621,8 +621,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
             account(pp, zz, accW, accC);
         };
         // (1) x / u rows
-        if (kDiag && (p.cp_dbg & 1)) {
-        } else if (creg > 0 && tq >= 0 && tr >= 0) {
+        if (creg > 0 && tq >= 0 && tr >= 0) {
             // regular block: per-parent tiles (4 (4 / c) parents per tile); x rows, then u rows
             const int Q = 4 / creg, PT = 4 * Q;
             const int hA = MF<T>::h_of(lo), eA = MF<T>::e_of(lo);
@@ -724,7 +723,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
         // r_k = alpha_r y_k - y_{c+k} + y_{2c} - tau_k - s_k, w = (r - 1 sum(r) / (a + c)) / a,
         // a = alpha_r^2 + 3; y_k -= alpha_r w_k, y_{c+k} += w_k, y_{2c} -= sum(w), tau_k += w_k,
         // s_k += w_k). Lane rk < cmax: child rk; rk == cmax: y_2c (and the root's s_0).
-        if (!(kDiag && (p.cp_dbg & 2))) {
+        {
             const int cmax = p.cmax, G = cmax + 1, per = blockDim.x / G;
             const int gl = tid / G, rk = tid - gl * G, kb = gl * G;
             for (int q0 = 0; q0 < P; q0 += per) {
@@ -844,7 +843,7 @@ __global__ void __launch_bounds__(256) k_cpp2(Dev p, Ctl* __restrict__ ctl, Bufs
         dma_wait();
         lds_sync();
         if (done) return;
-        const int ntl = (kDiag && (p.cp_dbg & 4)) ? 0 : (Lc + 15) >> 4;
+        const int ntl = (Lc + 15) >> 4;
         for (int t = wv; t < ntl; t += nw) {
             const int q0 = 16 * t, qa = q0 + lo;
             const bool la = qa < Lc;

@@ -265,379 +265,6 @@ __global__ void __launch_bounds__(256, LPF ? 1 : 2) k_cp5_leaf(Dev p, Ctl* ctl, 
     block_maxima(part, rs);
 }
 
-// ================================ k_cp5_fam ================================
-// The operands of one family tile (parent lane lo, lane group h), in three parts loaded at
-// different points of the previous tile (the software pipeline of k_cp5_fam): the parent's
-// part (its rows and scalars, double-buffered), the child slots' rows (refilled slot by slot
-// as the previous tile's phase 2 consumes them) and the eta7 rows (refilled after phase 3).
-// The scalars are spread over the lane groups: lane group h holds y entries q = h + 4 t and
-// child slot h's scalars.
-template <class T, int NX, int NU, int C>
-struct ParOps {
-    static constexpr int RX = (NX + 15) / 16, RU = (NU + 15) / 16, G = 2 * C + 1, NQ = (G + 3) / 4;
-    T yz[NQ], yp[NQ], y1[NQ];  // the parent's y entries q = h + 4 t of z+, p and its eta1 entries
-    T cph;                     // cond of child h (h < C)
-    T zs, ps, d2, e2, al;      // the parent's s (z+, p), eta2, eta2+ (k_cp5_leaf), alpha_r
-    T c5, c6, ctz, ctp, csl;   // child h: eta5, eta6, tau of z+ and p, s of the half step
-    T xz[RX][4], xp[RX][4], uz[RU][4], up[RU][4];
-    __device__ __forceinline__ void load(const Dev& p, cglbp<T> zp, cglbp<T> pz, cglbp<T> d, cglbp<T> eo, cglbp<T> out,
-                                         cglbp<T> cond, int iq, bool live) {
-        const int h = (threadIdx.x & 63) >> 4;
-        const int yo = G * iq;
-        _Pragma("unroll") for (int t = 0; t < NQ; ++t) {
-            const int q = h + 4 * t;
-            const bool ok = live && q < G;
-            const int qq = q < G ? q : 0;
-            yz[t] = ldz_o(zp, p.Y0 + yo + qq, ok);
-            yp[t] = ldz_o(pz, p.Y0 + yo + qq, ok);
-            y1[t] = ldz_o(d, p.E1 + yo + qq, ok);
-        }
-        const bool hc = live && h < C;
-        const int jh = 1 + C * iq + (h < C ? h : 0);
-        cph = ldz_o(cond, jh, hc);
-        zs = ldz_o(zp, p.S0 + iq, live);
-        ps = ldz_o(pz, p.S0 + iq, live);
-        d2 = ldz_o(d, p.E2 + iq, live);
-        e2 = ldz_o(eo, p.E2 + iq, live);
-        ld_rows_o<T, NX>(zp, p.X0 + iq * NX, live, xz);
-        ld_rows_o<T, NX>(pz, p.X0 + iq * NX, live, xp);
-        ld_rows_o<T, NU>(zp, p.U0 + iq * NU, live, uz);
-        ld_rows_o<T, NU>(pz, p.U0 + iq * NU, live, up);
-        c5 = ldz_o(d, p.E5 + jh, hc);
-        c6 = ldz_o(d, p.E6 + jh, hc);
-        ctz = ldz_o(zp, p.T0 + jh, hc);
-        ctp = ldz_o(pz, p.T0 + jh, hc);
-        csl = ldz_o(out, p.S0 + jh, hc);
-        al = ldz_o((cglbp<T>)p.alpha_r, iq, live);
-    }
-};
-// the eta3 / eta4 rows of child slot k of the tile's parents
-template <class T, int NX, int NU, int C>
-__device__ __forceinline__ void load_slot(const Dev& p, cglbp<T> d, int iq, bool live, int k,
-                                          T (&d3)[(NX + 15) / 16][4], T (&d4)[(NU + 15) / 16][4]) {
-    const int j = 1 + C * iq + k;
-    ld_rows_o<T, NX>(d, p.E3 + 1 + (j - 1) * NX, live, d3);
-    ld_rows_o<T, NU>(d, p.E4 + 1 + (j - 1) * NU, live, d4);
-}
-
-// tiles of 16 parents (lane lo = parent) from the ranges of tk, one tile per wave at a time,
-// a grid-stride loop; PF: the next tile's operands in flight during the current tile (else
-// every operand of a tile is loaded at its start)
-template <class T, int NX, int NU, int C, int BXN, bool PF>
-__global__ void __launch_bounds__(256, 1) k_cp5_fam(Dev p, Ctl* ctl, Bufs bf, double* __restrict__ part, Cp3Tasks tk,
-                                                    const double* __restrict__ img) {
-    typedef typename MF<T>::v4 v4;
-    static_assert(NX % 4 == 0 && NU % 4 == 0, "row layout needs nx, nu multiples of 4");
-    static_assert(C >= 1 && C <= 4, "one lane group per child slot");
-    typedef ParOps<T, NX, NU, C> Par;
-    constexpr int RX = Par::RX, RU = Par::RU, G = Par::G, NQ = Par::NQ;
-    typedef WL<T, NX, NX> WQ;
-    typedef WL<T, NU, NU> WR;
-    __shared__ KpScratch<T> kps_[4];
-    __shared__ __attribute__((aligned(16))) T wlds_[WQ::N + WR::N];
-    __shared__ __attribute__((aligned(16))) T blds_[2 * (NX + NU)];  // one-table trees: [lo_nl | hi_nl]
-    // per wave: the children's (eta+, d - eta+, xi2) eta3 | eta4 rows summed per parent over the
-    // slots, three streams of (RX + RU) row-layout chunks (registers are the scarce resource)
-    constexpr int SB = 3 * (RX + RU) * 64 * 4;
-    __shared__ __attribute__((aligned(16))) T sums_[4 * SB];
-    const int lane = threadIdx.x & 63, lo = lane & 15, h = lane >> 4, wv = threadIdx.x >> 6;
-    const int gw = blockIdx.x * (blockDim.x >> 6) + wv, nwv = gridDim.x * (blockDim.x >> 6);
-    typedef __attribute__((address_space(3))) KpScratch<T> lkps;
-    lkps& ks = *(lkps*)&kps_[wv];
-    typedef __attribute__((address_space(3))) T lTs;
-    lTs* sbx[3], *sbu[3];
-    _Pragma("unroll") for (int q = 0; q < 3; ++q) {
-        sbx[q] = (lTs*)sums_ + wv * SB + q * (RX + RU) * 256;
-        sbu[q] = sbx[q] + RX * 256;
-    }
-    cglbp<T> pz = (cglbp<T>)bf.z0;  // p
-    cglbp<T> zp = (cglbp<T>)bf.z1;  // z+
-    glbp<T> out = (glbp<T>)bf.z2;   // next half step
-    cglbp<T> d = (cglbp<T>)bf.e0;   // eta
-    glbp<T> eo = (glbp<T>)bf.e1;    // eta+
-    cglbp<T> cond = (cglbp<T>)p.cond;
-    typedef __attribute__((address_space(3))) T lT;
-    lT* bl_ = (lT*)blds_;
-    const int ntask = tk.t0[tk.nr];
-    // the parent of lane lo in task `task` (clamped to node 0 when past the tile or the tasks)
-    auto parent_of = [&](int task, int& iq, bool& live) {
-        int i0 = 0, iend = 0;
-        if (task < ntask) {
-            int r = 0;
-            while (r + 1 < tk.nr && task >= tk.t0[r + 1]) ++r;
-            i0 = tk.lo[r] + 16 * (task - tk.t0[r]);
-            iend = tk.hi[r];
-        }
-        live = task < ntask && i0 + lo < iend;
-        iq = live ? i0 + lo : 0;
-    };
-    // a tile's operands: the parent part, the slots' rows, the eta7 rows
-    Par pc;
-    T d3[C][RX][4], d4[C][RU][4], d7x[RX][4], d7u[RU][4];
-    auto load_tile = [&](int iq, bool live) {
-        pc.load(p, zp, pz, d, (cglbp<T>)eo, (cglbp<T>)out, cond, iq, live);
-        _Pragma("unroll") for (int k = 0; k < C; ++k) load_slot<T, NX, NU, C>(p, d, iq, live, k, d3[k], d4[k]);
-        if (BXN == 1) {
-            ld_rows_o<T, NX>(d, p.E7 + iq * (NX + NU), live, d7x);
-            ld_rows_o<T, NU>(d, p.E7 + iq * (NX + NU) + NX, live, d7u);
-        }
-    };
-    if (PF) {  // the first tile's operands, in flight during the prologue
-        int iq;
-        bool live;
-        parent_of(gw, iq, live);
-        load_tile(iq, live);
-    }
-    {
-        lds_fill((lds_d*)wlds_, img, (WQ::N + WR::N) * (int)sizeof(T) / 16);  // [sqrtQ | sqrtR]
-        for (int e = threadIdx.x; e < 2 * (NX + NU); e += blockDim.x)  // one box table (cp5_supported)
-            bl_[e] = BXN == 1 ? (e < NX + NU ? ((cglbp<T>)p.blo_nl)[e] : ((cglbp<T>)p.bhi_nl)[e - (NX + NU)]) : T(0);
-    }
-    const int done = ctl->done;
-    Resid<T> rs;
-    rs.alpha = (T)ctl->alpha;
-    rs.ra = T(1) / rs.alpha;
-    const T alpha = rs.alpha, ra = rs.ra;
-    dma_wait();
-    __syncthreads();
-    if (done) return;  // uniform over the grid
-    const WQ wq{(const lT*)wlds_};
-    const WR wr{(const lT*)wlds_ + WQ::N};
-    bool nanf = false;  // a NaN reached a box (Rectangle._constrain raises)
-    for (int task = gw; task < ntask; task += nwv) {
-        int iq, nq;
-        bool live, nlive;
-        parent_of(task, iq, live);
-        parent_of(task + nwv, nq, nlive);  // the next tile's (PF: its loads go out during this one)
-        if (!PF) load_tile(iq, live);
-        const int i = iq, yo = G * iq;
-        // ---------------- phase 1: eta1 of the parent (AVaR cone) and y_i of the half step;
-        // eta2+_i from k_cp5_leaf; b'(z+ - p) over the lane groups (cache.py:321-372)
-        T pb = T(0);
-        if (h < C) pb = pc.cph * (pc.yz[0] - pc.yp[0]);
-        _Pragma("unroll") for (int t = 0; t < NQ; ++t)
-            if (h + 4 * t == 2 * C) pb += pc.yz[t] - pc.yp[t];
-        const T byb = sum_h(pb);
-        const T e2A = pc.e2, e2W = pc.d2 - e2A;
-        const T e2C = (pc.d2 - e2A) * ra + ((pc.zs - pc.ps) - byb);
-        _Pragma("unroll") for (int t = 0; t < NQ; ++t) {
-            const int q = h + 4 * t;
-            if (!live || q >= G) break;
-            const T zy = pc.yz[t], py = pc.yp[t], dv = pc.y1[t];
-            const T v = (dv + alpha * (T(2) * zy - py)) * ra;
-            T ep, x2;
-            rs.fin(dv, v, q < 2 * C ? fmax(v, T(0)) : v, zy - py, ep, x2);
-            *elw(eo, p.E1 + yo + q) = ep;
-            const T b = q < C ? pc.cph : (q < 2 * C ? T(0) : T(1));
-            ks.y[lo][q] = zy - alpha * (ep - b * e2A);
-            rs.account(py, zy, (dv - ep) - b * e2W, x2 - b * e2C);
-        }
-        if (live && h < C) ks.s[lo][h] = pc.csl;  // child h's s of the half step (k_cp5_leaf)
-        // L products of the parent: a = L(2z+ - p), b = L(z+ - p) on the children's rows
-        v4 qa[RX], qb[RX], ua[RU], ub[RU];
-        {
-            T a1[RX][4], a2[RX][4];
-            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                a1[rt][e] = T(2) * pc.xz[rt][e] - pc.xp[rt][e];
-                a2[rt][e] = pc.xz[rt][e] - pc.xp[rt][e];
-            }
-            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) qa[rt] = qb[rt] = v4{0, 0, 0, 0};
-            mmt(wq.fresh(), a1, qa);
-            mmt(wq.fresh(), a2, qb);
-            T c1[RU][4], c2[RU][4];
-            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                c1[rt][e] = T(2) * pc.uz[rt][e] - pc.up[rt][e];
-                c2[rt][e] = pc.uz[rt][e] - pc.up[rt][e];
-            }
-            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) ua[rt] = ub[rt] = v4{0, 0, 0, 0};
-            mmt(wr.fresh(), c1, ua);
-            mmt(wr.fresh(), c2, ub);
-        }
-        // the next tile's parent part
-        Par pn;
-        if (PF) pn.load(p, zp, pz, d, (cglbp<T>)eo, (cglbp<T>)out, cond, nq, nlive);
-        // ---------------- phase 2: child slots (the child block SOC; the children's
-        // (eta+, d - eta+, xi2) eta3 / eta4 rows summed per parent in slot order); each slot's
-        // rows are refilled with the next tile's as soon as they are used
-        _Pragma("unroll") for (int k = 0; k < C; ++k) {
-            const int j = 1 + C * iq + k;
-            const int src = lo + 16 * k;  // lane group k holds slot k's scalars
-            const T d5 = bcast(pc.c5, src), d6 = bcast(pc.c6, src), tz = bcast(pc.ctz, src), tp = bcast(pc.ctp, src);
-            T v3[RX][4], v4_[RU][4];
-            T ss = T(0);
-            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                v3[rt][e] = (d3[k][rt][e] + alpha * qa[rt][e]) * ra;
-                if (tok<NX>(rt, e)) ss += v3[rt][e] * v3[rt][e];
-            }
-            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                v4_[rt][e] = (d4[k][rt][e] + alpha * ua[rt][e]) * ra;
-                if (tok<NU>(rt, e)) ss += v4_[rt][e] * v4_[rt][e];
-            }
-            ss = sum_h(ss);
-            const T a5 = T(0.5) * (T(2) * tz - tp), b5 = T(0.5) * (tz - tp);
-            const T v5 = (d5 + alpha * a5) * ra + T(-0.5);
-            const T v6 = (d6 + alpha * a5) * ra + T(0.5);
-            ss += v5 * v5;
-            const Soc<T> so(sqrt(ss), v6);
-            {
-                T eA[RX][4], eW[RX][4], eC[RX][4];
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    T ep = T(0), x2 = T(0);
-                    if (tok<NX>(rt, e)) rs.fin(d3[k][rt][e], v3[rt][e], so.first(v3[rt][e]), qb[rt][e], ep, x2);
-                    eA[rt][e] = ep;
-                    eW[rt][e] = d3[k][rt][e] - ep;
-                    eC[rt][e] = x2;
-                }
-                st_rows_o<T, NX>(eo, p.E3 + 1 + (j - 1) * NX, live, eA);
-                lds_put<T, NX>(sbx[0], eA, k > 0);
-                lds_put<T, NX>(sbx[1], eW, k > 0);
-                lds_put<T, NX>(sbx[2], eC, k > 0);
-            }
-            {
-                T eA[RU][4], eW[RU][4], eC[RU][4];
-                _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    T ep = T(0), x2 = T(0);
-                    if (tok<NU>(rt, e)) rs.fin(d4[k][rt][e], v4_[rt][e], so.first(v4_[rt][e]), ub[rt][e], ep, x2);
-                    eA[rt][e] = ep;
-                    eW[rt][e] = d4[k][rt][e] - ep;
-                    eC[rt][e] = x2;
-                }
-                st_rows_o<T, NU>(eo, p.E4 + 1 + (j - 1) * NU, live, eA);
-                lds_put<T, NU>(sbu[0], eA, k > 0);
-                lds_put<T, NU>(sbu[1], eW, k > 0);
-                lds_put<T, NU>(sbu[2], eC, k > 0);
-            }
-            if (PF) load_slot<T, NX, NU, C>(p, d, nq, nlive, k, d3[k], d4[k]);  // the next tile's slot k
-            T ep5, x25, ep6, x26;
-            rs.fin(d5, v5, so.first(v5), b5, ep5, x25);
-            rs.fin(d6, v6, so.last(v6), b5, ep6, x26);
-            if (live && h == 0) {
-                *elw(eo, p.E5 + j) = ep5;
-                ks.tau[lo][k] = tz - alpha * (T(0.5) * (ep5 + ep6));
-                rs.account(tp, tz, T(0.5) * ((d5 - ep5) + (d6 - ep6)), T(0.5) * (x25 + x26));
-            }
-            if (live && h == 1) *elw(eo, p.E6 + j) = ep6;
-        }
-        // ---------------- phase 3: L^T = Gamma' eta7 (box on [x_i; u_i]) + sqrtQ' / sqrtR' of
-        // the summed children's rows (operators.py:73-85); x_i, u_i of the half step
-        {
-            v4 gxA[RX], gxW[RX], gxC[RX], guA[RU], guW[RU], guC[RU];
-            if (BXN == 1) {
-                const int o7 = p.E7 + iq * (NX + NU);
-                T lx[RX][4], hx[RX][4], lu[RU][4], hu[RU][4];
-                ld_rows_lds<T, NX>(bl_, lx);
-                ld_rows_lds<T, NX>(bl_ + (NX + NU), hx);
-                ld_rows_lds<T, NU>(bl_ + NX, lu);
-                ld_rows_lds<T, NU>(bl_ + (NX + NU) + NX, hu);
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    lx[rt][e] = live ? lx[rt][e] : T(0);  // a dead lane's terms stay zero
-                    hx[rt][e] = live ? hx[rt][e] : T(0);
-                }
-                _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    lu[rt][e] = live ? lu[rt][e] : T(0);
-                    hu[rt][e] = live ? hu[rt][e] : T(0);
-                }
-                T e7[RX][4], e7u[RU][4];
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    T ep = T(0), x2 = T(0);
-                    if (tok<NX>(rt, e)) {
-                        const T v = (d7x[rt][e] + alpha * (T(2) * pc.xz[rt][e] - pc.xp[rt][e])) * ra;
-                        rs.fin(d7x[rt][e], v, box_sel(v, lx[rt][e], hx[rt][e], nanf), pc.xz[rt][e] - pc.xp[rt][e], ep, x2);
-                    }
-                    e7[rt][e] = ep;
-                    gxA[rt][e] = ep;
-                    gxW[rt][e] = d7x[rt][e] - ep;
-                    gxC[rt][e] = x2;
-                }
-                st_rows_o<T, NX>(eo, o7, live, e7);
-                _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                    T ep = T(0), x2 = T(0);
-                    if (tok<NU>(rt, e)) {
-                        const T v = (d7u[rt][e] + alpha * (T(2) * pc.uz[rt][e] - pc.up[rt][e])) * ra;
-                        rs.fin(d7u[rt][e], v, box_sel(v, lu[rt][e], hu[rt][e], nanf), pc.uz[rt][e] - pc.up[rt][e], ep, x2);
-                    }
-                    e7u[rt][e] = ep;
-                    guA[rt][e] = ep;
-                    guW[rt][e] = d7u[rt][e] - ep;
-                    guC[rt][e] = x2;
-                }
-                st_rows_o<T, NU>(eo, o7 + NX, live, e7u);
-                if (PF) {  // the next tile's eta7 rows
-                    ld_rows_o<T, NX>(d, p.E7 + nq * (NX + NU), nlive, d7x);
-                    ld_rows_o<T, NU>(d, p.E7 + nq * (NX + NU) + NX, nlive, d7u);
-                }
-            } else {
-                _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) gxA[rt] = gxW[rt] = gxC[rt] = v4{0, 0, 0, 0};
-                _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) guA[rt] = guW[rt] = guC[rt] = v4{0, 0, 0, 0};
-            }
-            {
-                T sx[RX][4], su[RU][4];
-                lds_get<T, NX>(sbx[0], sx);
-                mmt(wq.fresh(), sx, gxA);
-                lds_get<T, NU>(sbu[0], su);
-                mmt(wr.fresh(), su, guA);
-            }
-            {
-                T sx[RX][4], su[RU][4];
-                lds_get<T, NX>(sbx[1], sx);
-                mmt(wq.fresh(), sx, gxW);
-                lds_get<T, NU>(sbu[1], su);
-                mmt(wr.fresh(), su, guW);
-            }
-            {
-                T sx[RX][4], su[RU][4];
-                lds_get<T, NX>(sbx[2], sx);
-                mmt(wq.fresh(), sx, gxC);
-                lds_get<T, NU>(sbu[2], su);
-                mmt(wr.fresh(), su, guC);
-            }
-            T ox[RX][4], ou[RU][4];
-            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                ox[rt][e] = pc.xz[rt][e] - alpha * gxA[rt][e];
-                if (tok<NX>(rt, e)) rs.account(pc.xp[rt][e], pc.xz[rt][e], gxW[rt][e], gxC[rt][e]);
-            }
-            st_rows_o<T, NX>(out, p.X0 + iq * NX, live, ox);
-            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
-                ou[rt][e] = pc.uz[rt][e] - alpha * guA[rt][e];
-                if (tok<NU>(rt, e)) rs.account(pc.up[rt][e], pc.uz[rt][e], guW[rt][e], guC[rt][e]);
-            }
-            st_rows_o<T, NU>(out, p.U0 + iq * NU, live, ou);
-        }
-        // ---------------- phase 5: AVaR kernel projection of the family (cache.py:290-317,
-        // closed form: raocp_cp3.hip)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (live) {
-            const T al = pc.al;
-            const T y2c = ks.y[lo][2 * C];
-            T rk[C], sr = T(0);
-            _Pragma("unroll") for (int k = 0; k < C; ++k) {
-                rk[k] = al * ks.y[lo][k] - ks.y[lo][C + k] + y2c - ks.tau[lo][k] - ks.s[lo][k];
-                sr += rk[k];
-            }
-            const T a = al * al + T(3);
-            T sw = T(0);
-            _Pragma("unroll") for (int k = 0; k < C; ++k) {
-                const T w = (rk[k] - sr / (a + (T)C)) / a;
-                sw += w;
-                if (k == h) {
-                    const int j = 1 + C * i + k;
-                    *elw(out, p.Y0 + yo + k) = ks.y[lo][k] - al * w;
-                    *elw(out, p.Y0 + yo + C + k) = ks.y[lo][C + k] + w;
-                    *elw(out, p.T0 + j) = ks.tau[lo][k] + w;
-                    *elw(out, p.S0 + j) = ks.s[lo][k] + w;
-                }
-            }
-            if (h == 0) *elw(out, p.Y0 + yo + 2 * C) = y2c - sw;
-        }
-        __builtin_amdgcn_wave_barrier();
-        if (PF) pc = pn;
-    }
-    flag_nan(ctl, nanf);
-    block_maxima(part, rs);
-}
-
 // ================================ k_cp5_fams ================================
 // k_cp5_fam's family tiles with the child slots in parallel: one tile per workgroup of C waves
 // (k_cp6's role split without the leaf waves; the leaves and eta2 are k_cp5_leaf's), so a
@@ -1465,32 +1092,18 @@ int resident_grid(long tasks, int per) {
 
 template <class T, int NX, int NU, int C>
 void launch_t(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, int l0, int l1, int gl, const Cp3Tasks& tk, int gf,
-              const double* img, bool fs, bool lpf, bool pf, hipStream_t s) {
+              const double* img, bool lpf, hipStream_t s) {
     // the sqrtPf fragments follow [sqrtQ | sqrtR] in the image (16-B aligned: N multiples of 64)
     const double* imp = img + (size_t)(WL<T, NX, NX>::N + WL<T, NU, NU>::N) * sizeof(T) / 8;
-    if (fs) {
-        if (lpf) {
-            if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-            else k_cp5_leaf<T, NX, C, 2, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-        } else {
-            if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-            else k_cp5_leaf<T, NX, C, 2, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-        }
-        if ((bx & 3) == 1) k_cp5_fams<T, NX, NU, C, 1><<<gf, 64 * C, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
-        else k_cp5_fams<T, NX, NU, C, 2><<<gf, 64 * C, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
-        return;
-    }
-    if ((bx & 3) == 1) {
-        if (lpf) k_cp5_leaf<T, NX, C, 1, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-        else k_cp5_leaf<T, NX, C, 1, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-        if (pf) k_cp5_fam<T, NX, NU, C, 1, true><<<gf, 256, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
-        else k_cp5_fam<T, NX, NU, C, 1, false><<<gf, 256, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
+    if (lpf) {
+        if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
+        else k_cp5_leaf<T, NX, C, 2, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
     } else {
-        if (lpf) k_cp5_leaf<T, NX, C, 2, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
+        if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
         else k_cp5_leaf<T, NX, C, 2, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-        if (pf) k_cp5_fam<T, NX, NU, C, 2, true><<<gf, 256, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
-        else k_cp5_fam<T, NX, NU, C, 2, false><<<gf, 256, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
     }
+    if ((bx & 3) == 1) k_cp5_fams<T, NX, NU, C, 1><<<gf, 64 * C, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
+    else k_cp5_fams<T, NX, NU, C, 2><<<gf, 64 * C, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
 }
 
 }  // namespace
@@ -1503,17 +1116,10 @@ bool cp5_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbo
     if (!f32) return (nx == 20 && nu == 8 && C == 4) || (nx == 32 && nu == 12 && C == 3);
     return nx == 64 && nu == 16 && C == 4;
 }
-const char* cp5_name(bool f32, int nx, int nu, int C, bool fs) {
-    (void)C;
-    (void)nu;
-    if (fs) {
-        if (f32) return "k_cp5_leaf<float, 64, 4> x1 + k_cp5_fams<float, 64, 16, 4> x1";
-        if (nx == 20) return "k_cp5_leaf<double, 20, 4> x1 + k_cp5_fams<double, 20, 8, 4> x1";
-        return "k_cp5_leaf<double, 32, 3> x1 + k_cp5_fams<double, 32, 12, 3> x1";
-    }
-    if (f32) return "k_cp5_leaf<float, 64, 4> x1 + k_cp5_fam<float, 64, 16, 4> x1";
-    if (nx == 20) return "k_cp5_leaf<double, 20, 4> x1 + k_cp5_fam<double, 20, 8, 4> x1";
-    return "k_cp5_leaf<double, 32, 3> x1 + k_cp5_fam<double, 32, 12, 3> x1";
+const char* cp5_name(bool f32, int nx) {
+    if (f32) return "k_cp5_leaf<float, 64, 4> x1 + k_cp5_fams<float, 64, 16, 4> x1";
+    if (nx == 20) return "k_cp5_leaf<double, 20, 4> x1 + k_cp5_fams<double, 20, 8, 4> x1";
+    return "k_cp5_leaf<double, 32, 3> x1 + k_cp5_fams<double, 32, 12, 3> x1";
 }
 // persistent grids (every workgroup resident, one wave per SIMD): a wave's tiles stream behind
 // each other; at most one workgroup per CU
@@ -1525,14 +1131,11 @@ int cp5_leaf_grid(int l0, int l1, bool lpf) {
     return (lpf ? 1 : 2) * resident_grid(tasks, 2);  // two workgroups per CU without the prefetch
 }
 // rows of residual partials of the two launches (one per workgroup)
-int cp5_rows(int gl, int gf, bool fs, int C) {
-    (void)fs;
-    (void)C;
+int cp5_rows(int gl, int gf) {
     return gl + gf;
 }
-int cp5_fam_grid(const Cp3Tasks& tk, bool fs) {
-    if (fs) return (int)std::max(1L, std::min((long)tk.t0[tk.nr], 2L * cu_count()));  // two workgroups per CU
-    return resident_grid(tk.t0[tk.nr], 1);
+int cp5_fam_grid(const Cp3Tasks& tk) {
+    return (int)std::max(1L, std::min((long)tk.t0[tk.nr], 2L * cu_count()));  // two workgroups per CU
 }
 // k_cp6: fp64 at nx = 20, nu = 8 with C = 2 (config 2), boxes as for k_cp5
 bool cp6_supported(bool f32, int nx, int nu, int C, int bx, int nbox_nl, int nbox_l) {
@@ -1549,10 +1152,10 @@ void cp6_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, const Cp3
     else k_cp6<double, 20, 8, 2, 2, 2><<<grid, 256, 0, s>>>(p, ctl, bf, part, tk, img);
 }
 void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, int l0, int l1, int gl,
-                const Cp3Tasks& tk, int gf, const double* img, bool fs, bool lpf, bool fpf, hipStream_t s) {
-    if (p.nx == 20) launch_t<double, 20, 8, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, fs, lpf, fpf, s);
-    else if (p.nx == 32) launch_t<double, 32, 12, 3>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, fs, lpf, fpf, s);
-    else launch_t<float, 64, 16, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, fs, lpf, fpf, s);
+                const Cp3Tasks& tk, int gf, const double* img, bool lpf, hipStream_t s) {
+    if (p.nx == 20) launch_t<double, 20, 8, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, lpf, s);
+    else if (p.nx == 32) launch_t<double, 32, 12, 3>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, lpf, s);
+    else launch_t<float, 64, 16, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, lpf, s);
     (void)C;
 }
 

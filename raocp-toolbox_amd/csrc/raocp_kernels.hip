@@ -795,12 +795,23 @@ __global__ void k_zero_idx(double* __restrict__ x, const int* __restrict__ idx, 
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) x[idx[i]] = 0.0;
 }
 
+// the control block and the error word to pinned host memory (one thread, after its updates)
+__device__ __forceinline__ void publish_ctl(const Ctl* ctl, CtlPub* pub, const unsigned* errw) {
+    pub->ctl = *ctl;
+    pub->err = errw ? *errw : 0u;
+    __threadfence_system();
+}
+
 // end of iteration: record residuals, stopping test (solver.py:137-161)
-// nanbit: as ChkArg::nanbit (0: the CP kernels raise bit 0 themselves)
+// nanbit: as ChkArg::nanbit (0: the CP kernels raise bit 0 themselves); pub (a batch's last
+// test): the control block and the error word errw published to pinned host memory
 __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, const double* __restrict__ part,
-                                                      int rows, int nanbit) {
+                                                      int rows, int nanbit, CtlPub* pub, const unsigned* errw) {
     __shared__ double s_m[6][kBlock];
-    if (ctl->done) return;
+    if (ctl->done) {
+        if (pub && threadIdx.x == 0) publish_ctl(ctl, pub, errw);
+        return;
+    }
     double m[6] = {0, 0, 0, 0, 0, 0};
     for (int r = threadIdx.x; r < rows; r += blockDim.x)
         _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], part[(size_t)r * 6 + q]);
@@ -822,6 +833,7 @@ __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, con
     } else {
         ctl->k = k + 1;
     }
+    if (pub) publish_ctl(ctl, pub, errw);
 }
 
 // ---- subtree sharding (raocp_capi.hip, raocp_shard_setup): exchange packing and the

@@ -1,8 +1,8 @@
 """GPU parity of k_cp5 (raocp_cp5.hip): the fused CP iteration of k_cp3 (raocp_cp3.hip;
 solver.py:27-95, cache.py:248-393) for the large uniform trees as two software-pipelined
 launches -- k_cp5_leaf (eta2 and s of every nonleaf node; the leaf tiles: eta11..eta14, x_l
-and s_l of the half step before the kernel projection), then k_cp5_fam (the family tiles,
-reading eta2+ and the children's s from the first launch). The default of configs 3 (fp64,
+and s_l of the half step before the kernel projection), then k_cp5_fams (the family tiles, a
+workgroup of C waves per tile, reading eta2+ and the children's s from the first launch). The default of configs 3 (fp64,
 20 / 8, C = 4), 4 (fp64, 32 / 12, C = 3) and 5 (fp32, 64 / 16, C = 4) with all nodes boxed
 or none; RAOCP_CP5=0 keeps k_cp3.
 
@@ -44,8 +44,11 @@ def _with_env(env, fn):
 def _recipe(case):
     """Small trees of the compiled (nx, nu, C) combinations (the oracle runs them in
     seconds) and the benchmark configs."""
-    if case == "q20":  # C = 4 at 20 / 8 (config 3's sizes), 5,461 nodes
-        return recipe_synthetic(np.full((4, 4), .25), np.full(4, .25), 6, 6, 20, 8, seed=6)
+    if case in ("q20", "q20-nobox"):  # C = 4 at 20 / 8 (config 3's sizes), 5,461 nodes
+        r = recipe_synthetic(np.full((4, 4), .25), np.full(4, .25), 6, 6, 20, 8, seed=6)
+        if case == "q20-nobox":
+            r["nl_min"] = r["nl_max"] = r["l_min"] = r["l_max"] = None
+        return r
     if case == "m20":  # Markov 4 modes at 20 / 8 (per-mode dynamics, one cost table)
         rng = np.random.default_rng(5)
         P = rng.random((4, 4)) + 0.1
@@ -171,8 +174,8 @@ def test_cp5_early_stop_matches_cp3(case):
     """A tolerance between the first two residual maxima stops k_cp5 and k_cp3 at iteration 1
     with the same status and history (to rounding). On these trees the maximum is flat after
     it (the xi2 term of the leaf SOC's constant offsets dominates, as the oracle's trace
-    shows), so a later stop is not reachable by any tolerance; config 2's mid-batch stops:
-    test_gpu_cp3.py / test_gpu_cp4.py."""
+    shows), so a later stop is not reachable by any tolerance there; the unboxed trees' mid-batch
+    stops: test_cp5_mid_batch_early_stop_matches_cp3."""
     r = _recipe(case)
     tree, prob = build_problem(r)
     c5, c3 = _pair(prob)
@@ -187,6 +190,31 @@ def test_cp5_early_stop_matches_cp3(case):
     assert trace_rel_err(a[1], b[1]) <= 1e-12 and rel_err(a[3], b[3]) <= 1e-12
 
 
+@pytest.mark.parametrize("case", ["t32-nobox", "q20-nobox"])
+def test_cp5_mid_batch_early_stop_matches_cp3(case):
+    """Unboxed trees, whose residual maxima keep falling (with ripples): the tolerance is the
+    first new low of k_cp3's trace after the first graph batch (k > 24, not at a batch's first
+    or last iteration) by a 1 % margin, so both loops first meet it at that iteration; k_cp5
+    stops there inside its graph batch with k_cp3's status, history and iterate."""
+    r = _recipe(case)
+    tree, prob = build_problem(r)
+    c5, c3 = _pair(prob)
+    assert c5.native.kernel_info(10).startswith("k_cp5_leaf<double")
+    alpha = 0.999 / c5.native.step_size()
+    K = 72
+    _, err, _ = c3.native.cp_run(r["x0"], K, 0.0, alpha)
+    mx = err.max(axis=1)
+    lows = [k for k in range(25, K) if k % 24 not in (0, 23) and mx[k] < 0.99 * mx[:k].min()]
+    assert lows, "the trace makes no new low after the first batch"
+    k = lows[0]
+    tol = float(mx[k]) * (1 + 1e-9)
+    a = _run(c5, r["x0"], K, alpha, tol)
+    b = _run(c3, r["x0"], K, alpha, tol)
+    assert a[0] == b[0] == 0 and a[1].shape == b[1].shape == (k + 1, 3)
+    assert trace_rel_err(a[1], b[1]) <= 1e-12 and trace_rel_err(a[2], b[2]) <= 1e-12
+    assert rel_err(a[3], b[3]) <= 1e-12 and rel_err(a[4], b[4]) <= 1e-12
+
+
 def test_cp5_nan_in_box_raises():
     """A NaN reaching a box projection (Rectangle._constrain, rectangle.py:50-59) raises
     ValueError through k_cp5 as through the reference."""
@@ -199,29 +227,6 @@ def test_cp5_nan_in_box_raises():
     alpha = 0.999 / cache.native.step_size()
     with pytest.raises(ValueError):
         cache.native.cp_run(x0, 5, 0.0, alpha)
-
-
-@pytest.mark.parametrize("case", ["q20", "t32", "t32-nobox", "q64", "c4"])
-def test_cp5_slot_parallel_family_matches_wave_family(case):
-    """k_cp5_fams (a workgroup of C waves per family tile, RAOCP_CP5_FAMS=1) against k_cp5_fam
-    (one wave per tile): the same entry arithmetic and slot-order sums, so the loops agree at
-    rounding level (1e-12 fp64, fp32: 1e-5 on the traces)."""
-    r = _recipe(case)
-    tree, prob = build_problem(r)
-    dt = "float32" if case == "q64" else None
-    mk = (lambda: core.Cache(prob, dtype=dt)) if dt else (lambda: core.Cache(prob))
-    a = _with_env({"RAOCP_CP5_FAMS": "1"}, mk)
-    b = _with_env({"RAOCP_CP5_FAMS": "0"}, mk)
-    assert " + k_cp5_fams<" in a.native.kernel_info(10) and " + k_cp5_fam<" in b.native.kernel_info(10)
-    alpha = 0.999 / a.native.step_size(rtol=1e-7 if dt else 1e-14)
-    K = 14 if case == "c4" else 30
-    ra = _run(a, r["x0"], K, alpha)
-    rb = _run(b, r["x0"], K, alpha)
-    tol = 1e-5 if dt else 1e-12
-    assert ra[0] == rb[0] == 1
-    assert trace_rel_err(ra[1], rb[1]) <= tol and trace_rel_err(ra[2], rb[2]) <= tol
-    assert rel_err(ra[3], rb[3]) <= tol and rel_err(ra[4], rb[4]) <= tol
-    print(f"{case}: bit-identical {all(np.array_equal(u, v) for u, v in zip(ra, rb))}")
 
 
 @pytest.mark.parametrize("case", ["q20", "t32", "c4", "q64"])

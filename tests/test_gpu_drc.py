@@ -191,3 +191,32 @@ def test_drc_bench_loop_matches_cp_run():
     st, err, _ = on.native.cp_run(r["x0"], K - 1, 0.0, alpha)
     assert st == 1 and err.shape[0] == K
     assert np.array_equal(z_b, on.get_primal_flat())
+
+
+def test_drc_two_contexts_in_threads():
+    """One active context per device: k_drc needs its whole grid resident, so the entry points
+    that launch it hold a per-device lock (raocp_capi.hip SweepLock). Two threads solving on two
+    contexts of one device at once finish, each with the result of a solve alone."""
+    import threading
+    r, prob, on, _ = _caches("c2")
+    other = core.Cache(prob)
+    alpha = 0.999 / on.native.step_size()
+    ref = _run(on, r["x0"], 40, alpha)
+    res, errs = {}, []
+
+    def work(name, cache):
+        try:
+            for _ in range(3):
+                res[name] = _run(cache, r["x0"], 40, alpha)
+        except Exception as e:  # reported by the main thread
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(k, c)) for k, c in (("a", on), ("b", other))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs and not any(t.is_alive() for t in th)
+    for name in ("a", "b"):
+        for u, v in zip(res[name], ref):
+            assert np.array_equal(u, v)

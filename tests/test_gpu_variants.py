@@ -1,8 +1,6 @@
 """GPU parity of the kernel variants kept selectable: the eager stopping test after every
-iteration (RAOCP_DEFER_CHECK=0) against the default deferred one; the staging switch
-RAOCP_DYN_ROT=0 (every staged range of the tiered dynamics kernels starts at wave 0), which
-must not change a bit; and the default per-parent L^T tiles against the
-LDS-staged path (RAOCP_ELLT_PARENT_TILES=0); the streaming L^T (k_ellt3, default on
+iteration (RAOCP_DEFER_CHECK=0) against the default deferred one; the block L^T kernel
+k_ell_t against the oracle; the streaming L^T (k_ellt3, default on
 uniform trees) against the block kernel (RAOCP_ELLT3=0) and the oracle.
 
 Tolerances as in test_gpu_parity.py.
@@ -59,44 +57,19 @@ def test_deferred_stopping_test_matches_eager(iters, stop):
         assert s1 == 0 and e1.shape[0] <= stop + 1  # stopped early
 
 
-@pytest.mark.parametrize("cfg", [1, 2])
-def test_staging_switches_bit_identical(cfg):
-    """Staging only moves bytes: the CP loop with RAOCP_DYN_ROT=0 reproduces the default run
-    bit for bit (config 1: the generic-size kernels; config 2 on the tiered sweep, RAOCP_DR=0,
-    the regular-tree sweep has no rotation)."""
-    from raocp.problems import recipe_main
-    r = recipe_main() if cfg == 1 else recipe_config(2)
-    tree, prob = build_problem(r)
-    base = {"RAOCP_DR": "0"}
-    a = _with_env(base, lambda: core.Cache(prob))
-    b = _with_env({**base, "RAOCP_DYN_ROT": "0"}, lambda: core.Cache(prob))
-    alpha = 0.999 / a.native.step_size()
-    out = []
-    for cache in (a, b):
-        status, err, derr = cache.native.cp_run(r["x0"], 12, 0.0, alpha)
-        out.append((status, err, derr, cache.get_primal_flat(), cache.get_dual_flat()))
-    for u, v in zip(out[0], out[1]):
-        assert np.array_equal(u, v)
-
-
 @pytest.mark.parametrize("cfg", [2, 3, 4, "4-modes"])
-def test_ell_t_parent_tiles_bit_identical_to_staged(cfg):
-    """k_ell_t's per-parent MFMA tiles (regular blocks, default) against the LDS-staged
-    product path (RAOCP_ELLT_PARENT_TILES=0): the children are summed in the same order, so
-    the results are bit-identical; both match the oracle. Config 4-modes mixes weight tables
-    (the staged path is taken there either way)."""
+def test_ell_t_block_kernel_matches_oracle(cfg):
+    """k_ell_t (RAOCP_ELLT3=0): per-parent MFMA tiles on regular blocks, the LDS-staged product
+    path where a block mixes weight tables (config 4-modes), against the oracle."""
     from oracle.raocp_oracle import OracleProblem
     r = recipe_config(4 if cfg == "4-modes" else cfg)
     if cfg == "4-modes":
         r["Q"] = np.array([(1.0 + k) * q for k, q in enumerate(r["Q"])])
     tree, prob = build_problem(r)
-    tiles = _with_env({"RAOCP_ELLT3": "0"}, lambda: core.Cache(prob))
-    staged = _with_env({"RAOCP_ELLT3": "0", "RAOCP_ELLT_PARENT_TILES": "0"}, lambda: core.Cache(prob))
+    blk = _with_env({"RAOCP_ELLT3": "0"}, lambda: core.Cache(prob))
     rng = np.random.default_rng(11)
-    ee = rng.standard_normal(tiles.dual_size)
-    a, b = tiles.native.ell_t(ee), staged.native.ell_t(ee)
-    assert np.array_equal(a, b)
-    assert rel_err(a, OracleProblem(prob).ell_t(ee)) <= 1e-12
+    ee = rng.standard_normal(blk.dual_size)
+    assert rel_err(blk.native.ell_t(ee), OracleProblem(prob).ell_t(ee)) <= 1e-12
 
 
 @pytest.mark.parametrize("cfg", ["chain", 2, "2-nobox", "2-leafbox", 4, "4-c2", "stop", "stop-nobox"])

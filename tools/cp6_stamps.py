@@ -1,5 +1,5 @@
 """Diagnostics (diagnostic build: make DIAG=1, or tools/build_var.sh with -DRAOCP_DIAG): stamps of
-k_cp6 (raocp_cp5.hip) at config 2. The workgroup RAOCP_CP2_DBG (default 200: a tile of nonleaf
+k_cp6 (raocp_cp5.hip) at config 2. The workgroup STAMP_WG (default 200: a tile of nonleaf
 parents; 0..127 are leaf-parent tiles) stamps per wave [entry, prologue done, role done,
 barrier, streams done, exit]; every workgroup its [entry, exit]. Printed in ns (100 MHz).
 usage: RAOCP_HIP_LIB=build/var/diag.so python tools/cp6_stamps.py [reps]"""
@@ -7,8 +7,8 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "raocp-toolbox_amd"))
-os.environ["RAOCP_STAMP_KERNEL"] = "c"
-os.environ.setdefault("RAOCP_CP2_DBG", "200")
+WG = os.environ.get("STAMP_WG", "200")
+os.environ["RAOCP_STAMP_KERNEL"] = "c" + WG  # the stamped workgroup / task after the letter
 import numpy as np  # noqa: E402
 import raocp.core as core  # noqa: E402
 from raocp.problems import build_problem, recipe_config  # noqa: E402
@@ -16,7 +16,7 @@ from raocp.problems import build_problem, recipe_config  # noqa: E402
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
 r = recipe_config(2)
 cache = core.Cache(build_problem(r)[1])
-print(cache.native.kernel_info(10), "workgroup", os.environ["RAOCP_CP2_DBG"], flush=True)
+print(cache.native.kernel_info(10), "workgroup", WG, flush=True)
 for rep in range(reps):
     st = cache.native.debug_dyn_stamps(4200).astype(np.int64)
     w = st[64:64 + 4000].reshape(-1, 2)

@@ -23,6 +23,7 @@
 #               (tools/build_var.sh)
 #   cp6stamps   k_cp6's in-kernel stamps at config 2 (diagnostic variant build/var/diag.so)
 #   dy3trace    per-launch trace of the config-4 / config-5 dynamics (rocprofv3 kernel trace, tools/trace_seq.py)
+#   ksweep      tools/k_sweep.py: device / wall time of a benchmark call against K, graphs and eager
 #   bench20     bench.py --steps 20 --warmup 5 (the driver's K)
 #   bench       bench.py default run
 #   prof        rocprofv3 --kernel-trace --stats of bench.py (eager launches)
@@ -88,12 +89,18 @@ for step in "$@"; do
                  echo "variant $v"; grep config $out/l_sweep_$v.log
                done ;;
     cp6stamps) for wg in 200 50; do
-                 RAOCP_CP2_DBG=$wg RAOCP_HIP_LIB=build/var/diag.so timeout -k 10 120 python -u tools/cp6_stamps.py 3 >> $out/cp6_stamps.log 2>&1 || fail $step $out/cp6_stamps.log
+                 STAMP_WG=$wg RAOCP_HIP_LIB=build/var/diag.so timeout -k 10 120 python -u tools/cp6_stamps.py 3 >> $out/cp6_stamps.log 2>&1 || fail $step $out/cp6_stamps.log
                done; cat $out/cp6_stamps.log ;;
     dy3trace) for cfg in 4 5; do
                 timeout -k 10 240 rocprofv3 --kernel-trace -d $out/tr$cfg -o tr --output-format csv -- python3 tools/dyn_time.py child $cfg trace > $out/tr$cfg.log 2>&1 || fail $step $out/tr$cfg.log
                 python3 tools/trace_seq.py $out/tr$cfg 30 > $out/dy3_stages_c$cfg.log; cat $out/dy3_stages_c$cfg.log
               done ;;
+    ksweep) timeout -k 10 300 python -u tools/k_sweep.py > $out/k_sweep.log 2>&1 || fail $step $out/k_sweep.log
+          cat $out/k_sweep.log
+          for v in ${KS_LIBS:-}; do
+            RAOCP_HIP_LIB=build/var/$v.so KS_EAGER=0 timeout -k 10 300 python -u tools/k_sweep.py > $out/k_sweep_$v.log 2>&1 || fail $step $out/k_sweep_$v.log
+            echo "variant $v"; cat $out/k_sweep_$v.log
+          done ;;
     bench20) timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $out/bench_k20.log 2>&1 || fail $step $out/bench_k20.log
           tail -1 $out/bench_k20.log > $out/bench_k20.json; cut -c1-400 $out/bench_k20.json ;;
     bench) timeout -k 10 500 python -u bench.py > $out/bench.log 2>&1 || fail $step $out/bench.log
