@@ -939,7 +939,7 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
 // (binary trees, 20 / 8, fp64, every node boxed or none), the fused launch replaces the pair;
 // RAOCP_DRC=0 keeps them. Its weight image is k_cp3's [sqrtQ | sqrtR | sqrtPf] followed by the
 // one box table of each kind [lo_nl | hi_nl | lo_l | hi_l] (zeros when unboxed); its residual rows
-// are two sets of one row per sweep workgroup (drc_part).
+// are two sets of one row per sweep wave (8 per workgroup, drc_part).
 int drc_setup(raocp_ctx* c) {
     c->drc = false;
     if (!c->dr || !c->cp6 || c->f32 || c->sh_S > 0 || !raocp::drc_supported(c->nx, c->nu, c->reg_C)) return RAOCP_OK;
@@ -971,7 +971,7 @@ int drc_setup(raocp_ctx* c) {
         HIPCHK(hipMemcpy(bx0 + 2 * R, c->dev.blo_l, nx * sizeof(double), hipMemcpyDeviceToDevice));
         HIPCHK(hipMemcpy(bx0 + 2 * R + nx, c->dev.bhi_l, nx * sizeof(double), hipMemcpyDeviceToDevice));
     }
-    const int rows = p.nblk;
+    const int rows = 8 * p.nblk;
     if (2 * rows > c->red_rows) {
         c->red_rows = 2 * rows;
         if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return rc;

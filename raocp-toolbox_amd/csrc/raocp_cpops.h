@@ -21,6 +21,7 @@ struct Amax<float> {
     __device__ __forceinline__ void add(float v) { m = __builtin_elementwise_maximum(m, fabsf(v)); }
     __device__ __forceinline__ double get() const { return (double)m; }
 };
+#ifndef RAOCP_AMAX_BITS
 template <>
 struct Amax<double> {
     double m = 0.0;
@@ -31,6 +32,21 @@ struct Amax<double> {
     }
     __device__ __forceinline__ double get() const { return nan ? __builtin_nan("") : m; }
 };
+#else
+// (RAOCP_AMAX_BITS, k_drc's unit) the maximum of |v| by the bit patterns: non-negative doubles
+// order as unsigned integers, a NaN above +inf, so the unsigned maximum propagates NaN with no
+// lane mask kept alive across the kernel's divergent role branches (whose joins each carried
+// the six masks through scalar registers)
+template <>
+struct Amax<double> {
+    double m = 0.0;
+    __device__ __forceinline__ void add(double v) {
+        const double a = fabs(v);
+        m = (unsigned long long)__double_as_longlong(a) > (unsigned long long)__double_as_longlong(m) ? a : m;
+    }
+    __device__ __forceinline__ double get() const { return m; }
+};
+#endif
 
 // the six residual maxima of a wave, and the per-entry terms (raocp_cp3.hip fin / account).
 // A lane past its tile's nodes has zero operands (ldz / ld_rows) and zero box bounds, so

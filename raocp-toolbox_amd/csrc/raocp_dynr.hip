@@ -43,6 +43,7 @@
 // and the granules, raocp_capi.hip).
 
 #include "raocp_dynr.h"
+#define RAOCP_AMAX_BITS
 #include "raocp_cpops.h"
 
 namespace raocp {
@@ -521,6 +522,22 @@ __device__ __forceinline__ void cpa_commit(ldsd* A, const CpaStage& st) {
     }
 }
 
+// a wave's maximum of non-negative doubles (NaN above +inf) by their bit patterns as unsigned
+// integers: wave_nmax's DPP steps with one 64-bit compare and two selects per step; lane 63
+// ends with it
+__device__ __forceinline__ double bmax(double a, double b) {
+    return (unsigned long long)__double_as_longlong(a) > (unsigned long long)__double_as_longlong(b) ? a : b;
+}
+__device__ __forceinline__ double wave_bmax(double v) {
+    v = bmax(v, dpp_d<0xB1, 0xF>(v));   // lane ^ 1
+    v = bmax(v, dpp_d<0x4E, 0xF>(v));   // lane ^ 2
+    v = bmax(v, dpp_d<0x141, 0xF>(v));  // row half-mirror
+    v = bmax(v, dpp_d<0x140, 0xF>(v));  // row mirror
+    v = bmax(v, dpp_d<0x142, 0xA>(v));  // row_bcast15 into rows 1 and 3
+    v = bmax(v, dpp_d<0x143, 0xC>(v));  // row_bcast31 into rows 2 and 3
+    return v;
+}
+
 // an R-row node vector from an LDS row in the tile's row layout (raocp_tile.h ld_rows), zero
 // when !live (row must be a valid LDS row either way)
 template <int R>
@@ -562,10 +579,12 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
     typedef WL<T, NX, NX> WQ;
     typedef WL<T, NU, NU> WR;
     typedef __attribute__((address_space(3))) KpScratch<T> lkps;
+    // (the wave index as a lane value: with it in a scalar register the role branches become
+    // scalar ones and the allocator overlaps the roles' live ranges, 91 VGPRs spilled)
     const int tid = threadIdx.x, lane = tid & 63, lo = lane & 15, h = lane >> 4, wv = tid >> 6;
     // diagnostics: per-wave stamps of the first (deepest) and the last (top) workgroup at
     // 3072 + {0, 64} + 8 wave + {0 start, 1 first role done, 2 second role done, 3 third role
-    // done, 4 end}
+    // done, 5 last role done, 6 maxima reduced, 4 end}
     auto dstamp = [&](int q) {
         if (kDiag && dstamps && lane == 0 && (blockIdx.x == 0 || (int)blockIdx.x == nblk - 1))
             dstamps[3072 + ((int)blockIdx.x == 0 ? 0 : 64) + 8 * wv + q] = __builtin_amdgcn_s_memrealtime();
@@ -871,23 +890,36 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         // ================= the box rows of the families (Rectangle on eta7 = [x_i | u_i],
         // cache.py:374-393): eta7+ to the dual, and per entry the three streams' seeds
         // (eta7+ over eta7 in place, d - eta7+ and xi2 over the dead eta3 / eta4 rows)
-        // lane group h takes the entries r = r0 + h, r0 = 0, 4, .., 24
-        _Pragma("unroll") for (int r0 = 0; r0 < NX + NU; r0 += 4) {
-            const int r = r0 + h;
-            const T zv = live ? (r < NX ? XD[lq * SXD + r] : U[lq * NU + r - NX]) : T(0);
-            const T pv = live ? (r < NX ? A[Cpa::PX + lq * NX + r] : A[Cpa::PU + lq * NU + r - NX]) : T(0);
-            const int o = lq * (NX + NU) + r;
-            const T d7 = live ? A[Cpa::D7 + o] : T(0);
-            const T lv = live ? BX[r] : T(0), hv = live ? BX[(NX + NU) + r] : T(0);  // dead lanes: zero terms
+        // lane group h takes the entries r = 4 t + h, t < 7 (x rows for t < 5); the operands of
+        // entry t + 1 are read before entry t's stores (the in-place stores would otherwise
+        // order each entry's reads behind the previous entry's writes)
+        constexpr int NT = (NX + NU) / 4;
+        auto opnd = [&](int t, T (&o5)[5]) {
+            const int r = 4 * t + h;
+            const bool xr = 4 * t < NX;
+            o5[0] = xr ? XD[lq * SXD + r] : U[lq * NU + (xr ? 0 : r - NX)];
+            o5[1] = xr ? A[Cpa::PX + lq * NX + r] : A[Cpa::PU + lq * NU + (xr ? 0 : r - NX)];
+            o5[2] = A[Cpa::D7 + lq * (NX + NU) + r];
+            o5[3] = BX[r];
+            o5[4] = BX[(NX + NU) + r];
+            _Pragma("unroll") for (int q = 0; q < 5; ++q) o5[q] = live ? o5[q] : T(0);  // dead lanes: zero terms
+        };
+        T cur[5], nxt[5];
+        opnd(0, cur);
+        _Pragma("unroll") for (int t = 0; t < NT; ++t) {
+            if (t + 1 < NT) opnd(t + 1, nxt);
+            const int r = 4 * t + h, o = lq * (NX + NU) + r;
+            const T zv = cur[0], pv = cur[1], d7 = cur[2];
             const T v = (d7 + alpha * (T(2) * zv - pv)) * ra;
             T ep, x2;
-            rs.fin(d7, v, box_sel(v, lv, hv, nanf), zv - pv, ep, x2);
+            rs.fin(d7, v, box_sel(v, cur[3], cur[4], nanf), zv - pv, ep, x2);
             if (live) {
                 gput(stv, eo, a.E7 + i * (NX + NU) + r, ep);
                 A[Cpa::D7 + o] = ep;
                 A[Cpa::SDW + o] = d7 - ep;
                 A[Cpa::SDC + o] = x2;
             }
+            _Pragma("unroll") for (int q = 0; q < 5; ++q) cur[q] = nxt[q];
         }
     }
     if (!(wv == 2 && deepest)) {
@@ -1024,8 +1056,21 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         dstamp(3);
         lds_sync();  // C
     }
+    dstamp(5);
     flag_nan(a.ctl, nanf, a.nanbit);
-    block_maxima_at(a.part, blockIdx.x, rs, SL + Cps::RED);
+    // one residual row per wave (no workgroup barrier behind the last role): the six maxima by
+    // DPP, lanes 58..63 (which hold all six) store one each
+    {
+        const double mm[6] = {wave_bmax(rs.m0.get()), wave_bmax(rs.m1.get()), wave_bmax(rs.m2.get()),
+                              wave_bmax(rs.m3.get()), wave_bmax(rs.m4.get()), wave_bmax(rs.m5.get())};
+        dstamp(6);
+        if (lane >= 58) {
+            const int q = lane - 58;
+            double v = mm[0];
+            _Pragma("unroll") for (int qq = 1; qq < 6; ++qq) v = q == qq ? mm[qq] : v;
+            a.part[((size_t)blockIdx.x * 8 + wv) * 6 + q] = v;
+        }
+    }
     dstamp(4);
 }
 
@@ -1253,6 +1298,41 @@ k_dr(DrPlan pl, Bufs bf, int zsel, const Ctl* ctl, ChkArg ck) {
     wg_stamp(pl, 2);
 }
 
+// the previous iteration's stopping test (solver.py:137-161) by k_drc's extra workgroup: the
+// residual rows (one per sweep wave) spread over all its lanes (a few loads each, issued
+// together), the maxima by DPP per wave and through LDS across the waves
+__device__ __forceinline__ void cp_check_block(const ChkArg& ck, ldsd* red) {
+    Ctl* ctl = ck.ctl;
+    if (ctl->done) return;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nt = blockDim.x;
+    double m[6] = {0, 0, 0, 0, 0, 0};
+    _Pragma("unroll") for (int j = 0; j < 8; ++j) {
+        const int r = tid + j * nt;
+        if (r < ck.rows) _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = bmax(m[q], ck.part[(size_t)r * 6 + q]);
+    }
+    for (int r = tid + 8 * nt; r < ck.rows; r += nt)
+        _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = bmax(m[q], ck.part[(size_t)r * 6 + q]);
+    _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = wave_bmax(m[q]);
+    if (lane == 63) _Pragma("unroll") for (int q = 0; q < 6; ++q) red[q * 16 + wv] = m[q];
+    __syncthreads();
+    if (tid != 0) return;
+    _Pragma("unroll") for (int q = 0; q < 6; ++q) {
+        double b = red[q * 16];
+        for (int w = 1; w < (nt >> 6); ++w) b = bmax(b, red[q * 16 + w]);
+        m[q] = b;
+    }
+    const int k = ctl->k;
+    for (int q = 0; q < 6; ++q) ck.hist[(size_t)k * 6 + q] = m[q];
+    const double err = nmax(nmax(m[0], m[1]), m[2]);
+    if (ctl->flags & ck.nanbit) ctl->flags |= 1;
+    if (k >= ctl->max_iters || err <= ctl->tol || (ctl->flags & 1)) {
+        ctl->done = 1;
+        ctl->final_k = k;
+    } else {
+        ctl->k = k + 1;
+    }
+}
+
 // k_drc: k_dr's sweep with each subtree's CP families behind its forward sweep (every tier of 4
 // levels, binary trees at nx / nu = 20 / 8; the host checks the plan). One launch per CP
 // iteration; the extra workgroup runs the previous iteration's stopping test (its residual rows
@@ -1265,7 +1345,7 @@ k_drc(DrPlan pl, DrcArg ca, Bufs bf, ChkArg ck) {
     __shared__ int s_ok;
     const int tid = threadIdx.x;
     if (ck.on && (int)blockIdx.x == pl.nblk) {  // the previous CP iteration's stopping test
-        if (tid < 64) cp_check_wave(ck);
+        cp_check_block(ck, (ldsd*)smem_);
         return;
     }
     if (tid == 0) {

@@ -4,9 +4,10 @@
 
 `ell` / `ell_transpose` keep the reference's block-list calling convention: the
 caller owns both lists, only the slots L (L^T) writes are replaced, every other
-slot keeps what the caller passed. The arithmetic runs in the `k_ell` /
-`k_ell_t` HIP kernels (raocp_kernels.hip) through `raocp_ell` / `raocp_ell_t`.
-"""
+slot keeps what the caller passed. The arithmetic runs in HIP kernels through
+`raocp_ell` / `raocp_ell_t`: the streaming MFMA wave tasks `k_ell3` / `k_ellt3`
+(raocp_ell3.hip) on trees with uniform weight tables (and branching <= 4 for L^T), the
+node-range block kernels `k_ell` / `k_ell_t` (raocp_kernels.hip) otherwise."""
 import numpy as np
 
 import raocp.core.cache as core_cache

@@ -192,7 +192,7 @@ def _c5_against_fixture(cache, fx, K, x0):
 
 
 def test_fp32_cp_loop_config5_20_iterations_vs_oracle(c5, golden):
-    """20 iterations of the fp32 CP loop at config 5 (k_cp3<float, 64, 16> + k_dy3<float>)
+    """20 iterations of the fp32 CP loop at config 5 (k_cp5_leaf + k_cp5_fams<float> + k_dy3<float>)
     against the fp64 oracle at the oracle's own step size (c5_cp.npz: the oracle's traces and
     iterate samples, 6 min of CPU per run, hence stored). Tolerances from fp32 rounding
     through 20 nonexpansive CP steps: the residual traces 2e-3 relative per entry, the iterate

@@ -35,6 +35,7 @@ for rep in range(reps):
     for which, base, b in (("deep wg 0", 3072, 0), ("top", 3136, 272)):
         s = st[base:base + 64].reshape(8, 8)
         s = np.where(s > 0, (s - t0) * 10, -1)
-        print(f"rep {rep} {which} (fwd done {w[b, 3]}): per wave [start, role, barrier, role2, end] ns", flush=True)
+        print(f"rep {rep} {which} (fwd done {w[b, 3]}): per wave [start, role, barrier, role2, last role, "
+              f"maxima, end] ns", flush=True)
         for wv in range(8):
-            print(f"    wave {wv}: " + " ".join(f"{x:6d}" for x in s[wv, :5]), flush=True)
+            print(f"    wave {wv}: " + " ".join(f"{x:6d}" for x in s[wv, [0, 1, 2, 3, 5, 6, 4]]), flush=True)
