@@ -62,6 +62,18 @@ struct Resid {
         m2.add(x2);
         m5.add(ep - dv);
     }
+    // account() in two parts (the same operations): every term but xi0, returning xi1; then
+    // xi0 = xi1 + lc once L^T xi2 is known
+    __device__ __forceinline__ T account_pre(T pp, T zz, T w) {
+        const T x1 = (pp - zz) * ra - w;
+        const T dl1 = zz - pp;
+        const T dl0 = dl1 + w;
+        m1.add(x1);
+        m3.add(dl0);
+        m4.add(dl1);
+        return x1;
+    }
+    __device__ __forceinline__ void account_post(T x1, T lc) { m0.add(x1 + lc); }
     // one primal entry: pp = p, zz = z+, w = L^T(d - eta+), lc = L^T xi2
     __device__ __forceinline__ void account(T pp, T zz, T w, T lc) {
         const T x1 = (pp - zz) * ra - w;

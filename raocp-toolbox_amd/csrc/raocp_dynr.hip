@@ -407,10 +407,12 @@ struct Cps {
     static constexpr int QA = 0, QB = 512, LB = 1024, UA = 1536, UB = 1792;  // products (row-layout v4 x 64 lanes)
     static constexpr int SB = 0, SX = 320, SS = 448;                          // stream rows (compacted)
     static constexpr int WP = 2 * SLOT, BX = 2 * SLOT + 640, LEW = 2 * SLOT + 736, KPS = 2 * SLOT + 1056;
-    static constexpr int WQ = 3 * SLOT, WR = 3 * SLOT + 640, LEC = 3 * SLOT + 768, RED = 3 * SLOT + 1088;
+    // MX2: the deepest leaf wave's lane maxima for wave 0's residual row ([m2 64 | m5 64 | m0, m1,
+    // m3, m4 of lanes 0..15])
+    static constexpr int WQ = 3 * SLOT, WR = 3 * SLOT + 640, LEC = 3 * SLOT + 768, MX2 = 3 * SLOT + 1088;
 };
 static_assert(Cps::UB + 256 <= 2 * Cps::SLOT && 6 * Cps::SS <= 2 * Cps::SLOT, "slots 0-1");
-static_assert(Cps::KPS + 272 <= 3 * Cps::SLOT && Cps::RED + 96 <= 4 * Cps::SLOT, "slot tails");
+static_assert(Cps::KPS + 272 <= 3 * Cps::SLOT && Cps::MX2 + 192 <= 4 * Cps::SLOT, "slot tails");
 
 // The CP operands through registers: every lane loads up to four pairs of the region (pair f =
 // doubles 2 f, 2 f + 1 of Cpa, f = tid + 512 s) with 8-byte loads at valid addresses (zeros from
@@ -603,6 +605,28 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
     rs.ra = T(1) / rs.alpha;
     const T alpha = rs.alpha, ra = rs.ra;
     bool nanf = false;  // a NaN reached a box (Rectangle._constrain raises)
+    // the wave's residual row (its six maxima by DPP; lanes 58..63 hold all six and store one
+    // each), written by every wave once its terms are final: in the idle time of its role where
+    // it has one, so that only waves 1 and 4 reduce (one maximum) behind the last barrier
+    // (lane 63 stores the row as three 16-B stores: a per-lane pick of one of six values became
+    // an indexed private array in scratch, whose load waited for every store of the wave)
+    auto put_row = [&](const double (&mm)[6]) {
+        if (lane == 63) {
+            glb2* row = (glb2*)(a.part + ((size_t)blockIdx.x * 8 + wv) * 6);
+            row[0] = d2v{mm[0], mm[1]};
+            row[1] = d2v{mm[2], mm[3]};
+            row[2] = d2v{mm[4], mm[5]};
+        }
+    };
+    auto emit_row = [&]() {
+        const double mm[6] = {wave_bmax(rs.m0.get()), wave_bmax(rs.m1.get()), wave_bmax(rs.m2.get()),
+                              wave_bmax(rs.m3.get()), wave_bmax(rs.m4.get()), wave_bmax(rs.m5.get())};
+        put_row(mm);
+    };
+    auto zero_row = [&]() {
+        const double mm[6] = {0, 0, 0, 0, 0, 0};
+        put_row(mm);
+    };
     const bool live = lo < 15;
     const int lq = live ? lo : 0;
     const int i = gnode(R0, lq), yo = G * i;  // this lane's parent (global)
@@ -855,6 +879,20 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             }
             eA[rt][e] = ep;
         }
+        // its terms are final here (the leaf box terms are wave 4's): the lane maxima to LDS for
+        // wave 0's row (m2, m5 of every lane; m0, m1, m3, m4 of the lanes h = 0 that account s_l)
+        {
+            ldsd* mx = SL + Cps::MX2;
+            mx[lane] = rs.m2.get();
+            mx[64 + lane] = rs.m5.get();
+            if (h == 0) {
+                mx[128 + lo] = rs.m0.get();
+                mx[144 + lo] = rs.m1.get();
+                mx[160 + lo] = rs.m3.get();
+                mx[176 + lo] = rs.m4.get();
+            }
+        }
+        zero_row();
         // the eta+ stream (after barrier B, the same wave): sqrtPf' eta11+ onto the box term
         lds_sync();  // B
         dstamp(2);
@@ -869,7 +907,8 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
                     const T lzv = XL[lo * NX + r], lpv = A[Cpa::LP + lo * NX + r], d14 = A[Cpa::D14 + lo * NX + r];
                     const T v = (d14 + alpha * (T(2) * lzv - lpv)) * ra;
                     T ep, x2;
-                    rs.fin(d14, v, box_sel(v, BX[2 * (NX + NU) + r], BX[2 * (NX + NU) + NX + r], nanf), lzv - lpv, ep, x2);
+                    Resid<T> dup = rs;  // (the terms are wave 4's: the same entries)
+                    dup.fin(d14, v, box_sel(v, BX[2 * (NX + NU) + r], BX[2 * (NX + NU) + NX + r], nanf), lzv - lpv, ep, x2);
                     gA[rt][e] = ep;
                     gput(stv, eo, a.E14 + m + (l - m) * NX + r, ep);
                 }
@@ -885,6 +924,10 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             ox[rt][e] = lz[rt][e] - alpha * gA[rt][e];
         if (stv) st_rows_o<T, NX>(out, X0 + l * NX, true, ox);
     }
+    // rows final at A: wave 5 (phase 1), wave 6 (the children's s); none: wave 3, and waves 2, 4
+    // outside the deepest tier
+    if (wv == 5 || wv == 6) emit_row();
+    else if (wv == 3 || ((wv == 2 || wv == 4) && !deepest)) zero_row();
     if (!(wv < 2 || (wv == 2 && deepest))) lds_sync();  // A2
     if (BXN == 1 && wv == 7) {
         // ================= the box rows of the families (Rectangle on eta7 = [x_i | u_i],
@@ -926,6 +969,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         dstamp(2);
         lds_sync();  // B: the stream rows, tau, s, y of the half step are in LDS
     }
+    if (wv == 7) emit_row();  // its box terms (zeros when unboxed)
     // ============ II: the L^T streams (operators.py:73-94), one MFMA chain per wave
     if (wv == 0 || wv == 1 || wv == 3) {
         // families: wave 0 the eta+ stream onto Gamma' eta7 (box) -> x_i, u_i of the half step;
@@ -966,6 +1010,18 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                 ou[rt][e] = uz[rt][e] - alpha * hh[rt][e];
             if (stv) st_rows_o<T, NU>(out, U0 + i * NU, live, ou);
+            if (deepest) {  // the leaf wave's lane maxima join this wave's row
+                const ldsd* mx = SL + Cps::MX2;
+                const T v2 = mx[lane], v5 = mx[64 + lane];
+                const T v0 = mx[128 + lo], v1 = mx[144 + lo], v3 = mx[160 + lo], v4 = mx[176 + lo];
+                rs.m2.add(v2);
+                rs.m5.add(v5);
+                rs.m0.add(h == 0 ? v0 : T(0));
+                rs.m1.add(h == 0 ? v1 : T(0));
+                rs.m3.add(h == 0 ? v3 : T(0));
+                rs.m4.add(h == 0 ? v4 : T(0));
+            }
+            emit_row();
             dstamp(3);
             lds_sync();  // C
         } else if (wv == 3) {
@@ -977,18 +1033,28 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             dstamp(3);
             lds_sync();  // C
         } else {
-            dstamp(3);
-            lds_sync();  // C
-            // ============ III: the residual terms of x_i, u_i from both streams
+            // ============ III: the residual terms of x_i, u_i from both streams; all but the xi2
+            // stream's (xi0 = xi1 + L^T xi2) before barrier C, with the row's other five maxima
             T xz[RX][4], xp[RX][4], uz[RU][4], up[RU][4];
             ld_lr<NX>(XD + lq * SXD, live, xz);
             ld_lr<NX>(A + Cpa::PX + lq * NX, live, xp);
             ld_lr<NU>(U + lq * NU, live, uz);
             ld_lr<NU>(A + Cpa::PU + lq * NU, live, up);
+            T x1x[RX][4], x1u[RU][4];
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
-                if (tok<NX>(rt, e)) rs.account(xp[rt][e], xz[rt][e], g[rt][e], A[Cpa::SC + cpos<NX>(rt, e)]);
+                if (tok<NX>(rt, e)) x1x[rt][e] = rs.account_pre(xp[rt][e], xz[rt][e], g[rt][e]);
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
-                if (tok<NU>(rt, e)) rs.account(up[rt][e], uz[rt][e], hh[rt][e], A[Cpa::SC + SX + cpos<NU>(rt, e)]);
+                if (tok<NU>(rt, e)) x1u[rt][e] = rs.account_pre(up[rt][e], uz[rt][e], hh[rt][e]);
+            double mm[6] = {0, wave_bmax(rs.m1.get()), wave_bmax(rs.m2.get()), wave_bmax(rs.m3.get()),
+                            wave_bmax(rs.m4.get()), wave_bmax(rs.m5.get())};
+            dstamp(3);
+            lds_sync();  // C
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) rs.account_post(x1x[rt][e], A[Cpa::SC + cpos<NX>(rt, e)]);
+            _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NU>(rt, e)) rs.account_post(x1u[rt][e], A[Cpa::SC + SX + cpos<NU>(rt, e)]);
+            mm[0] = wave_bmax(rs.m0.get());
+            put_row(mm);
         }
     } else if ((wv == 4 || wv == 5) && deepest) {
         // leaves: wave 4 the (d - eta+) stream, wave 5 the xi2 stream (to LDS for wave 4's terms)
@@ -1002,7 +1068,12 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
                     const T lzv = XL[lo * NX + r], lpv = A[Cpa::LP + lo * NX + r], d14 = A[Cpa::D14 + lo * NX + r];
                     const T v = (d14 + alpha * (T(2) * lzv - lpv)) * ra;
                     T ep, x2;
-                    rs.fin(d14, v, box_sel(v, BX[2 * (NX + NU) + r], BX[2 * (NX + NU) + NX + r], nanf), lzv - lpv, ep, x2);
+                    Resid<T> dup = rs;  // the entry's terms: wave 4's (waves 2 and 5 compute the same entries)
+                    dup.fin(d14, v, box_sel(v, BX[2 * (NX + NU) + r], BX[2 * (NX + NU) + NX + r], nanf), lzv - lpv, ep, x2);
+                    if (wv == 4) {
+                        rs.m2.add(x2);
+                        rs.m5.add(ep - d14);
+                    }
                     g[rt][e] = wv == 4 ? d14 - ep : x2;
                 }
                 __builtin_amdgcn_sched_barrier(0);  // a row block at a time: bounded live operands
@@ -1020,13 +1091,20 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             dstamp(3);
             lds_sync();  // C
         } else {
-            dstamp(3);
-            lds_sync();  // C
-            T lz[RX][4], lp[RX][4];
+            // the leaves' residual terms as wave 1's: all but xi0 before barrier C
+            T lz[RX][4], lp[RX][4], x1x[RX][4];
             ld_lr<NX>(XL + lo * NX, true, lz);
             ld_lr<NX>(A + Cpa::LP + lo * NX, true, lp);
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
-                if (tok<NX>(rt, e)) rs.account(lp[rt][e], lz[rt][e], g[rt][e], A[Cpa::D11 + cpos<NX>(rt, e)]);
+                if (tok<NX>(rt, e)) x1x[rt][e] = rs.account_pre(lp[rt][e], lz[rt][e], g[rt][e]);
+            double mm[6] = {0, wave_bmax(rs.m1.get()), wave_bmax(rs.m2.get()), wave_bmax(rs.m3.get()),
+                            wave_bmax(rs.m4.get()), wave_bmax(rs.m5.get())};
+            dstamp(3);
+            lds_sync();  // C
+            _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
+                if (tok<NX>(rt, e)) rs.account_post(x1x[rt][e], A[Cpa::D11 + cpos<NX>(rt, e)]);
+            mm[0] = wave_bmax(rs.m0.get());
+            put_row(mm);
         }
     } else if (wv == 6 && live) {
         // ================= the AVaR kernel projection of the family (cache.py:290-317)
@@ -1058,19 +1136,6 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
     }
     dstamp(5);
     flag_nan(a.ctl, nanf, a.nanbit);
-    // one residual row per wave (no workgroup barrier behind the last role): the six maxima by
-    // DPP, lanes 58..63 (which hold all six) store one each
-    {
-        const double mm[6] = {wave_bmax(rs.m0.get()), wave_bmax(rs.m1.get()), wave_bmax(rs.m2.get()),
-                              wave_bmax(rs.m3.get()), wave_bmax(rs.m4.get()), wave_bmax(rs.m5.get())};
-        dstamp(6);
-        if (lane >= 58) {
-            const int q = lane - 58;
-            double v = mm[0];
-            _Pragma("unroll") for (int qq = 1; qq < 6; ++qq) v = q == qq ? mm[qq] : v;
-            a.part[((size_t)blockIdx.x * 8 + wv) * 6 + q] = v;
-        }
-    }
     dstamp(4);
 }
 
