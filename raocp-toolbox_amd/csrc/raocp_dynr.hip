@@ -44,6 +44,9 @@
 
 #include "raocp_dynr.h"
 #define RAOCP_AMAX_BITS
+// sum_h by shuffles here: the row-swap form (raocp_tile.h) spills 4 VGPRs in k_drc and measured
+// 0.25 us per iteration slower (profiles/r06/drc_variants.log)
+#define RAOCP_SUMH_SHFL
 #include "raocp_cpops.h"
 
 namespace raocp {
@@ -530,14 +533,39 @@ __device__ __forceinline__ void cpa_commit(ldsd* A, const CpaStage& st) {
 __device__ __forceinline__ double bmax(double a, double b) {
     return (unsigned long long)__double_as_longlong(a) > (unsigned long long)__double_as_longlong(b) ? a : b;
 }
+// (the steps whose rows and banks are all written take no "old" operand: no copy per step)
+template <int CTRL>
+__device__ __forceinline__ double dpp_full(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// N maxima at once, step by step (independent chains interleaved: the DPP hazards of one value
+// are filled with the others' work)
+template <int N>
+__device__ __forceinline__ void wave_bmax_n(double (&v)[N]) {
+#ifdef RAOCP_BMAX_SEQ
+    _Pragma("unroll") for (int q = 0; q < N; ++q) {
+        v[q] = bmax(v[q], dpp_full<0xB1>(v[q]));
+        v[q] = bmax(v[q], dpp_full<0x4E>(v[q]));
+        v[q] = bmax(v[q], dpp_full<0x141>(v[q]));
+        v[q] = bmax(v[q], dpp_full<0x140>(v[q]));
+        v[q] = bmax(v[q], dpp_d<0x142, 0xA>(v[q]));
+        v[q] = bmax(v[q], dpp_d<0x143, 0xC>(v[q]));
+    }
+    return;
+#endif
+    _Pragma("unroll") for (int q = 0; q < N; ++q) v[q] = bmax(v[q], dpp_full<0xB1>(v[q]));   // lane ^ 1
+    _Pragma("unroll") for (int q = 0; q < N; ++q) v[q] = bmax(v[q], dpp_full<0x4E>(v[q]));   // lane ^ 2
+    _Pragma("unroll") for (int q = 0; q < N; ++q) v[q] = bmax(v[q], dpp_full<0x141>(v[q]));  // row half-mirror
+    _Pragma("unroll") for (int q = 0; q < N; ++q) v[q] = bmax(v[q], dpp_full<0x140>(v[q]));  // row mirror
+    _Pragma("unroll") for (int q = 0; q < N; ++q) v[q] = bmax(v[q], dpp_d<0x142, 0xA>(v[q]));  // row_bcast15
+    _Pragma("unroll") for (int q = 0; q < N; ++q) v[q] = bmax(v[q], dpp_d<0x143, 0xC>(v[q]));  // row_bcast31
+}
 __device__ __forceinline__ double wave_bmax(double v) {
-    v = bmax(v, dpp_d<0xB1, 0xF>(v));   // lane ^ 1
-    v = bmax(v, dpp_d<0x4E, 0xF>(v));   // lane ^ 2
-    v = bmax(v, dpp_d<0x141, 0xF>(v));  // row half-mirror
-    v = bmax(v, dpp_d<0x140, 0xF>(v));  // row mirror
-    v = bmax(v, dpp_d<0x142, 0xA>(v));  // row_bcast15 into rows 1 and 3
-    v = bmax(v, dpp_d<0x143, 0xC>(v));  // row_bcast31 into rows 2 and 3
-    return v;
+    double a[1] = {v};
+    wave_bmax_n<1>(a);
+    return a[0];
 }
 
 // an R-row node vector from an LDS row in the tile's row layout (raocp_tile.h ld_rows), zero
@@ -619,8 +647,8 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         }
     };
     auto emit_row = [&]() {
-        const double mm[6] = {wave_bmax(rs.m0.get()), wave_bmax(rs.m1.get()), wave_bmax(rs.m2.get()),
-                              wave_bmax(rs.m3.get()), wave_bmax(rs.m4.get()), wave_bmax(rs.m5.get())};
+        double mm[6] = {rs.m0.get(), rs.m1.get(), rs.m2.get(), rs.m3.get(), rs.m4.get(), rs.m5.get()};
+        wave_bmax_n<6>(mm);
         put_row(mm);
     };
     auto zero_row = [&]() {
@@ -1045,15 +1073,15 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
                 if (tok<NX>(rt, e)) x1x[rt][e] = rs.account_pre(xp[rt][e], xz[rt][e], g[rt][e]);
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                 if (tok<NU>(rt, e)) x1u[rt][e] = rs.account_pre(up[rt][e], uz[rt][e], hh[rt][e]);
-            double mm[6] = {0, wave_bmax(rs.m1.get()), wave_bmax(rs.m2.get()), wave_bmax(rs.m3.get()),
-                            wave_bmax(rs.m4.get()), wave_bmax(rs.m5.get())};
+            double m5[5] = {rs.m1.get(), rs.m2.get(), rs.m3.get(), rs.m4.get(), rs.m5.get()};
+            wave_bmax_n<5>(m5);
             dstamp(3);
             lds_sync();  // C
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                 if (tok<NX>(rt, e)) rs.account_post(x1x[rt][e], A[Cpa::SC + cpos<NX>(rt, e)]);
             _Pragma("unroll") for (int rt = 0; rt < RU; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                 if (tok<NU>(rt, e)) rs.account_post(x1u[rt][e], A[Cpa::SC + SX + cpos<NU>(rt, e)]);
-            mm[0] = wave_bmax(rs.m0.get());
+            const double mm[6] = {wave_bmax(rs.m0.get()), m5[0], m5[1], m5[2], m5[3], m5[4]};
             put_row(mm);
         }
     } else if ((wv == 4 || wv == 5) && deepest) {
@@ -1097,13 +1125,13 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             ld_lr<NX>(A + Cpa::LP + lo * NX, true, lp);
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                 if (tok<NX>(rt, e)) x1x[rt][e] = rs.account_pre(lp[rt][e], lz[rt][e], g[rt][e]);
-            double mm[6] = {0, wave_bmax(rs.m1.get()), wave_bmax(rs.m2.get()), wave_bmax(rs.m3.get()),
-                            wave_bmax(rs.m4.get()), wave_bmax(rs.m5.get())};
+            double m5[5] = {rs.m1.get(), rs.m2.get(), rs.m3.get(), rs.m4.get(), rs.m5.get()};
+            wave_bmax_n<5>(m5);
             dstamp(3);
             lds_sync();  // C
             _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e)
                 if (tok<NX>(rt, e)) rs.account_post(x1x[rt][e], A[Cpa::D11 + cpos<NX>(rt, e)]);
-            mm[0] = wave_bmax(rs.m0.get());
+            const double mm[6] = {wave_bmax(rs.m0.get()), m5[0], m5[1], m5[2], m5[3], m5[4]};
             put_row(mm);
         }
     } else if (wv == 6 && live) {
@@ -1377,7 +1405,7 @@ __device__ __forceinline__ void cp_check_block(const ChkArg& ck, ldsd* red) {
     }
     for (int r = tid + 8 * nt; r < ck.rows; r += nt)
         _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = bmax(m[q], ck.part[(size_t)r * 6 + q]);
-    _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = wave_bmax(m[q]);
+    wave_bmax_n<6>(m);
     if (lane == 63) _Pragma("unroll") for (int q = 0; q < 6; ++q) red[q * 16 + wv] = m[q];
     __syncthreads();
     if (tid != 0) return;

@@ -178,9 +178,32 @@ __device__ __forceinline__ T ldz_o(cglbp<T> base, unsigned off, bool live) {
 // sum over the 4 lane groups (the rows of one node)
 template <class T>
 __device__ __forceinline__ T sum_h(T v) {
+#ifdef RAOCP_SUMH_SHFL
     v += __shfl_xor(v, 16, 64);
     v += __shfl_xor(v, 32, 64);
     return v;
+#endif
+    // lanes l ^ 16 and l ^ 32 by gfx950's row swaps (v_permlane16_swap / v_permlane32_swap: VALU
+    // moves, no LDS round trip as ds_bpermute); every lane adds its own value and its partner's,
+    // so the four lane groups end with the same sum, as with the shuffles
+    if constexpr (sizeof(T) == 8) {
+        auto sw16 = [](T x) {
+            const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(x), __double2loint(x), false, false);
+            const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(x), __double2hiint(x), false, false);
+            return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+        };
+        auto sw32 = [](T x) {
+            const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(x), __double2loint(x), false, false);
+            const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(x), __double2hiint(x), false, false);
+            return __hiloint2double(hi[0], lo[0]) + __hiloint2double(hi[1], lo[1]);
+        };
+        return sw32(sw16(v));
+    } else {
+        const auto a = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+        const T w = __int_as_float(a[0]) + __int_as_float(a[1]);
+        const auto b = __builtin_amdgcn_permlane32_swap(__float_as_int(w), __float_as_int(w), false, false);
+        return __int_as_float(b[0]) + __int_as_float(b[1]);
+    }
 }
 
 template <class T>

@@ -5,6 +5,7 @@
 #   drc         tests/test_gpu_drc.py (the fused dynamics + CP launch k_drc)
 #   drcq        its config-2 parity cases only
 #   drcchk      tools/drc_check.py: the fused loop against the pair and the oracle, op / loop times
+#   drcvar      tools/drc_check.py for each library in $DRC_LIBS ("default" or build/var/<v>.so)
 #   drcstamps   tools/drc_stamps.py on the diagnostic variant build/var/diag.so (VAR_UNIT=dynr)
 #   dynr        tests/test_gpu_dynr.py (the regular-tree sweep)
 #   cp4         tests/test_gpu_cp4.py (k_cp4 against k_cp3 and the oracle)
@@ -51,6 +52,11 @@ for step in "$@"; do
           tail -3 $out/pytest_drcq.log ;;
     drcchk) timeout -k 10 240 python -u tools/drc_check.py 30 > $out/drc_check.log 2>&1 || fail $step $out/drc_check.log
           cat $out/drc_check.log ;;
+    drcvar) for v in ${DRC_LIBS:-}; do
+              if [ "$v" = default ]; then lib=raocp-toolbox_amd/raocp/core/libraocp_hip.so; else lib=build/var/$v.so; fi
+              RAOCP_HIP_LIB=$lib timeout -k 10 120 python -u tools/drc_check.py 30 > $out/drc_check_$v.log 2>&1 || fail $step $out/drc_check_$v.log
+              echo "variant $v: $(grep -h 'op 11\|loop' $out/drc_check_$v.log | tr '\n' ' ')"
+            done ;;
     drcstamps) RAOCP_HIP_LIB=build/var/diag.so RAOCP_STAMP_KERNEL=f timeout -k 10 120 python -u tools/drc_stamps.py 6 > $out/drc_stamps.log 2>&1 || fail $step $out/drc_stamps.log
           cat $out/drc_stamps.log ;;
     drcprobe) RAOCP_HIP_LIB=build/var/diag.so timeout -k 10 300 python -u tools/drc_probe.py 400 > $out/drc_probe.log 2>&1 || fail $step $out/drc_probe.log
