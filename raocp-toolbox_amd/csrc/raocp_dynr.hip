@@ -614,7 +614,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
     const int tid = threadIdx.x, lane = tid & 63, lo = lane & 15, h = lane >> 4, wv = tid >> 6;
     // diagnostics: per-wave stamps of the first (deepest) and the last (top) workgroup at
     // 3072 + {0, 64} + 8 wave + {0 start, 1 first role done, 2 second role done, 3 third role
-    // done, 5 last role done, 6 maxima reduced, 4 end}
+    // done, 5 last role done, 4 end; slot waves: 6 after barrier A2, 7 their block's SOC}
     auto dstamp = [&](int q) {
         if (kDiag && dstamps && lane == 0 && (blockIdx.x == 0 || (int)blockIdx.x == nblk - 1))
             dstamps[3072 + ((int)blockIdx.x == 0 ? 0 : 64) + 8 * wv + q] = __builtin_amdgcn_s_memrealtime();
@@ -649,6 +649,20 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
     auto emit_row = [&]() {
         double mm[6] = {rs.m0.get(), rs.m1.get(), rs.m2.get(), rs.m3.get(), rs.m4.get(), rs.m5.get()};
         wave_bmax_n<6>(mm);
+        put_row(mm);
+    };
+    // rows of waves whose terms feed only some maxima: the others stay zero (wave 6 accounts s_j
+    // only: xi0, xi1, delta0, delta1; wave 7 the box entries only: xi2, delta2)
+    auto emit_acc_row = [&]() {
+        double m4[4] = {rs.m0.get(), rs.m1.get(), rs.m3.get(), rs.m4.get()};
+        wave_bmax_n<4>(m4);
+        const double mm[6] = {m4[0], m4[1], 0, m4[2], m4[3], 0};
+        put_row(mm);
+    };
+    auto emit_fin_row = [&]() {
+        double m2[2] = {rs.m2.get(), rs.m5.get()};
+        wave_bmax_n<2>(m2);
+        const double mm[6] = {0, 0, m2[0], 0, 0, m2[1]};
         put_row(mm);
     };
     auto zero_row = [&]() {
@@ -816,6 +830,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         const ldsd* sc = A + Cpa::SC + (cl - 1) * 16;
         const T d5 = live ? sc[0] : T(0), d6 = live ? sc[1] : T(0), tz = live ? sc[2] : T(0), tp = live ? sc[3] : T(0);
         lds_sync();  // A2
+        dstamp(6);
         // ---------------- the child block SOC (cache.py:321-372)
         T v3[RX][4], v4_[RU][4];
         T ss = T(0);
@@ -833,6 +848,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         const T v6 = (d6 + alpha * a5) * ra + T(0.5);
         ss += v5 * v5;
         const Soc<T> so(sqrt(ss), v6);
+        dstamp(7);
         // each entry's (eta+, d - eta+, xi2) straight to the slot's stream rows and eta+ to the dual
         ldsd* sk = SL + Cps::SB + k * 3 * SS;
         _Pragma("unroll") for (int rt = 0; rt < RX; ++rt) _Pragma("unroll") for (int e = 0; e < 4; ++e) {
@@ -952,11 +968,13 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             ox[rt][e] = lz[rt][e] - alpha * gA[rt][e];
         if (stv) st_rows_o<T, NX>(out, X0 + l * NX, true, ox);
     }
-    // rows final at A: wave 5 (phase 1), wave 6 (the children's s); none: wave 3, and waves 2, 4
-    // outside the deepest tier
-    if (wv == 5 || wv == 6) emit_row();
-    else if (wv == 3 || ((wv == 2 || wv == 4) && !deepest)) zero_row();
     if (!(wv < 2 || (wv == 2 && deepest))) lds_sync();  // A2
+    // rows final at A, written in the waves' idle time up to barrier B (not before A2, which the
+    // slot waves wait for): wave 5 (phase 1), wave 6 (the children's s); none: wave 3, and
+    // waves 2, 4 outside the deepest tier
+    if (wv == 5) emit_row();
+    else if (wv == 6) emit_acc_row();
+    else if (wv == 3 || ((wv == 2 || wv == 4) && !deepest)) zero_row();
     if (BXN == 1 && wv == 7) {
         // ================= the box rows of the families (Rectangle on eta7 = [x_i | u_i],
         // cache.py:374-393): eta7+ to the dual, and per entry the three streams' seeds
@@ -997,7 +1015,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         dstamp(2);
         lds_sync();  // B: the stream rows, tau, s, y of the half step are in LDS
     }
-    if (wv == 7) emit_row();  // its box terms (zeros when unboxed)
+    if (wv == 7) emit_fin_row();  // its box terms (zeros when unboxed)
     // ============ II: the L^T streams (operators.py:73-94), one MFMA chain per wave
     if (wv == 0 || wv == 1 || wv == 3) {
         // families: wave 0 the eta+ stream onto Gamma' eta7 (box) -> x_i, u_i of the half step;

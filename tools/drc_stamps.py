@@ -36,6 +36,6 @@ for rep in range(reps):
         s = st[base:base + 64].reshape(8, 8)
         s = np.where(s > 0, (s - t0) * 10, -1)
         print(f"rep {rep} {which} (fwd done {w[b, 3]}): per wave [start, role, barrier, role2, last role, "
-              f"end] ns", flush=True)
+              f"end, (slot waves: A2, SOC)] ns", flush=True)
         for wv in range(8):
-            print(f"    wave {wv}: " + " ".join(f"{x:6d}" for x in s[wv, [0, 1, 2, 3, 5, 4]]), flush=True)
+            print(f"    wave {wv}: " + " ".join(f"{x:6d}" for x in s[wv, [0, 1, 2, 3, 5, 4, 6, 7]]), flush=True)
