@@ -119,8 +119,17 @@ def pmc_traffic(kernel):
             ks = json.load(open(f))["kernels"]
         except Exception:
             continue
-        if all(name in ks for name, _ in terms):
-            return sum(cnt * ks[name]["traffic_bytes"] for name, cnt in terms), os.path.relpath(f, ROOT)
+        # a profiled name may carry template arguments raocp_kernel_info leaves out (the box
+        # pattern, the block size): "k_drc<20, 8, 2>" matches "k_drc<20, 8, 2, 1>"
+        def find(name):
+            if name in ks:
+                return ks[name]
+            stem = name[:-1] + ", " if name.endswith(">") else None
+            hits = [v for k, v in ks.items() if stem and k.startswith(stem)]
+            return hits[0] if len(hits) == 1 else None
+        found = [(find(name), cnt) for name, cnt in terms]
+        if all(v is not None for v, _ in found):
+            return sum(cnt * v["traffic_bytes"] for v, cnt in found), os.path.relpath(f, ROOT)
     return None, None
 
 
