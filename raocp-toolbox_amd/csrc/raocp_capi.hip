@@ -149,6 +149,7 @@ struct raocp_ctx {
     // sets of cp_rows rows (the extra workgroup tests the previous iteration beside the next)
     bool drc = false;
     raocp::DrcArg drca{};
+    raocp::DrcArg* d_drca = nullptr;  // drca per iteration parity in device memory (k_drc reads it there)
     size_t drc_lds = 0;
     size_t dr_gran = 0;  // granules of each hand-off buffer
     double* x0 = nullptr;
@@ -940,6 +941,8 @@ int dr_setup(raocp_ctx* c, const std::vector<double>& WT, int SKP, const std::ve
 // RAOCP_DRC=0 keeps them. Its weight image is k_cp3's [sqrtQ | sqrtR | sqrtPf] followed by the
 // one box table of each kind [lo_nl | hi_nl | lo_l | hi_l] (zeros when unboxed); its residual rows
 // are two sets of one row per sweep wave (8 per workgroup, drc_part).
+double* drc_part(raocp_ctx* c, int q);
+int drc_nanbit(int q);
 int drc_setup(raocp_ctx* c) {
     c->drc = false;
     if (!c->dr || !c->cp6 || c->f32 || c->sh_S > 0 || !raocp::drc_supported(c->nx, c->nu, c->reg_C)) return RAOCP_OK;
@@ -993,6 +996,19 @@ int drc_setup(raocp_ctx* c) {
     a.img = img;
     a.ctl = c->ctl;
     a.box = (bx & 3) == 1 ? 1 : 2;
+    // the launch's arguments in device memory, one copy per iteration parity (part / nanbit)
+    {
+        raocp::DrcArg two[2] = {a, a};
+        for (int q = 0; q < 2; ++q) {
+            two[q].part = drc_part(c, q);
+            two[q].nanbit = drc_nanbit(q);
+        }
+        double* d = nullptr;
+        const size_t words = (2 * sizeof(raocp::DrcArg) + 7) / 8;
+        if ((rc = c->alloc(&d, words))) return rc;
+        HIPCHK(hipMemcpy(d, two, sizeof(two), hipMemcpyHostToDevice));
+        c->d_drca = (raocp::DrcArg*)d;
+    }
     c->drc_lds = lds;
     c->drc = true;
     return RAOCP_OK;
@@ -1349,13 +1365,10 @@ double* drc_part(raocp_ctx* c, int q) { return c->redpart + (size_t)(q & 1) * c-
 int drc_nanbit(int q) { return 2 << (q & 1); }
 // the fused launch of iteration `it` (k = it mod 2 within a batch that starts at k = 0 mod 6)
 void launch_drc(raocp_ctx* c, int it, bool with_check) {
-    raocp::DrcArg a = c->drca;
-    a.part = drc_part(c, it);
-    a.nanbit = drc_nanbit(it);
     raocp::DrPlan p = c->drp;
     if (c->dev.stamps) p.stamps = c->dev.stamps;
     const raocp::ChkArg ck{c->ctl, c->hist, drc_part(c, it - 1), c->cp_rows, with_check ? 1 : 0, drc_nanbit(it - 1)};
-    raocp::drc_launch(p, a, c->drc_lds, c->bufs, c->ctl, ck, c->stream);
+    raocp::drc_launch(p, c->d_drca + (it & 1), c->drca.box, c->drc_lds, c->bufs, ck, c->stream);
 }
 int enqueue_cp_iteration(raocp_ctx* c, int it) {
     const raocp::Bufs keep = c->bufs;

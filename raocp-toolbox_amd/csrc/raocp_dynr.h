@@ -114,7 +114,8 @@ int drc_occupancy(size_t lds);
 // one launch: the projection of z1 = pick3(bf, 1) in place, then the CP iteration of every family
 // (p = bf.z0, eta = bf.e0 -> eta+ = bf.e1, the next half step -> bf.z2); ck: the previous
 // iteration's stopping test (an extra workgroup)
-void drc_launch(const DrPlan& pl, const DrcArg& a, size_t lds, Bufs bf, const Ctl* ctl, ChkArg ck, hipStream_t s);
+// dca: the DrcArg of this launch in device memory (one per iteration parity, raocp_capi.hip)
+void drc_launch(const DrPlan& pl, const DrcArg* dca, int box, size_t lds, Bufs bf, ChkArg ck, hipStream_t s);
 const char* drc_name();
 // this translation unit compiled with the in-kernel stamps (make DIAG=1, or a VAR_UNIT=dynr
 // variant build with -DRAOCP_DIAG, tools/build_var.sh)

@@ -1314,8 +1314,10 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
         wait_vm_c<(L - 1 - f) * TF::IPW + XW>();
         lds_sync();
         stamp(pl, stp);
+#ifndef DRC_NO_WDMA  // (timing probe builds only)
         if constexpr (CPF && f == 1) WAD::issue(SL + 3 * SLOT, ca->img);
         if constexpr (CPF && f == 2) WBD::issue(SL + 2 * SLOT, ca->img + Cps::WA);
+#endif
         if (work && !(kDiag && (pl.fault & 16))) {
             const bool last = f == L - 1;
             fwd_level<NX, NU, C, BS, UMAX, cnt>(SL + (L - 1 - f) * SLOT, XD + off * SXD, last ? XL : XD + (off + cnt) * SXD,
@@ -1358,9 +1360,11 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
     }
     if constexpr (CPF) {
         wg_stamp(pl, 3);
+#ifndef DRC_NO_CPCODE  // (timing probe builds only)
         if (work && !(kDiag && (pl.fault & 64)))
             cp_phase<NX, NU, BX, BX>(*ca, *bfp, alpha, pl.X0, pl.U0, R0, deepest, XD, XL, U, CPA, SL,
                                      kDiag ? pl.stamps : nullptr, pl.nblk, !(kDiag && (pl.fault & 1024)));
+#endif
     }
     if (top && tid == 0) st_u32(pl.sync, tag);  // every workgroup has read the epoch
 }
@@ -1450,7 +1454,7 @@ __device__ __forceinline__ void cp_check_block(const ChkArg& ck, ldsd* red) {
 // are the other of the two alternating row sets, ck.part).
 template <int NX, int NU, int C, int BX>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
-k_drc(DrPlan pl, DrcArg ca, Bufs bf, ChkArg ck) {
+k_drc(DrPlan pl, const DrcArg* __restrict__ cap, Bufs bf, ChkArg ck) {
     extern __shared__ __attribute__((aligned(16))) double smem_[];
     __shared__ Stamps stp;
     __shared__ int s_ok;
@@ -1466,8 +1470,12 @@ k_drc(DrPlan pl, DrcArg ca, Bufs bf, ChkArg ck) {
     const unsigned long long sw = sload_pair(pl.sync);
     const unsigned err = (unsigned)(sw >> 32);
     const unsigned tag = (unsigned)sw + 1u;
-    const int done = ca.ctl->done;
-    const double alpha = ca.ctl->alpha;  // the CP step size, read at the start (not on the CP path)
+    // the CP arguments are read from device memory where the CP step uses them (as kernel
+    // arguments they were loaded at the start and kept in scalar registers across the sweep,
+    // which then spilled scalars inside its levels)
+    Ctl* ctl = cap->ctl;
+    const int done = ctl->done;
+    const double alpha = ctl->alpha;  // the CP step size, read at the start (not on the CP path)
     stamp(pl, stp);
     wg_stamp(pl, 0);
     if (err) return;
@@ -1475,7 +1483,7 @@ k_drc(DrPlan pl, DrcArg ca, Bufs bf, ChkArg ck) {
     role(pl, k, o);
     glbd* z = pick3(bf, 1);
     if (pl.t[k].L == 4)
-        tier_body<NX, NU, C, 512, 1, 4, BX>(pl, k, o, z, tag, done == 0, stp, s_ok, (ldsd*)smem_, &ca, &bf, alpha);
+        tier_body<NX, NU, C, 512, 1, 4, BX>(pl, k, o, z, tag, done == 0, stp, s_ok, (ldsd*)smem_, cap, &bf, alpha);
     stamp(pl, stp);
     stamp_flush(pl, stp, k, o);
     wg_stamp(pl, 2);
@@ -1547,15 +1555,14 @@ int drc_occupancy(size_t lds) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb2, kf2, 512, lds) != hipSuccess) return 0;
     return nb < nb2 ? nb : nb2;
 }
-void drc_launch(const DrPlan& pl, const DrcArg& a, size_t lds, Bufs bf, const Ctl* ctl, ChkArg ck, hipStream_t s) {
-    (void)ctl;
+void drc_launch(const DrPlan& pl, const DrcArg* dca, int box, size_t lds, Bufs bf, ChkArg ck, hipStream_t s) {
     const int grid = pl.nblk + (ck.on ? 1 : 0);
-    if (a.box == 1) {
+    if (box == 1) {
         (void)hipFuncSetAttribute((const void*)k_drc<20, 8, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        k_drc<20, 8, 2, 1><<<grid, 512, lds, s>>>(pl, a, bf, ck);
+        k_drc<20, 8, 2, 1><<<grid, 512, lds, s>>>(pl, dca, bf, ck);
     } else {
         (void)hipFuncSetAttribute((const void*)k_drc<20, 8, 2, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        k_drc<20, 8, 2, 2><<<grid, 512, lds, s>>>(pl, a, bf, ck);
+        k_drc<20, 8, 2, 2><<<grid, 512, lds, s>>>(pl, dca, bf, ck);
     }
 }
 const char* drc_name() { return "k_drc<20, 8, 2>"; }

@@ -23,7 +23,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
     print(f"fault {os.environ.get('RAOCP_DR_FAULT', '0'):>4s}  k_drc {1e3 * t11:7.2f} us  k_dr {1e3 * t9:7.2f} us", flush=True)
     sys.exit(0)
 reps = sys.argv[1] if len(sys.argv) > 1 else "400"
-for f in ("0", "64", "128", "192", "512", "576", "640", "704"):
+for f in os.environ.get("PROBE_FAULTS", "0 64 128 192 512 576 640 704").split():
     env = dict(os.environ, RAOCP_DR_FAULT=f)
     out = subprocess.run([sys.executable, __file__, "child", reps], env=env, capture_output=True, text=True, timeout=120)
     print(out.stdout.strip() or out.stderr.strip()[-300:], flush=True)

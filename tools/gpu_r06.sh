@@ -6,6 +6,8 @@
 #   drcq        its config-2 parity cases only
 #   drcchk      tools/drc_check.py: the fused loop against the pair and the oracle, op / loop times
 #   drcvar      tools/drc_check.py for each library in $DRC_LIBS ("default" or build/var/<v>.so)
+#   drskew      tools/dr_skew.py: k_dr's per-workgroup stamps (diagnostic variant build/var/diag.so)
+#   drlevels    tools/dr_levels.py: per-level stamps of k_dr and of the sweep inside k_drc
 #   drcstamps   tools/drc_stamps.py on the diagnostic variant build/var/diag.so (VAR_UNIT=dynr)
 #   dynr        tests/test_gpu_dynr.py (the regular-tree sweep)
 #   cp4         tests/test_gpu_cp4.py (k_cp4 against k_cp3 and the oracle)
@@ -57,10 +59,14 @@ for step in "$@"; do
               RAOCP_HIP_LIB=$lib timeout -k 10 120 python -u tools/drc_check.py 30 > $out/drc_check_$v.log 2>&1 || fail $step $out/drc_check_$v.log
               echo "variant $v: $(grep -h 'op 11\|loop' $out/drc_check_$v.log | tr '\n' ' ')"
             done ;;
+    drskew) RAOCP_HIP_LIB=build/var/diag.so timeout -k 10 120 python -u tools/dr_skew.py 2 5 > $out/dr_skew.log 2>&1 || fail $step $out/dr_skew.log
+          cat $out/dr_skew.log ;;
+    drlevels) RAOCP_HIP_LIB=build/var/diag.so timeout -k 10 120 python -u tools/dr_levels.py 4 > $out/dr_levels.log 2>&1 || fail $step $out/dr_levels.log
+          cat $out/dr_levels.log ;;
     drcstamps) RAOCP_HIP_LIB=build/var/diag.so RAOCP_STAMP_KERNEL=f timeout -k 10 120 python -u tools/drc_stamps.py 6 > $out/drc_stamps.log 2>&1 || fail $step $out/drc_stamps.log
           cat $out/drc_stamps.log ;;
-    drcprobe) RAOCP_HIP_LIB=build/var/diag.so timeout -k 10 300 python -u tools/drc_probe.py 400 > $out/drc_probe.log 2>&1 || fail $step $out/drc_probe.log
-          cat $out/drc_probe.log ;;
+    drcprobe) RAOCP_HIP_LIB=build/var/${PROBE_LIB:-diag}.so timeout -k 10 300 python -u tools/drc_probe.py 400 > $out/drc_probe_${PROBE_LIB:-diag}.log 2>&1 || fail $step $out/drc_probe_${PROBE_LIB:-diag}.log
+          cat $out/drc_probe_${PROBE_LIB:-diag}.log ;;
     dynr) timeout -k 10 500 $PYT tests/test_gpu_dynr.py > $out/pytest_dynr.log 2>&1 || fail $step $out/pytest_dynr.log
           tail -3 $out/pytest_dynr.log ;;
     cp4) timeout -k 10 500 $PYT tests/test_gpu_cp4.py > $out/pytest_cp4.log 2>&1 || fail $step $out/pytest_cp4.log
