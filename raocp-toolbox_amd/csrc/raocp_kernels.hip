@@ -813,7 +813,8 @@ __global__ void __launch_bounds__(kBlock) k_cp_check(Ctl* ctl, double* hist, con
         return;
     }
     double m[6] = {0, 0, 0, 0, 0, 0};
-    for (int r = threadIdx.x; r < rows; r += blockDim.x)
+    // (four rows per lane per round: their loads go out together)
+    _Pragma("unroll 4") for (int r = threadIdx.x; r < rows; r += blockDim.x)
         _Pragma("unroll") for (int q = 0; q < 6; ++q) m[q] = nmax(m[q], part[(size_t)r * 6 + q]);
     _Pragma("unroll") for (int q = 0; q < 6; ++q) s_m[q][threadIdx.x] = m[q];
     __syncthreads();
