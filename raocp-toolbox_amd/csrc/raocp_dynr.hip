@@ -597,10 +597,12 @@ __device__ __forceinline__ void gput(bool stv, glbp<double> b, unsigned o, doubl
     if (stv) *elw(b, o) = v;
 }
 
-template <int NX, int NU, int BXN, int BXL>
+// wo(t0, nt): the sweep's write-out of the projected x / u rows, run by waves 3 and 4 in their
+// wait between barriers A2 and B
+template <int NX, int NU, int BXN, int BXL, class WO>
 __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double alpha_in, int X0, int U0, int R0,
                                          bool deepest, const ldsd* XD, const ldsd* XL, const ldsd* U, ldsd* A,
-                                         ldsd* SL, unsigned long long* dstamps, int nblk, bool stv = true) {
+                                         ldsd* SL, unsigned long long* dstamps, int nblk, const WO& wo, bool stv = true) {
     typedef double T;
     typedef MF<T>::v4 v4;
     constexpr int C = 2, RX = (NX + 15) / 16, RU = (NU + 15) / 16, G = 2 * C + 1, NQ = (G + 3) / 4;
@@ -969,6 +971,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         if (stv) st_rows_o<T, NX>(out, X0 + l * NX, true, ox);
     }
     if (!(wv < 2 || (wv == 2 && deepest))) lds_sync();  // A2
+    if (wv == 3 || wv == 4) wo(tid - 192, 128);  // the sweep's write-out
     // rows final at A, written in the waves' idle time up to barrier B (not before A2, which the
     // slot waves wait for): wave 5 (phase 1), wave 6 (the children's s); none: wave 3, and
     // waves 2, 4 outside the deepest tier
@@ -1223,6 +1226,7 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
                 lds_sync();
                 if (!(pl.fault & 64))
                     cp_phase<NX, NU, BX, BX>(*ca, *bfp, alpha, pl.X0, pl.U0, R0, deepest, XD, XL, U, CPA, SL, nullptr, pl.nblk,
+                                             [](int, int) {},
                                          !(pl.fault & 1024));
             }
             return;
@@ -1338,32 +1342,41 @@ __device__ __forceinline__ void tier_body(const DrPlan& pl, int k, int o, glbd* 
         dma_wait();
         lds_sync();  // operands, weights and boxes in LDS for every wave
     }
-    if (work && !(kDiag && (pl.fault & 8))) {
+    // the write-out of the projected rows by lanes t0, t0 + nt, ...: by the whole workgroup here,
+    // or (k_drc) inside the CP step by two waves that wait there anyway, so that the CP step
+    // starts right behind the forward sweep
+    auto writeout = [&](int t0, int nt) {
+        if (!(work && !(kDiag && (pl.fault & 8)))) return;
         static_for<0, L + 1>([&](auto lc) {
             constexpr int l = lc.value, cnt = cpow(C, l), off = (cnt - 1) / (C - 1);
             if (l == 0 && !top) return;  // the parent writes this subtree's root row
             glb2* dst = (glb2*)(z + pl.X0 + (size_t)gl[l] * NX);
             if constexpr (l < L) {
-                for (int e = tid; e < cnt * (NX / 2); e += BS) {
+                for (int e = t0; e < cnt * (NX / 2); e += nt) {
                     const int r = e / (NX / 2), c = e - r * (NX / 2);
                     dst[e] = ld2(XD + (off + r) * SXD + 2 * c);
                 }
             } else {
-                for (int e = tid; e < NB * (NX / 2); e += BS) dst[e] = ld2(XL + 2 * e);
+                for (int e = t0; e < NB * (NX / 2); e += nt) dst[e] = ld2(XL + 2 * e);
             }
         });
         static_for<0, L>([&](auto lc) {
             constexpr int l = lc.value, cnt = cpow(C, l), off = (cnt - 1) / (C - 1);
             glb2* dst = (glb2*)(z + pl.U0 + (size_t)gl[l] * NU);
-            for (int e = tid; e < cnt * (NU / 2); e += BS) dst[e] = ld2(U + off * NU + 2 * e);
+            for (int e = t0; e < cnt * (NU / 2); e += nt) dst[e] = ld2(U + off * NU + 2 * e);
         });
-    }
+    };
+    if constexpr (!CPF) writeout(tid, BS);
     if constexpr (CPF) {
         wg_stamp(pl, 3);
 #ifndef DRC_NO_CPCODE  // (timing probe builds only)
         if (work && !(kDiag && (pl.fault & 64)))
             cp_phase<NX, NU, BX, BX>(*ca, *bfp, alpha, pl.X0, pl.U0, R0, deepest, XD, XL, U, CPA, SL,
-                                     kDiag ? pl.stamps : nullptr, pl.nblk, !(kDiag && (pl.fault & 1024)));
+                                     kDiag ? pl.stamps : nullptr, pl.nblk, writeout, !(kDiag && (pl.fault & 1024)));
+        else
+            writeout(tid, BS);
+#else
+        writeout(tid, BS);
 #endif
     }
     if (top && tid == 0) st_u32(pl.sync, tag);  // every workgroup has read the epoch
