@@ -101,7 +101,7 @@ struct DrcArg {
     int box;                  // 1: every node boxed by one table per kind; 2: no boxes
 };
 // doubles of the CP operand region of a workgroup (raocp_dynr.hip Cpa)
-constexpr int kDrcCpa = 3712;
+constexpr int kDrcCpa = 3904;
 // the weight image (DrcArg::img): [sqrtQ 640 | sqrtR 128] (kDrcWa doubles), then [sqrtPf 640 |
 // lo_nl 28 | hi_nl 28 | lo_l 20 | hi_l 20] (kDrcWb)
 constexpr int kDrcWa = 768, kDrcWb = 736;

@@ -377,25 +377,30 @@ __device__ __forceinline__ int lev2(int lc) { return 31 - __builtin_clz((unsigne
 __device__ __forceinline__ int gnode(int R0, int lc) { return (R0 << lev2(lc)) + lc; }
 
 // the CP operand region (doubles): rows of the 15 families lo (row 15 zero), their 30 children
-// c = 2 lo + 1 + k (row c - 1; rows 30, 31 zero), the deepest tier's 16 leaves q
+// c = 2 lo + 1 + k (row c - 1; rows 30, 31 zero), the deepest tier's 16 leaves q. The child
+// rows are padded (strides D3S, D4S, SCS, zeros in the padding) so that the 16 lanes lo, whose
+// child rows lie two rows apart, read distinct LDS banks: unpadded, the child scalars' stride
+// of 256 B put all 16 on one bank and eta4's on two
 struct Cpa {
+    static constexpr int D3S = 22, D4S = 10, SCS = 18;
     static constexpr int PX = 0;      // [16][20] x of p (the previous z+) at the parents
     static constexpr int PU = 320;    // [16][8]  u of p
-    static constexpr int D3 = 448;    // [32][20] eta3 of the children
-    static constexpr int D4 = 1088;   // [32][8]  eta4
-    static constexpr int SC = 1344;   // [32][16] eta5, eta6, tau of z+ / p; a nonleaf child's s of z+ / p,
-                                      //          eta2, cond of its children, y of z+ / p (entries 0, 1, 2C)
-    static constexpr int PS = 1856;   // [16][24] y of z+ / p (5 + 5), eta1 (5), s of z+ / p, eta2,
+    static constexpr int D3 = 448;    // [32][D3S] eta3 of the children
+    static constexpr int D4 = 1152;   // [32][D4S] eta4
+    static constexpr int SC = 1472;   // [32][SCS] eta5, eta6, tau of z+ / p; a nonleaf child's s of z+ / p,
+                                      //           eta2, cond of its children, y of z+ / p (entries 0, 1, 2C)
+    static constexpr int PS = 2048;   // [16][24] y of z+ / p (5 + 5), eta1 (5), s of z+ / p, eta2,
                                       //          cond of the children (2), AVaR alpha
-    static constexpr int D7 = 2240;   // [16][28] eta7 (boxed nonleaf nodes)
-    static constexpr int LP = 2688;   // [16][20] x of p at the leaves (deepest tier)
-    static constexpr int D11 = 3008;  // [16][20] eta11
-    static constexpr int D14 = 3328;  // [16][20] eta14 (boxed leaves)
-    static constexpr int LS = 3648;   // [16][4]  eta12, eta13, s of z+ / p
-    static constexpr int N = 3712;
+    static constexpr int D7 = 2432;   // [16][28] eta7 (boxed nonleaf nodes)
+    static constexpr int LP = 2880;   // [16][20] x of p at the leaves (deepest tier)
+    static constexpr int D11 = 3200;  // [16][20] eta11
+    static constexpr int D14 = 3520;  // [16][20] eta14 (boxed leaves)
+    static constexpr int LS = 3840;   // [16][4]  eta12, eta13, s of z+ / p
+    static constexpr int N = 3904;
     // after barrier A2 (k_drc cp_phase): the families' box seeds of the (d - eta+) and xi2 streams
     // over the dead eta3 / eta4 rows ([16][28] each), the xi2 stream's L^T over the child scalars
     static constexpr int SDW = D3, SDC = D3 + 448;
+    static_assert(SDC + 448 <= SC && 448 <= SCS * 32, "reuse of the dead child rows");
 };
 static_assert(Cpa::N == kDrcCpa, "CP operand region");
 // scratch in the table slots once the forward sweep is done (doubles from the first slot; slot
@@ -447,17 +452,17 @@ __device__ __forceinline__ void cpa_issue(const DrcArg& a, const DrPlan& pl, con
             const int q = e - Cpa::PU, r = q / NU;
             if (r < 15) s0 = pz + pl.U0 + (size_t)gnode(R0, r) * NU + (q - r * NU);
         } else if (e < Cpa::D4) {
-            const int q = e - Cpa::D3, r = q / NX;
-            if (r < 30) s0 = dd + a.E3 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NX + (q - r * NX);
+            const int q = e - Cpa::D3, r = q / Cpa::D3S, c = q - r * Cpa::D3S;
+            if (r < 30 && c < NX) s0 = dd + a.E3 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NX + c;
         } else if (e < Cpa::SC) {
-            const int q = e - Cpa::D4, r = q / NU;
-            if (r < 30) s0 = dd + a.E4 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NU + (q - r * NU);
+            const int q = e - Cpa::D4, r = q / Cpa::D4S, c = q - r * Cpa::D4S;
+            if (r < 30 && c < NU) s0 = dd + a.E4 + 1 + (size_t)(gnode(R0, r + 1) - 1) * NU + c;
         } else if (e < Cpa::PS) {
             // child scalars (Cpa::SC): eta5, eta6 | tau z+, p | a nonleaf child's s z+, p | eta2,
             // cond k=0 | cond k=1, y0 z+ | y1 z+, y4 z+ | y0 p, y1 p | y4 p, -
             pair = false;
-            const int q = e - Cpa::SC, r = q >> 4, c = q & 15;
-            if (r < 30) {
+            const int q = e - Cpa::SC, r = q / Cpa::SCS, c = q - r * Cpa::SCS;
+            if (r < 30 && c < 16) {
                 const int j = gnode(R0, r + 1);
                 const bool nl = !(deepest && r + 1 >= 15);
                 switch (c) {
@@ -782,7 +787,7 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
         // family's phase 1, k_cp6's arithmetic)
         const int k = h, cl = 2 * lq + 1 + (h & 1);
         if (live && h < C && !(deepest && cl >= 15)) {
-            const ldsd* sc = A + Cpa::SC + (cl - 1) * 16;
+            const ldsd* sc = A + Cpa::SC + (cl - 1) * Cpa::SCS;
             const T csz = sc[4], csp = sc[5], cdj = sc[6];
             const T ccp[C] = {sc[7], sc[8]}, czy[C + 1] = {sc[9], sc[10], sc[11]}, cpy[C + 1] = {sc[12], sc[13], sc[14]};
             T ba = T(0), bb2 = T(0);
@@ -827,9 +832,9 @@ __device__ __forceinline__ void cp_phase(const DrcArg& a, const Bufs& bf, double
             }
         }
         T d3[RX][4], d4[RU][4];
-        ld_lr<NX>(A + Cpa::D3 + (cl - 1) * NX, live, d3);
-        ld_lr<NU>(A + Cpa::D4 + (cl - 1) * NU, live, d4);
-        const ldsd* sc = A + Cpa::SC + (cl - 1) * 16;
+        ld_lr<NX>(A + Cpa::D3 + (cl - 1) * Cpa::D3S, live, d3);
+        ld_lr<NU>(A + Cpa::D4 + (cl - 1) * Cpa::D4S, live, d4);
+        const ldsd* sc = A + Cpa::SC + (cl - 1) * Cpa::SCS;
         const T d5 = live ? sc[0] : T(0), d6 = live ? sc[1] : T(0), tz = live ? sc[2] : T(0), tp = live ? sc[3] : T(0);
         lds_sync();  // A2
         dstamp(6);
