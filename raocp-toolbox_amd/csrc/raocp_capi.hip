@@ -73,6 +73,9 @@ struct raocp_ctx {
     int cp6_grid = 0;
     raocp::Cp3Tasks cp5_tk{};    // k_cp5_fam's / k_cp6's task list (every parent, leaf parents first)
     int cp5_gl = 0, cp5_gf = 0;  // grids of the two launches
+    raocp::Cp3Tasks cp5_et{};    // k_cp5_leaf's eta2 tasks (nonleaf ranges, 64 nodes per task)
+    raocp::Cp3Tasks cp5_tkb{};   // a shard's second k_cp5 launch: the cut's parents, after X1
+    int cp5_gfb = 0;             // ... its grid
     bool cp5_lpf = false;        // k_cp5_leaf's form (RAOCP_CP5_LPF, raocp_cp5.h)
     int cp3_grid = 0;            // workgroups of the (first) k_cp3 launch
     int cp3_mL = 0;              // first parent whose children are leaves (stage N - 1)
@@ -1129,7 +1132,7 @@ bool cp3_sizes(bool f32, int nx, int nu) {
 // the tiles, or -1 when the nonempty ranges exceed the kernel argument's kCp3MaxR slots (the
 // caller must not launch it: a dropped range would leave its parents uncomputed)
 long cp3_tasks(raocp::Cp3Tasks& tk, const std::vector<std::pair<int, int>>& ranges, int l0, int l1, int split,
-               int mL) {
+               int mL, int gran = 16) {
     tk = raocp::Cp3Tasks{};
     tk.l0 = l0;
     tk.l1 = std::max(l0, l1);
@@ -1141,7 +1144,7 @@ long cp3_tasks(raocp::Cp3Tasks& tk, const std::vector<std::pair<int, int>>& rang
         if (tk.nr >= raocp::kCp3MaxR) return -1;
         tk.lo[tk.nr] = r.first;
         tk.hi[tk.nr] = r.second;
-        tk.t0[tk.nr + 1] = tk.t0[tk.nr] + (r.second - r.first + 15) / 16;
+        tk.t0[tk.nr + 1] = tk.t0[tk.nr] + (r.second - r.first + gran - 1) / gran;
         ++tk.nr;
     }
     if (tk.nr == 0) {  // an empty launch still needs one range (no tiles)
@@ -1192,9 +1195,17 @@ void launch_cp3(raocp_ctx* c, int part = 0) {
         raocp::cp6_launch(c->dev, c->ctl, c->bufs, c->redpart, c->box_mode, c->cp5_tk, c->cp6_grid, c->cp3img, c->stream);
         return;
     }
-    if (c->cp5 && c->sh_S == 0) {
-        raocp::cp5_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->m, c->n, c->cp5_gl, c->cp5_tk,
-                          c->cp5_gf, c->cp3img, c->cp5_lpf, c->stream);
+    if (c->cp5) {
+        // a shard: its eta2 tasks, leaves and families, then (part 1, after X1) the cut's parents
+        const bool sh = c->sh_S > 0;
+        if (part == 0)
+            raocp::cp5_launch(c->dev, c->ctl, c->bufs, c->redpart, c->unif_C, c->box_mode, c->cp5_et,
+                              sh ? c->own_lo[c->N] : c->m, sh ? c->own_hi[c->N] : c->n, c->cp5_gl, c->cp5_tk, c->cp5_gf,
+                              c->cp3img, c->cp5_lpf, c->stream);
+        else
+            raocp::cp5_launch(c->dev, c->ctl, c->bufs, c->redpart + (size_t)raocp::cp5_rows(c->cp5_gl, c->cp5_gf) * 6,
+                              c->unif_C, c->box_mode, c->cp5_et, 0, 0, 0, c->cp5_tkb, c->cp5_gfb, c->cp3img, c->cp5_lpf,
+                              c->stream);
         return;
     }
     if (c->cp4 && c->sh_S == 0) {
@@ -1294,24 +1305,37 @@ void shard_unpack_x2(raocp_ctx* c) {
         raocp::k_scatter_rows<double><<<g, kBlock, 0, c->stream>>>(c->x2_recv, x2_q(c), c->d_slc, c->sh_R, c->x_max,
                                                                     x2_row(c));
 }
-// X1 carries the roots' (eta+, xi2) eta2 entries and the previous iteration's residual record
+// X1 carries two entries per root and the previous iteration's residual record: under k_cp3
+// the roots' (eta+, xi2) eta2 entries, under k_cp5 the roots' s of the half step before their
+// parents' kernel projection (k_cp5_leaf's eta2 tasks write it, the cut's parents' family tiles
+// read it) and eta+ of their eta2
 int x1_len(const raocp_ctx* c) { return 2 * c->x_max + 16; }
+struct X1Src {
+    double *a, *b;  // buffers (of the context's type) and element offsets of root 0's entries
+    int oa, ob;
+};
+X1Src x1_src(const raocp_ctx* c) {
+    if (c->cp5) return X1Src{c->bufs.z2, c->bufs.e1, c->dev.S0, c->dev.E2};
+    return X1Src{c->bufs.e1, c->XI2, c->dev.E2, c->dev.E2};
+}
 void shard_pack_x1(raocp_ctx* c) {
-    const int g = std::max(1, cdiv(c->own_cnt, kBlock)), o = c->dev.E2 + c->own_first;
+    const int g = std::max(1, cdiv(c->own_cnt, kBlock)), o = c->own_first;
+    const X1Src x = x1_src(c);
     if (c->f32)
-        raocp::k_pack_x1<float><<<g, kBlock, 0, c->stream>>>(c->x1_send, (const float*)c->bufs.e1 + o, (const float*)c->XI2 + o,
-                                                             c->own_cnt, c->x_max, c->red8);
+        raocp::k_pack_x1<float><<<g, kBlock, 0, c->stream>>>(c->x1_send, (const float*)x.a + x.oa + o,
+                                                             (const float*)x.b + x.ob + o, c->own_cnt, c->x_max, c->red8);
     else
-        raocp::k_pack_x1<double><<<g, kBlock, 0, c->stream>>>(c->x1_send, c->bufs.e1 + o, c->XI2 + o, c->own_cnt, c->x_max,
-                                                              c->red8);
+        raocp::k_pack_x1<double><<<g, kBlock, 0, c->stream>>>(c->x1_send, x.a + x.oa + o, x.b + x.ob + o, c->own_cnt,
+                                                              c->x_max, c->red8);
 }
 void shard_unpack_x1(raocp_ctx* c) {
-    const int g = std::max(1, cdiv(c->sh_R * c->x_max, kBlock)), o = c->dev.E2;
+    const int g = std::max(1, cdiv(c->sh_R * c->x_max, kBlock));
+    const X1Src x = x1_src(c);
     if (c->f32)
-        raocp::k_unpack_x1<float><<<g, kBlock, 0, c->stream>>>(c->x1_recv, (float*)c->bufs.e1 + o, (float*)c->XI2 + o,
-                                                               c->d_slc, c->sh_R, c->x_max);
+        raocp::k_unpack_x1<float><<<g, kBlock, 0, c->stream>>>(c->x1_recv, (float*)x.a + x.oa, (float*)x.b + x.ob, c->d_slc,
+                                                               c->sh_R, c->x_max);
     else
-        raocp::k_unpack_x1<double><<<g, kBlock, 0, c->stream>>>(c->x1_recv, c->bufs.e1 + o, c->XI2 + o, c->d_slc, c->sh_R,
+        raocp::k_unpack_x1<double><<<g, kBlock, 0, c->stream>>>(c->x1_recv, x.a + x.oa, x.b + x.ob, c->d_slc, c->sh_R,
                                                                 c->x_max);
     raocp::k_cp_check_gather<<<1, 64, 0, c->stream>>>(c->ctl, c->hist, c->x1_recv, c->sh_R, c->x_max);
 }
@@ -1461,11 +1485,11 @@ std::string kernel_name(const raocp_ctx* c, int op) {
         case 11:  // the CP loop's fused launch (dynamics projection + CP iteration), if any
             return c->drc && c->sh_S == 0 ? raocp::drc_name() : "";
         case 12:  // the forms of the k_cp5 launches, when they run ("" otherwise)
-            if (!(c->cp5 && c->sh_S == 0)) return "";
+            if (!c->cp5) return "";
             return std::string("leaf_pf=") + (c->cp5_lpf ? "1" : "0");
         case 10:
             if (c->cp6 && c->sh_S == 0) return raocp::cp6_name();
-            if (c->cp5 && c->sh_S == 0) return raocp::cp5_name(c->f32, c->nx);
+            if (c->cp5) return std::string(raocp::cp5_name(c->f32, c->nx)) + (c->sh_S > 0 ? " (+ fams x1 after X1)" : "");
             if (c->cp4 && c->sh_S == 0) return raocp::cp4_name(c->f32, c->nx, c->nu);
             if (c->cp3) return "k_cp3<" + T + ", " + nn + (c->sh_S > 0 ? ", true> x2" : ", false>");
             return kernel_name(c, 2) + " + " + kernel_name(c, 6);
@@ -2883,7 +2907,8 @@ int raocp_ctx_create(const raocp_tree_desc* t, const raocp_problem_desc* pr, int
                 // RAOCP_CP5_LPF gets its own)
                 c->cp5_lpf = raocp::cp5_leaf_pf_default(c->f32);
                 if (const char* e = getenv("RAOCP_CP5_LPF")) c->cp5_lpf = atoi(e) != 0;
-                c->cp5_gl = raocp::cp5_leaf_grid(m, n, c->cp5_lpf);
+                cp3_tasks(c->cp5_et, {{0, m}}, 0, 0, 1, 0, 64);
+                c->cp5_gl = raocp::cp5_leaf_grid(c->cp5_et, m, n, c->cp5_lpf);
                 // k_cp5_fams (profiles/r05/cp_time_fams*.log: config 4 100.7 -> 90.9 us, config 5
                 // 335.3 -> 334.8 us, config 3 60.9 -> 57.4 us with the compacted slot sums)
                 c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk);
@@ -3522,6 +3547,30 @@ int raocp_shard_setup(raocp_ctx* c, int nranks, int rank) {
         c->cp3_grid = cp3_grid_of(ta);
         c->cp3_gridb = cp3_grid_of(tb);
         c->cp_rows = c->cp3_grid + c->cp3_gridb;
+        if (c->cp_rows > c->red_rows) {
+            c->red_rows = c->cp_rows;
+            if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return rc;
+        }
+        HIPCHK(hipMemset(c->redpart, 0, (size_t)c->red_rows * 6 * sizeof(double)));
+    }
+    if (c->cp5) {
+        // k_cp5 in two launch pairs: the eta2 tasks of the replicated top and the owned stages,
+        // the owned leaves, and the owned families plus the top above the cut's parents; after
+        // X1 (the roots' s of the half step) the cut's parents' family tiles alone
+        std::vector<std::pair<int, int>> er{{0, c->stage_ptr[S]}};
+        for (int t = S; t < N; ++t) er.push_back({c->own_lo[t], c->own_hi[t]});
+        std::vector<std::pair<int, int>> ra;
+        if (N - 1 >= S) ra.push_back({c->own_lo[N - 1], c->own_hi[N - 1]});
+        for (int t = S; t < N - 1; ++t) ra.push_back({c->own_lo[t], c->own_hi[t]});
+        if (S >= 2) ra.push_back({0, c->stage_ptr[S - 1]});
+        if (cp3_tasks(c->cp5_et, er, 0, 0, 1, 0, 64) < 0 || cp3_tasks(c->cp5_tk, ra, 0, 0, 1, c->cp3_mL) < 0 ||
+            cp3_tasks(c->cp5_tkb, {{c->stage_ptr[S - 1], c->stage_ptr[S]}}, 0, 0, 1, c->cp3_mL) < 0)
+            return fail(RAOCP_ERR_ARG, "shard's k_cp5 task lists exceed their " + std::to_string(raocp::kCp3MaxR) +
+                                           " range slots (too many stages below the cut)");
+        c->cp5_gl = raocp::cp5_leaf_grid(c->cp5_et, c->own_lo[N], c->own_hi[N], c->cp5_lpf);
+        c->cp5_gf = raocp::cp5_fam_grid(c->cp5_tk);
+        c->cp5_gfb = raocp::cp5_fam_grid(c->cp5_tkb);
+        c->cp_rows = raocp::cp5_rows(c->cp5_gl, c->cp5_gf) + c->cp5_gfb;
         if (c->cp_rows > c->red_rows) {
             c->red_rows = c->cp_rows;
             if ((rc = c->alloc(&c->redpart, (size_t)c->red_rows * 6))) return rc;

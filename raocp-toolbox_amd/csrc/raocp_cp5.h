@@ -16,18 +16,18 @@ const char* cp5_name(bool f32, int nx);
 // tile's operands in flight (register double buffering), 0 = two waves per SIMD, a tile's
 // operands at its start and one L^T stream at a time; the default of the context's type
 bool cp5_leaf_pf_default(bool f32);
-// grids of the two launches for the leaves [l0, l1) (lpf: the leaf launch's form) and the family
-// task list tk
-int cp5_leaf_grid(int l0, int l1, bool lpf);
+// grids of the two launches for the eta2 tasks et (Cp3Tasks ranges of nonleaf nodes, 64 per task),
+// the leaves [l0, l1) (lpf: the leaf launch's form) and the family task list tk
+int cp5_leaf_grid(const Cp3Tasks& et, int l0, int l1, bool lpf);
 int cp5_fam_grid(const Cp3Tasks& tk);
 // rows of residual partials the two launches write (one per workgroup; the family launch's
 // rows after the leaf launch's gl)
 int cp5_rows(int gl, int gf);
-// the two launches on stream s: leaves [l0, l1) (residual partials in rows [0, gl) of part),
-// then the families of tk (the rows after them, cp5_rows); img is k_cp3's weight image
-// ([sqrtQ | sqrtR | sqrtPf] fragments); lpf: the leaf launch's form. hipGetLastError() after it
-// is the caller's.
-void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, int l0, int l1, int gl,
+// the two launches on stream s: the eta2 tasks et and the leaves [l0, l1) (residual partials in
+// rows [0, gl) of part; gl = 0: no leaf launch, a shard's second CP launch), then the families
+// of tk (the rows after them, cp5_rows); img is k_cp3's weight image ([sqrtQ | sqrtR | sqrtPf]
+// fragments); lpf: the leaf launch's form. hipGetLastError() after it is the caller's.
+void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, const Cp3Tasks& et, int l0, int l1, int gl,
                 const Cp3Tasks& tk, int gf, const double* img, bool lpf, hipStream_t s);
 
 // k_cp6 (raocp_cp5.hip): the small trees' fused CP iteration, one family tile per workgroup of

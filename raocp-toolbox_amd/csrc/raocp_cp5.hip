@@ -60,12 +60,13 @@ struct LeafOps {
     }
 };
 
-// Tasks of a wave (grid-stride over the waves): the eta2 tasks of nonleaf nodes [0, m) (64 per
-// task, lane = node), then the leaf tiles of [l0, l1) (16 per tile), each tile's loads issued
-// before the previous tile's arithmetic.
+// Tasks of a wave (grid-stride over the waves): the eta2 tasks of the nonleaf ranges of et (64
+// per task, lane = node; unsharded [0, m), a shard its own stages and the replicated top), then
+// the leaf tiles of [l0, l1) (16 per tile), each tile's loads issued before the previous tile's
+// arithmetic.
 template <class T, int NX, int C, int BXL, bool LPF>
-__global__ void __launch_bounds__(256, LPF ? 1 : 2) k_cp5_leaf(Dev p, Ctl* ctl, Bufs bf, double* __restrict__ part, int l0,
-                                                     int l1, const double* __restrict__ img) {
+__global__ void __launch_bounds__(256, LPF ? 1 : 2) k_cp5_leaf(Dev p, Ctl* ctl, Bufs bf, double* __restrict__ part, Cp3Tasks et,
+                                                     int l0, int l1, const double* __restrict__ img) {
     typedef typename MF<T>::v4 v4;
     constexpr int RX = (NX + 15) / 16, G = 2 * C + 1;
     typedef WL<T, NX, NX> WP;
@@ -82,7 +83,7 @@ __global__ void __launch_bounds__(256, LPF ? 1 : 2) k_cp5_leaf(Dev p, Ctl* ctl, 
     cglbp<T> cond = (cglbp<T>)p.cond;
     typedef __attribute__((address_space(3))) T lT;
     lT* bl_ = (lT*)blds_;
-    const int nL = (l1 - l0 + 15) >> 4, nE = (l0 + 63) >> 6;  // leaf tiles, eta2 tasks (nonleaf [0, l0 = m))
+    const int nL = (l1 - l0 + 15) >> 4, nE = et.t0[et.nr];  // leaf tiles, eta2 tasks
     // the first leaf tile's operands, in flight during the prologue and the eta2 tasks
     LeafOps<T, NX, BXL> cur;
     if (LPF) cur.load(p, zp, pz, d, l0 + 16 * gw + lo, gw < nL && l0 + 16 * gw + lo < l1);
@@ -103,8 +104,10 @@ __global__ void __launch_bounds__(256, LPF ? 1 : 2) k_cp5_leaf(Dev p, Ctl* ctl, 
     bool nanf = false;  // a NaN reached a box (Rectangle._constrain raises)
     // ---- (a) eta2 of the nonleaf nodes (cache.py:321-372; raocp_cp3.hip phase 1)
     for (int t = gw; t < nE; t += nwv) {
-        const int j = 64 * t + lane;
-        const bool live = j < l0;
+        int r = 0;
+        while (r + 1 < et.nr && t >= et.t0[r + 1]) ++r;
+        const int j = et.lo[r] + 64 * (t - et.t0[r]) + lane;
+        const bool live = j < et.hi[r];
         const int jq = live ? j : 0, yj = G * jq;
         T cp[C], zy[C], py[C];
         _Pragma("unroll") for (int k = 0; k < C; ++k) {
@@ -1091,16 +1094,16 @@ int resident_grid(long tasks, int per) {
 
 
 template <class T, int NX, int NU, int C>
-void launch_t(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, int l0, int l1, int gl, const Cp3Tasks& tk, int gf,
-              const double* img, bool lpf, hipStream_t s) {
+void launch_t(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, const Cp3Tasks& et, int l0, int l1, int gl,
+              const Cp3Tasks& tk, int gf, const double* img, bool lpf, hipStream_t s) {
     // the sqrtPf fragments follow [sqrtQ | sqrtR] in the image (16-B aligned: N multiples of 64)
     const double* imp = img + (size_t)(WL<T, NX, NX>::N + WL<T, NU, NU>::N) * sizeof(T) / 8;
-    if (lpf) {
-        if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-        else k_cp5_leaf<T, NX, C, 2, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-    } else {
-        if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
-        else k_cp5_leaf<T, NX, C, 2, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, l0, l1, imp);
+    if (gl > 0 && lpf) {
+        if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, et, l0, l1, imp);
+        else k_cp5_leaf<T, NX, C, 2, true><<<gl, 256, 0, s>>>(p, ctl, bf, part, et, l0, l1, imp);
+    } else if (gl > 0) {
+        if ((bx & 3) == 1) k_cp5_leaf<T, NX, C, 1, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, et, l0, l1, imp);
+        else k_cp5_leaf<T, NX, C, 2, false><<<gl, 256, 0, s>>>(p, ctl, bf, part, et, l0, l1, imp);
     }
     if ((bx & 3) == 1) k_cp5_fams<T, NX, NU, C, 1><<<gf, 64 * C, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
     else k_cp5_fams<T, NX, NU, C, 2><<<gf, 64 * C, 0, s>>>(p, ctl, bf, part + (size_t)gl * 6, tk, img);
@@ -1126,8 +1129,8 @@ const char* cp5_name(bool f32, int nx) {
 // k_cp5_leaf's default form (raocp_cp5.h): 0 in fp64 (config 3 56.3 -> 53.2 us, config 4 91.3 ->
 // 89.7 us for the CP iteration), 1 in fp32 (config 5 327.8 vs 333.0 us; profiles/r05/cp_time_lpf.log)
 bool cp5_leaf_pf_default(bool f32) { return f32; }
-int cp5_leaf_grid(int l0, int l1, bool lpf) {
-    const long tasks = (long)(std::max(l1 - l0, 0) + 15) / 16 + (l0 + 63) / 64;
+int cp5_leaf_grid(const Cp3Tasks& et, int l0, int l1, bool lpf) {
+    const long tasks = (long)(std::max(l1 - l0, 0) + 15) / 16 + et.t0[et.nr];
     return (lpf ? 1 : 2) * resident_grid(tasks, 2);  // two workgroups per CU without the prefetch
 }
 // rows of residual partials of the two launches (one per workgroup)
@@ -1151,11 +1154,11 @@ void cp6_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int bx, const Cp3
     if ((bx & 3) == 1) k_cp6<double, 20, 8, 2, 1, 1><<<grid, 256, 0, s>>>(p, ctl, bf, part, tk, img);
     else k_cp6<double, 20, 8, 2, 2, 2><<<grid, 256, 0, s>>>(p, ctl, bf, part, tk, img);
 }
-void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, int l0, int l1, int gl,
+void cp5_launch(const Dev& p, Ctl* ctl, Bufs bf, double* part, int C, int bx, const Cp3Tasks& et, int l0, int l1, int gl,
                 const Cp3Tasks& tk, int gf, const double* img, bool lpf, hipStream_t s) {
-    if (p.nx == 20) launch_t<double, 20, 8, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, lpf, s);
-    else if (p.nx == 32) launch_t<double, 32, 12, 3>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, lpf, s);
-    else launch_t<float, 64, 16, 4>(p, ctl, bf, part, bx, l0, l1, gl, tk, gf, img, lpf, s);
+    if (p.nx == 20) launch_t<double, 20, 8, 4>(p, ctl, bf, part, bx, et, l0, l1, gl, tk, gf, img, lpf, s);
+    else if (p.nx == 32) launch_t<double, 32, 12, 3>(p, ctl, bf, part, bx, et, l0, l1, gl, tk, gf, img, lpf, s);
+    else launch_t<float, 64, 16, 4>(p, ctl, bf, part, bx, et, l0, l1, gl, tk, gf, img, lpf, s);
     (void)C;
 }
 

@@ -197,3 +197,38 @@ def test_fp32_sharded_config5_matches_unsharded(R, kern):
     other = _kern_cache(prob, "two" if kern == "fused" else "fused", "float32")
     stf, errf, _ = other.native.cp_run(r["x0"], iters, 0.0, alpha)
     assert stf == st0 and np.max(np.abs(errf - err0) / np.abs(err0)) <= 1e-4
+
+
+@pytest.mark.parametrize("R", [2, 4, 8])
+@pytest.mark.parametrize("cfg,dtype", [(4, "float64"), (5, "float32")])
+def test_sharded_default_kernels_match_unsharded(cfg, dtype, R):
+    """The shipped CP kernels on the sharded path (BASELINE configs[3] fp64, configs[4] fp32):
+    k_cp5 with no pins on either side. A shard runs k_cp5_leaf's eta2 tasks over the
+    replicated top and its own stages, its own leaves, and its own families plus the top above
+    the cut's parents; X1 delivers the roots' s of the half step, then the cut's parents'
+    family tiles run alone. Residual histories and the owned iterate equal the unsharded
+    default solve bit for bit (only max reductions are regrouped)."""
+    r = recipe_config(cfg, seed=0)
+    tree, prob = build_problem(r)
+    base = core.Cache(prob, dtype=dtype)
+    assert base.native.kernel_info(10).startswith("k_cp5_leaf")
+    alpha = 0.999 / base.native.step_size(rtol=1e-7 if dtype == "float32" else 1e-14)
+    iters = 12 if cfg == 4 else 6
+    st0, err0, derr0 = base.native.cp_run(r["x0"], iters, 0.0, alpha)
+    z0 = base.get_primal_flat()
+    shards = [core.Cache(prob, dtype=dtype) for _ in range(R)]
+    for k, s in enumerate(shards):
+        s.native.shard(k, R)
+        assert s.native.kernel_info(10).startswith("k_cp5_leaf")
+    st, err, derr = group_cp_run([s.native for s in shards], r["x0"], iters, 0.0, alpha)
+    assert st == st0 and err.shape == err0.shape == (iters + 1, 3)
+    assert np.array_equal(err, err0) and np.array_equal(derr, derr0)
+    nx = base.packed.nx
+    covered = np.zeros(tree.num_nodes, dtype=bool)
+    for s in shards:
+        z = s.get_primal_flat()
+        for (a, b) in _owned_x_slices(s.native):
+            if b > a:
+                np.testing.assert_array_equal(z[a * nx:b * nx], z0[a * nx:b * nx])
+                covered[a:b] = True
+    assert covered.all()
