@@ -455,6 +455,13 @@ struct Dyn2Op {
 // test in an extra workgroup of the first launch (defer_check)
 // part: 0 the whole projection; 1 (a shard) the backward stages below its cut, on its owned
 // parents; 2 the replicated top backward, then every forward stage (owned below the cut)
+// the stages k_dy3_top_back / k_dy3_top_fwd run in one workgroup: a shard merges only stages of
+// its replicated top (t < sh_S, run after X2), at least two of them
+int dyn3_top_stages(const raocp_ctx* c) {
+    if (c->sh_S == 0) return c->d3ts;
+    const int ts = std::min(c->d3ts, c->sh_S);
+    return ts >= 2 ? ts : 0;
+}
 template <class T, int NX, int NU>
 void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck, int part) {
     typedef raocp::Dy3Lds<T, NX, NU> L;
@@ -491,8 +498,8 @@ void launch_dyn3t(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* 
     auto threads = [&](int t) { return coop(t) ? thr : thr_w; };
     const int N = c->N, S = c->sh_S;  // S > 0: a shard owns the stages >= S partly
     auto stage = [&](int t) -> const raocp::Dy3Stage& { return S > 0 && t >= S ? c->d3own[t] : c->d3st[t]; };
-    // the top stages t < ts in one workgroup per direction (unsharded contexts, dyn3_top_stages)
-    const int ts = S == 0 ? c->d3ts : 0;
+    // the top stages t < ts in one workgroup per direction (dyn3_top_stages)
+    const int ts = dyn3_top_stages(c);
     raocp::Dy3Top tp{};
     tp.ts = ts;
     for (int t = 0; t < ts; ++t) tp.st[t] = c->d3st[t];
@@ -1461,7 +1468,7 @@ std::string kernel_name(const raocp_ctx* c, int op) {
             if (c->dr && c->sh_S == 0) {
                 return std::string(raocp::dr_name(c->nx, c->nu)) + " x1";
             } else if (c->dyn3) {  // a backward and a forward launch per nonleaf stage below the top
-                const int ts = c->sh_S == 0 ? c->d3ts : 0;
+                const int ts = dyn3_top_stages(c);
                 for (int t = ts; t < c->N; ++t) add("k_dy3_back<" + T + ", " + nn + ">");
                 if (ts) add("k_dy3_top_back<" + T + ", " + nn + ">");
                 if (ts) add("k_dy3_top_fwd<" + T + ", " + nn + ">");

@@ -206,7 +206,8 @@ def test_sharded_default_kernels_match_unsharded(cfg, dtype, R):
     k_cp5 with no pins on either side. A shard runs k_cp5_leaf's eta2 tasks over the
     replicated top and its own stages, its own leaves, and its own families plus the top above
     the cut's parents; X1 delivers the roots' s of the half step, then the cut's parents'
-    family tiles run alone. Residual histories and the owned iterate equal the unsharded
+    family tiles run alone. The dynamics run k_dy3 with its merged top (k_dy3_top_back / _fwd)
+    over the replicated stages above the cut, as the unsharded default does. Residual histories and the owned iterate equal the unsharded
     default solve bit for bit (only max reductions are regrouped)."""
     r = recipe_config(cfg, seed=0)
     tree, prob = build_problem(r)
@@ -220,6 +221,7 @@ def test_sharded_default_kernels_match_unsharded(cfg, dtype, R):
     for k, s in enumerate(shards):
         s.native.shard(k, R)
         assert s.native.kernel_info(10).startswith("k_cp5_leaf")
+        assert "k_dy3_top_back" in s.native.kernel_info(9)  # the merged top over the replicated stages
     st, err, derr = group_cp_run([s.native for s in shards], r["x0"], iters, 0.0, alpha)
     assert st == st0 and err.shape == err0.shape == (iters + 1, 3)
     assert np.array_equal(err, err0) and np.array_equal(derr, derr0)

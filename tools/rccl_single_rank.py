@@ -31,3 +31,24 @@ for cp3 in ("0", "1"):
     ms1 = sh.native.cp_bench(r["x0"], 480, alpha)
     print(f"RCCL single-rank shard path OK ({base.native.kernel_info(10)}): traces bit-identical; "
           f"{480 / ms0 * 1e3:.0f} it/s unsharded, {480 / ms1 * 1e3:.0f} it/s through the shard exchange path")
+# the shipped kernels at config 4 (BASELINE configs[3], the sharded bench leg's tree): k_cp5 and
+# k_dy3 with its merged top, no pins on either side
+for k in ("RAOCP_DR", "RAOCP_CP4", "RAOCP_CP6", "RAOCP_CP3"):
+    os.environ.pop(k, None)
+r = recipe_config(4)
+tree, prob = build_problem(r)
+base = core.Cache(prob)
+alpha = 0.999 / base.native.step_size()
+st0, e0, d0 = base.native.cp_run(r["x0"], 24, 0.0, alpha)
+sh = core.Cache(prob)
+sh.native.shard(0, 1)
+sh.native.comm_init(comm_unique_id(), 0, 1)
+assert sh.native.kernel_info(10).startswith("k_cp5_leaf"), sh.native.kernel_info(10)
+st1, e1, d1 = sh.native.cp_run(r["x0"], 24, 0.0, alpha)
+assert st0 == st1 and np.array_equal(e0, e1) and np.array_equal(d0, d1), (np.max(np.abs(e0 - e1)))
+assert np.array_equal(base.get_primal_flat(), sh.get_primal_flat())
+ms0 = base.native.cp_bench(r["x0"], 240, alpha)
+ms1 = sh.native.cp_bench(r["x0"], 240, alpha)
+print(f"RCCL single-rank shard path OK at config 4 ({sh.native.kernel_info(10)}; {sh.native.kernel_info(9)}): "
+      f"traces bit-identical; {240 / ms0 * 1e3:.0f} it/s unsharded, {240 / ms1 * 1e3:.0f} it/s through the shard "
+      f"exchange path")
