@@ -23,7 +23,8 @@ script starts the N rank processes itself before anything touches a GPU.
       ONE config-5 tree (configs[4]: branching 4, N = 9, 349,525 nodes, nx = 64, nu = 16,
       fp32) whose subtrees below the replicated top are sharded across the N GPUs
       (SURVEY.md 8(e)), with RCCL exchanges each iteration; CP iterations/s of that one tree
-      (N = 1 is the unsharded solve, reported from the one-GPU legs below). At N > 1 each
+      (N = 1 is the unsharded solve, reported from the one-GPU legs below; both run k_cp5 and
+      k_dy3 with its merged top, each entry names its kernels). At N > 1 each
       leg runs as N fresh child processes under a time limit, so that a failure there
       cannot take the line down.
 
@@ -330,7 +331,8 @@ def shard_leg(args):
     if rank == 0:
         lo, hi = nat.shard_owned() if world > 1 else (None, None)
         print(json.dumps({"its": args.shard_steps / wall, "wall_s": wall, "device_ms": dev_ms, "steps": args.shard_steps,
-                          "nodes": cache.packed.n, "owned_leaves_rank0": None if lo is None else int(hi[-1] - lo[-1])}),
+                          "nodes": cache.packed.n, "owned_leaves_rank0": None if lo is None else int(hi[-1] - lo[-1]),
+                          "cp_kernel": nat.kernel_info(10), "dynamics_kernels": nat.kernel_info(9)}),
               flush=True)
     if group:
         group.barrier()
@@ -362,9 +364,11 @@ def sharded_entry(args, world, cfg, dtype, steps, warmup):
     r = json.loads(line[-1])
     desc.update({"value": r["its"], "ms_per_step": 1e3 * r["wall_s"] / r["steps"], "nodes": r["nodes"],
                  "device_ms_per_step": r["device_ms"] / r["steps"],
+                 "cp_kernel": r.get("cp_kernel"), "dynamics_kernels": r.get("dynamics_kernels"),
                  "exchanges": "per iteration: all-gather of the boundary roots' q rows (dynamics), all-gather of "
-                              "their eta+ / xi2 eta2 entries together with the previous iteration's residual record "
-                              "(the stopping test runs one iteration late, so the residual reduction rides on it)"
+                              "two entries per root (k_cp5: s of the half step and eta+ of eta2) together with the "
+                              "previous iteration's residual record (the stopping test runs one iteration late, so "
+                              "the residual reduction rides on it)"
                               if world > 1 else None})
     return desc
 
@@ -440,7 +444,8 @@ def config_leg(cfg, dtype, steps, warmup, reps, nsets):
            "dtype": "f32" if w == 4 else "f64", "nodes": pk.n,
            "cp": {"value": steps / wall, "unit": "it/s", "steps": steps, "ms_per_step": 1e3 * wall / steps,
                   "device_ms_per_step": dev_ms / steps},
-           "kernels": kernels, "roofline": roofline}
+           "kernels": kernels, "roofline": roofline,
+           "cp_kernel": nat.kernel_info(10), "dynamics_kernels": nat.kernel_info(9)}
     if nsets:
         leg["l_sweep"] = op_pair(nat, c, w, max(10, reps // 2), nsets)
     del c
@@ -546,7 +551,8 @@ def main():
                                       "unsharded on 1 GPU (the N = 1 point of the strong-scaling leg)",
                             "dtype": leg["dtype"], "n_gpus": 1, "steps": steps, "unit": "it/s", "scaling": "strong",
                             "value": leg["cp"]["value"], "ms_per_step": leg["cp"]["ms_per_step"],
-                            "device_ms_per_step": leg["cp"]["device_ms_per_step"], "nodes": leg["nodes"]}
+                            "device_ms_per_step": leg["cp"]["device_ms_per_step"], "nodes": leg["nodes"],
+                            "cp_kernel": leg.get("cp_kernel"), "dynamics_kernels": leg.get("dynamics_kernels")}
         out["sharded"] = sharded
     if not args.no_cpu and world == 1:
         out["cpu_baseline"] = cpu_baseline(recipe, args.cpu_seconds)
