@@ -548,7 +548,8 @@ bool dyn3_lds_fits(bool f32, int nx, int nu, int C) {
     size_t b = ~(size_t)0;
     if (nx == 20 && nu == 8) b = f32 ? dyn3_lds<float, 20, 8>(C) : dyn3_lds<double, 20, 8>(C);
     else if (nx == 32 && nu == 12) b = f32 ? dyn3_lds<float, 32, 12>(C) : dyn3_lds<double, 32, 12>(C);
-    else if (nx == 64 && nu == 16) b = f32 ? dyn3_lds<float, 64, 16>(C) : dyn3_lds<double, 64, 16>(C);
+    else if (nx == 64 && nu == 16 && f32) b = dyn3_lds<float, 64, 16>(C);
+    // (fp64 at nx = 64: the tables exceed the LDS, so k_dy3 has no such instantiation)
     return b <= 160 * 1024;
 }
 // the per-stage table images of the sweep, laid out once (k_dy3_image, one workgroup per stage)
@@ -592,7 +593,7 @@ int dyn3_images(raocp_ctx* c) {
     }
     if (c->nx == 20) return dyn3_imagest<double, 20, 8>(c);
     if (c->nx == 32) return dyn3_imagest<double, 32, 12>(c);
-    return dyn3_imagest<double, 64, 16>(c);
+    return fail(RAOCP_ERR_ARG, "k_dy3 has no fp64 form at nx = 64 (dyn3_lds_fits)");
 }
 void launch_dyn3(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* ck, int part) {
     if (c->f32) {
@@ -600,9 +601,9 @@ void launch_dyn3(raocp_ctx* c, double* z, const Ctl* ctl, const raocp::ChkArg* c
         else if (c->nx == 32) launch_dyn3t<float, 32, 12>(c, z, ctl, ck, part);
         else launch_dyn3t<float, 64, 16>(c, z, ctl, ck, part);
     } else {
+        // (no fp64 nx = 64 form: dyn3_lds_fits keeps such contexts off k_dy3)
         if (c->nx == 20) launch_dyn3t<double, 20, 8>(c, z, ctl, ck, part);
         else if (c->nx == 32) launch_dyn3t<double, 32, 12>(c, z, ctl, ck, part);
-        else launch_dyn3t<double, 64, 16>(c, z, ctl, ck, part);
     }
 }
 
