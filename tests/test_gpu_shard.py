@@ -234,3 +234,27 @@ def test_sharded_default_kernels_match_unsharded(cfg, dtype, R):
                 np.testing.assert_array_equal(z[a * nx:b * nx], z0[a * nx:b * nx])
                 covered[a:b] = True
     assert covered.all()
+
+
+def test_sharded_default_kernels_stop_with_unsharded():
+    """Early stop through the sharded k_cp5 path (config 4, R = 2): the stopping test sees the
+    maxima over shards and fires at the unsharded default solve's iteration, mid-run."""
+    r = recipe_config(4, seed=0)
+    tree, prob = build_problem(r)
+    base = core.Cache(prob)
+    alpha = 0.999 / base.native.step_size()
+    _, e_full, _ = base.native.cp_run(r["x0"], 40, 0.0, alpha)
+    e = e_full.max(axis=1)
+    # a tolerance first met mid-run: the first new running minimum of the error after k = 3
+    ks = [k for k in range(4, len(e)) if e[k] < e[:k].min()]
+    if not ks:
+        pytest.skip("the config-4 trace has no new minimum after iteration 3")
+    tol = float(e[ks[0]])
+    st0, err0, derr0 = base.native.cp_run(r["x0"], 40, tol, alpha)
+    assert st0 == 0 and err0.shape[0] == ks[0] + 1
+    shards = [core.Cache(prob) for _ in range(2)]
+    for k, s in enumerate(shards):
+        s.native.shard(k, 2)
+    st, err, derr = group_cp_run([s.native for s in shards], r["x0"], 40, tol, alpha)
+    assert st == st0 and err.shape == err0.shape
+    assert np.array_equal(err, err0) and np.array_equal(derr, derr0)
